@@ -1,0 +1,139 @@
+/*
+ * psfm.h — C-ABI of the MI355X (gfx950) photometric hot path.
+ *
+ * The reference has no FFI: its hot path is the Python call chain
+ *   MultiViewPhotometricLoss.forward        packnet_sfm/losses/multiview_photometric_loss.py:331-410
+ *     warp_ref_image / view_synthesis       :131-195, geometry/camera_utils.py:27-59
+ *       Camera.reconstruct / project        geometry/camera.py:111-190
+ *       grid_sample(bilinear, zeros, align_corners=True)
+ *     calc_photometric_loss (SSIM + L1)     :199-267, SSIM :15-54
+ *     reduce_photometric_loss ('min'/'mean', automask)  :269-297, :394-399
+ *     calc_smoothness_loss                  :301-327, utils/depth.py:146-198
+ * plus its autograd backward.  Each entry point below replaces one stage of that
+ * chain (cited per function); a Python `torch.autograd.Function` drives them
+ * through ctypes.
+ *
+ * Conventions
+ *   - every pointer is DEVICE memory, fp32, NCHW contiguous unless stated; the caller
+ *     owns every buffer (no allocation inside); sizes come from psfm_workspace_floats().
+ *   - all work is enqueued on `stream`; no host synchronisation, graph-capturable.
+ *   - deterministic: no float atomics; every reduction is two-stage in a fixed order.
+ *   - return 0 on success, <0 on a bad argument, or a positive hipError_t; the
+ *     message is available from psfm_last_error() (thread-local).
+ */
+#ifndef PSFM_H
+#define PSFM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSFM_MAX_CTX 4     /* context frames per target (reference: back+forward context, default 2) */
+#define PSFM_MAX_SCALES 4  /* num_scales (default 4, configs/default_config.py:45) */
+#define PSFM_CAMREC 32     /* floats per camera record: Kinv[9] | Kref[9] | T[12] | pad[2] */
+
+enum psfm_reduce_op { PSFM_REDUCE_MIN = 0, PSFM_REDUCE_MEAN = 1 };
+
+/* Hyper-parameters of one photometric call: MultiViewPhotometricLoss.__init__ :92-118.
+ * One call processes `S` scales that share the image size H x W (the reference's
+ * upsample_depth_maps=True case has all num_scales at full resolution in ONE call;
+ * multi-resolution scales are issued as one call per scale with S=1). */
+typedef struct psfm_params {
+    int B, H, W;            /* batch and image size of this call                      */
+    int N;                  /* context frames, 1..PSFM_MAX_CTX                         */
+    int S;                  /* scales in this call, 1..PSFM_MAX_SCALES                 */
+    int scale0;             /* global index of the first scale (smoothness 1/2^i)      */
+    int n_scales;           /* n = total scales (ProgressiveScaling, loss_base.py:31)  */
+    int automask;           /* automask_loss                                          */
+    int reduce_op;          /* psfm_reduce_op                                         */
+    int l1_only;            /* ssim_loss_weight == 0 -> 3-channel L1 candidates :246  */
+    float ssim_w, C1, C2;   /* ssim_loss_weight, C1, C2                               */
+    float min_depth, max_depth;
+    float clip_loss;        /* >0: clamp each candidate map at mean+clip*std :249-253 */
+    float smooth_w;         /* smooth_loss_weight                                     */
+} psfm_params;
+
+/* Device inputs of one call. `cam` holds one record per (scale, context, batch):
+ *   cam[((s*N + j)*B + b)*PSFM_CAMREC + ...] = Kinv(3x3, row-major) of the target camera
+ *   at that scale (camera.py:72-81), Kref(3x3) of the context camera (scaled,
+ *   camera_utils.py:16-22), T = [R|t] (3x4) target->context (pose.py:39-46). */
+typedef struct psfm_inputs {
+    const float* tgt;                     /* [B,3,H,W] target image at this size           */
+    const float* ctx[PSFM_MAX_CTX];       /* N x [B,3,H,W] context images at this size     */
+    const float* sig[PSFM_MAX_SCALES];    /* S x [B,1,H,W] sigmoid depth maps               */
+    const float* cam;                     /* [S][N][B][PSFM_CAMREC]                          */
+    const float* mask;                    /* [B,1,H,W] or NULL (NULL == all ones)           */
+} psfm_inputs;
+
+/* Workspace layout (floats), all caller-allocated, sized by psfm_workspace_floats(). */
+typedef struct psfm_workspace {
+    float* photo_part;   /* [S][B*tiles]            per-tile photometric partial sums      */
+    float* smooth_part;  /* [S][B][tiles][4]        per-tile smoothness partial sums       */
+    float* clip_part;    /* [S][2N][B*tiles][2]     per-tile sum/sumsq per candidate map   */
+    float* clip_thr;     /* [S][2N]                 clip thresholds (written by finalize)  */
+    float* pose_part;    /* [S][N][B][tiles][12]    per-tile dL/dT partials                */
+    uint8_t* argmin;     /* [S][B][H][W]            selected candidate per pixel ('min')   */
+} psfm_workspace;
+
+/* number of floats (and argmin bytes) the workspace of this call needs */
+int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes);
+
+/* Clip statistics pass (only when clip_loss > 0): per-candidate-map sum / sum of squares
+ * (calc_photometric_loss :249-253), then thresholds mean + clip*std (unbiased). */
+int psfm_photometric_clip_stats(const psfm_params* p, const psfm_inputs* in,
+                                const psfm_workspace* ws, void* stream);
+
+/* K1 forward: lift -> transform -> project -> bilinear gather (view_synthesis), SSIM+L1
+ * (calc_photometric_loss), automask candidates, min/mean reduction (reduce_photometric_loss).
+ * Writes ws->photo_part and (op 'min') ws->argmin. */
+int psfm_photometric_fwd(const psfm_params* p, const psfm_inputs* in,
+                         const psfm_workspace* ws, void* stream);
+
+/* K3 forward: edge-aware smoothness partial sums (calc_smoothness, calc_smoothness_loss). */
+int psfm_smoothness_fwd(const psfm_params* p, const psfm_inputs* in,
+                        const psfm_workspace* ws, void* stream);
+
+/* Final deterministic reduction of up to PSFM_MAX_SCALES calls' partials into
+ *   out[0] = loss, out[1] = metrics['photometric_loss'], out[2] = metrics['smoothness_loss'],
+ * and per-(scale,batch) smoothness stats [n][B][4] for the backward.
+ * calls[i] / ws[i] describe the i-th call (scales calls[i]->scale0 ..+S-1). */
+int psfm_finalize(int ncalls, const psfm_params* const* calls, const psfm_workspace* const* ws,
+                  float* smooth_stats, float* out, void* stream);
+
+/* K2 backward of the photometric term: dL/dsig for the call's S scales (written, not
+ * accumulated) and per-tile dL/dT partials.  grad_out: device scalar dL/dloss. */
+int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                         const float* grad_out, float* const* grad_sig, void* stream);
+
+/* K3 backward: ADDS the smoothness gradient into grad_sig. */
+int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float* smooth_stats,
+                        const float* grad_out, float* const* grad_sig, void* stream);
+
+/* Sum the per-tile dL/dT partials of up to PSFM_MAX_SCALES calls into grad_T [N][B][12]. */
+int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
+                          const psfm_workspace* const* ws, float* grad_T, void* stream);
+
+/* Standalone view_synthesis (geometry/camera_utils.py:27-59) for one context:
+ * warped[B,3,H,W] = grid_sample(ref, project(reconstruct(depth))).  cam: [B][PSFM_CAMREC]. */
+int psfm_view_synthesis_fwd(int B, int H, int W, const float* ref, const float* depth,
+                            const float* cam, float* warped, void* stream);
+/* its backward: dL/ddepth [B,1,H,W] (written) and dL/dT partials [B][tiles][12], reduced into
+ * grad_T [B][12] */
+int psfm_view_synthesis_bwd(int B, int H, int W, const float* ref, const float* depth,
+                            const float* cam, const float* grad_warped, float* grad_depth,
+                            float* pose_part, float* grad_T, void* stream);
+
+/* tiles per image used by every kernel for H x W (for sizing pose_part of view synthesis) */
+int psfm_tiles_per_image(int H, int W);
+
+const char* psfm_last_error(void);
+const char* psfm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSFM_H */

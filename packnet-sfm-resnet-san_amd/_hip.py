@@ -1,0 +1,111 @@
+"""ctypes binding of the HIP C-ABI (include/psfm.h) — the only way the product path
+reaches the kernels.  There is deliberately NO fallback: if `libpsfm_hip.so` is missing or
+the tensors are not on a ROCm device, the call raises.
+
+The library is loaded after `torch` so that its `libamdhip64.so.7` dependency resolves to the
+HIP runtime torch already loaded (one runtime per process: device pointers and streams are
+shared with PyTorch-ROCm).
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_NAME = "libpsfm_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+MAX_CTX = 4
+MAX_SCALES = 4
+CAMREC = 32
+REDUCE_MIN, REDUCE_MEAN = 0, 1
+
+c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+
+
+class Params(ctypes.Structure):
+    """psfm_params (include/psfm.h)."""
+    _fields_ = [("B", c_int), ("H", c_int), ("W", c_int), ("N", c_int), ("S", c_int),
+                ("scale0", c_int), ("n_scales", c_int), ("automask", c_int), ("reduce_op", c_int),
+                ("l1_only", c_int), ("ssim_w", c_float), ("C1", c_float), ("C2", c_float),
+                ("min_depth", c_float), ("max_depth", c_float), ("clip_loss", c_float),
+                ("smooth_w", c_float)]
+
+
+class Inputs(ctypes.Structure):
+    """psfm_inputs."""
+    _fields_ = [("tgt", c_void_p), ("ctx", c_void_p * MAX_CTX), ("sig", c_void_p * MAX_SCALES),
+                ("cam", c_void_p), ("mask", c_void_p)]
+
+
+class Workspace(ctypes.Structure):
+    """psfm_workspace."""
+    _fields_ = [("photo_part", c_void_p), ("smooth_part", c_void_p), ("clip_part", c_void_p),
+                ("clip_thr", c_void_p), ("pose_part", c_void_p), ("argmin", c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the HIP library; raise loudly if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP extension {LIB_PATH} is not built: run `python -c 'import "
+                           f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, PP, V = ctypes.POINTER(Params), ctypes.POINTER(ctypes.POINTER(Params)), c_void_p
+    WS, WSP, IN = ctypes.POINTER(Workspace), ctypes.POINTER(ctypes.POINTER(Workspace)), ctypes.POINTER(Inputs)
+    sz = ctypes.POINTER(c_size_t)
+    sig = {
+        "psfm_workspace_floats": ([P, sz, sz, sz, sz, sz, sz], c_int),
+        "psfm_photometric_clip_stats": ([P, IN, WS, V], c_int),
+        "psfm_photometric_fwd": ([P, IN, WS, V], c_int),
+        "psfm_smoothness_fwd": ([P, IN, WS, V], c_int),
+        "psfm_finalize": ([c_int, PP, WSP, V, V, V], c_int),
+        "psfm_photometric_bwd": ([P, IN, WS, V, V, V], c_int),
+        "psfm_smoothness_bwd": ([P, IN, V, V, V, V], c_int),
+        "psfm_pose_grad_reduce": ([c_int, PP, WSP, V, V], c_int),
+        "psfm_view_synthesis_fwd": ([c_int, c_int, c_int, V, V, V, V, V], c_int),
+        "psfm_view_synthesis_bwd": ([c_int, c_int, c_int, V, V, V, V, V, V, V, V], c_int),
+        "psfm_tiles_per_image": ([c_int, c_int], c_int),
+        "psfm_last_error": ([], ctypes.c_char_p),
+        "psfm_version": ([], ctypes.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes, fn.restype = args, res
+    _lib = L
+    return L
+
+
+EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photometric_fwd",
+            "psfm_smoothness_fwd", "psfm_finalize", "psfm_photometric_bwd", "psfm_smoothness_bwd",
+            "psfm_pose_grad_reduce", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
+            "psfm_tiles_per_image", "psfm_last_error", "psfm_version")
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {lib().psfm_last_error().decode()}")
+
+
+def require_device(*tensors):
+    """The HIP path only runs on ROCm device tensors — no CPU fallback."""
+    for t in tensors:
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32):
+            raise RuntimeError("packnet_sfm_amd photometric path needs float32 tensors on a ROCm "
+                               f"(HIP) device; got {t.dtype} on {t.device}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def tiles_per_image(H, W):
+    return lib().psfm_tiles_per_image(H, W)

@@ -1,0 +1,238 @@
+// psfm_common.h — device helpers shared by the photometric kernels (gfx950 / CDNA4).
+//
+// Numerics follow the reference op chain exactly where the order of fp32 operations is
+// observable at 1e-4 (projection, normalise/unnormalise round trip, bilinear weights,
+// SSIM); see DESIGN.md "Numerics".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/psfm.h"
+
+namespace psfm {
+
+// Tile of output pixels owned by one 256-thread workgroup: 64 columns (one wave per row,
+// fully coalesced 256-B row segments) x 4 rows.
+constexpr int TX = 64;
+constexpr int TY = 4;
+constexpr int NT = TX * TY;
+constexpr int NWAVE = NT / 64;
+constexpr int MAXN = PSFM_MAX_CTX;
+constexpr int MAXS = PSFM_MAX_SCALES;
+
+__host__ __device__ inline int tiles_x(int W) { return (W + TX - 1) / TX; }
+__host__ __device__ inline int tiles_y(int H) { return (H + TY - 1) / TY; }
+__host__ __device__ inline int tiles_img(int H, int W) { return tiles_x(W) * tiles_y(H); }
+
+// ReflectionPad2d(1) index map (SSIM :34), clamped so that halo cells that no real output
+// reads (partial tiles) still address valid memory.
+__device__ __forceinline__ int reflect1(int i, int n) {
+    i = i < 0 ? -i : i;
+    i = i >= n ? 2 * n - 2 - i : i;
+    return min(max(i, 0), n - 1);
+}
+
+struct CamRec {
+    float Ki[9];  // K^-1 of the target camera at this scale (camera.py:72-81)
+    float Kr[9];  // K of the context camera at this scale
+    float T[12];  // [R|t] target -> context (pose.py:39-46), row-major 3x4
+};
+
+__device__ __forceinline__ void load_cam(const float* __restrict__ p, CamRec& c) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) c.Ki[i] = p[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) c.Kr[i] = p[9 + i];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) c.T[i] = p[18 + i];
+}
+
+// sigmoid -> depth (post_process_depth.py:101-106) -> inv (:369) -> warp depth (depth.py:120)
+struct DepthChain {
+    float lo, rng;
+    __device__ __forceinline__ float warp_depth(float s, float& d1, float& inv) const {
+        d1 = 1.0f / (lo + rng * s + 1e-8f);
+        inv = 1.0f / (d1 + 1e-8f);
+        return 1.0f / fmaxf(inv, 1e-6f);
+    }
+    // d(warp depth)/ds with torch's reciprocal-backward form (-out^2) at every 1/x
+    __device__ __forceinline__ float dwarp_ds(float d, float d1, float inv) const {
+        if (!(inv >= 1e-6f)) return 0.0f;  // clamp(min) passes where x >= min
+        return -(d * d) * (inv * inv) * (d1 * d1) * rng;
+    }
+};
+
+// Projection of pixel (u,v) with depth d: X = d K^-1 [u v 1]^T (camera.py:131-139),
+// c = R X + t (pose.py:80-86), p = K_ref c (camera.py:165-167), normalised and
+// unnormalised as project() + grid_sample(align_corners=True) do (camera.py:172-176).
+struct Proj {
+    float xn0, xn1, xn2;  // K^-1 [u v 1]
+    float X0, X1, X2;     // lifted point
+    float p0, p1, p2;     // K_ref (R X + t)
+    float z;              // clamp(p2, 1e-5)
+    float ix, iy;         // sampling position in pixels
+};
+
+__device__ __forceinline__ void project(const CamRec& c, float u, float v, float d, int H, int W,
+                                        Proj& r) {
+    r.xn0 = c.Ki[0] * u + c.Ki[1] * v + c.Ki[2];
+    r.xn1 = c.Ki[3] * u + c.Ki[4] * v + c.Ki[5];
+    r.xn2 = c.Ki[6] * u + c.Ki[7] * v + c.Ki[8];
+    r.X0 = r.xn0 * d;
+    r.X1 = r.xn1 * d;
+    r.X2 = r.xn2 * d;
+    const float c0 = c.T[0] * r.X0 + c.T[1] * r.X1 + c.T[2] * r.X2 + c.T[3];
+    const float c1 = c.T[4] * r.X0 + c.T[5] * r.X1 + c.T[6] * r.X2 + c.T[7];
+    const float c2 = c.T[8] * r.X0 + c.T[9] * r.X1 + c.T[10] * r.X2 + c.T[11];
+    r.p0 = c.Kr[0] * c0 + c.Kr[1] * c1 + c.Kr[2] * c2;
+    r.p1 = c.Kr[3] * c0 + c.Kr[4] * c1 + c.Kr[5] * c2;
+    r.p2 = c.Kr[6] * c0 + c.Kr[7] * c1 + c.Kr[8] * c2;
+    r.z = fmaxf(r.p2, 1e-5f);
+    const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+    const float xnorm = 2.0f * (r.p0 / r.z) / wm1 - 1.0f;
+    const float ynorm = 2.0f * (r.p1 / r.z) / hm1 - 1.0f;
+    r.ix = ((xnorm + 1.0f) / 2.0f) * wm1;
+    r.iy = ((ynorm + 1.0f) / 2.0f) * hm1;
+}
+
+// Bilinear taps of grid_sample(padding_mode='zeros'): per-tap zero when out of bounds.
+struct Taps {
+    int x0, y0;
+    float fx0, fy0;
+    bool ok;  // any tap can be in bounds (also guards int conversion of huge coordinates)
+};
+
+__device__ __forceinline__ Taps make_taps(float ix, float iy, int H, int W) {
+    Taps t;
+    // some tap may be in bounds iff ix in [-1, W) (and y alike); the wider open interval
+    // also keeps the float->int conversion below well defined (and rejects NaN)
+    t.ok = (ix > -2.0f) && (ix < (float)W + 1.0f) && (iy > -2.0f) && (iy < (float)H + 1.0f);
+    t.fx0 = floorf(ix);
+    t.fy0 = floorf(iy);
+    t.x0 = t.ok ? (int)t.fx0 : 0;
+    t.y0 = t.ok ? (int)t.fy0 : 0;
+    return t;
+}
+
+// warped[c] = sum_tap w_tap * img[c](tap)  (ATen grid_sampler_2d bilinear, nw,ne,sw,se order)
+__device__ __forceinline__ void bilinear3(const float* __restrict__ img, int H, int W, float ix,
+                                          float iy, float out[3]) {
+    out[0] = out[1] = out[2] = 0.0f;
+    const Taps t = make_taps(ix, iy, H, W);
+    if (!t.ok) return;
+    const float ixe = t.fx0 + 1.0f, iys = t.fy0 + 1.0f;
+    const float nw = (ixe - ix) * (iys - iy);
+    const float ne = (ix - t.fx0) * (iys - iy);
+    const float sw = (ixe - ix) * (iy - t.fy0);
+    const float se = (ix - t.fx0) * (iy - t.fy0);
+    const bool xw = t.x0 >= 0 && t.x0 < W, xe = t.x0 + 1 >= 0 && t.x0 + 1 < W;
+    const bool yn = t.y0 >= 0 && t.y0 < H, ys = t.y0 + 1 >= 0 && t.y0 + 1 < H;
+    const size_t plane = (size_t)H * W;
+    const size_t base = (size_t)t.y0 * W + t.x0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* p = img + c * plane;
+        float acc = 0.0f;
+        if (yn && xw) acc += p[base] * nw;
+        if (yn && xe) acc += p[base + 1] * ne;
+        if (ys && xw) acc += p[base + W] * sw;
+        if (ys && xe) acc += p[base + W + 1] * se;
+        out[c] = acc;
+    }
+}
+
+// Adjoint of bilinear3 w.r.t. the sampling position (the images carry no gradient:
+// they are data).  Returns d/d(ix), d/d(iy).
+__device__ __forceinline__ void bilinear3_grad_pos(const float* __restrict__ img, int H, int W,
+                                                   float ix, float iy, const float g[3],
+                                                   float& gix, float& giy) {
+    gix = giy = 0.0f;
+    const Taps t = make_taps(ix, iy, H, W);
+    if (!t.ok) return;
+    const float ixe = t.fx0 + 1.0f, iys = t.fy0 + 1.0f;
+    const bool xw = t.x0 >= 0 && t.x0 < W, xe = t.x0 + 1 >= 0 && t.x0 + 1 < W;
+    const bool yn = t.y0 >= 0 && t.y0 < H, ys = t.y0 + 1 >= 0 && t.y0 + 1 < H;
+    const size_t plane = (size_t)H * W;
+    const size_t base = (size_t)t.y0 * W + t.x0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* p = img + c * plane;
+        const float go = g[c];
+        if (yn && xw) {
+            const float v = p[base];
+            gix -= v * (iys - iy) * go;
+            giy -= v * (ixe - ix) * go;
+        }
+        if (yn && xe) {
+            const float v = p[base + 1];
+            gix += v * (iys - iy) * go;
+            giy -= v * (ix - t.fx0) * go;
+        }
+        if (ys && xw) {
+            const float v = p[base + W];
+            gix -= v * (iy - t.fy0) * go;
+            giy += v * (ixe - ix) * go;
+        }
+        if (ys && xe) {
+            const float v = p[base + W + 1];
+            gix += v * (iy - t.fy0) * go;
+            giy += v * (ix - t.fx0) * go;
+        }
+    }
+}
+
+// Adjoint of project() for one pixel: from (gix, giy) to dL/dd and dL/dT (12, accumulated).
+__device__ __forceinline__ float project_grad(const CamRec& c, const Proj& r, float d, float gix,
+                                              float giy, int H, int W, float gT[12]) {
+    // ix = ((2u/(W-1) - 1 + 1)/2)(W-1) with u = p0/z  ->  d ix/du = (W-1)/2 * 2/(W-1)
+    const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+    const float gu = gix * (wm1 / 2.0f) * (2.0f / wm1);
+    const float gv = giy * (hm1 / 2.0f) * (2.0f / hm1);
+    const float gp0 = gu / r.z;
+    const float gp1 = gv / r.z;
+    const float gp2 = (r.p2 >= 1e-5f) ? -(gu * (r.p0 / r.z) + gv * (r.p1 / r.z)) / r.z : 0.0f;
+    // c = K_ref^-1 p  -> gc = K_ref^T gp
+    const float gc0 = c.Kr[0] * gp0 + c.Kr[3] * gp1 + c.Kr[6] * gp2;
+    const float gc1 = c.Kr[1] * gp0 + c.Kr[4] * gp1 + c.Kr[7] * gp2;
+    const float gc2 = c.Kr[2] * gp0 + c.Kr[5] * gp1 + c.Kr[8] * gp2;
+    gT[0] += gc0 * r.X0; gT[1] += gc0 * r.X1; gT[2] += gc0 * r.X2; gT[3] += gc0;
+    gT[4] += gc1 * r.X0; gT[5] += gc1 * r.X1; gT[6] += gc1 * r.X2; gT[7] += gc1;
+    gT[8] += gc2 * r.X0; gT[9] += gc2 * r.X1; gT[10] += gc2 * r.X2; gT[11] += gc2;
+    // X = d xn, c = R X + t -> dL/dd = (R^T gc) . xn
+    const float gX0 = c.T[0] * gc0 + c.T[4] * gc1 + c.T[8] * gc2;
+    const float gX1 = c.T[1] * gc0 + c.T[5] * gc1 + c.T[9] * gc2;
+    const float gX2 = c.T[2] * gc0 + c.T[6] * gc1 + c.T[10] * gc2;
+    (void)d;
+    return gX0 * r.xn0 + gX1 * r.xn1 + gX2 * r.xn2;
+}
+
+// ---- deterministic block reductions (wave butterfly, then waves in fixed order) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Reduces K values per thread over the 256-thread block; result valid in thread 0.
+template <int K>
+__device__ __forceinline__ void block_sum(float (&v)[K], float* red /* LDS [NWAVE*K] */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float s = 0.0f;
+            for (int w = 0; w < NWAVE; ++w) s += red[w * K + k];
+            v[k] = s;
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace psfm

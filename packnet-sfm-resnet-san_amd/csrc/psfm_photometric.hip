@@ -1,0 +1,1041 @@
+// psfm_photometric.hip — fused view-synthesis + SSIM/L1 + min-reprojection + smoothness
+// kernels for MI355X (gfx950), behind the C-ABI of include/psfm.h.
+//
+// Reference op chain replaced (paths relative to the reference's packnet_sfm/):
+//   losses/multiview_photometric_loss.py:331-410 (forward), :131-195 (warp_ref_image),
+//   :15-54 + :199-267 (SSIM, calc_photometric_loss), :269-297 (reduce_photometric_loss),
+//   :301-327 + utils/depth.py:146-198 (smoothness), geometry/camera.py:111-190,
+//   geometry/camera_utils.py:27-59 (view_synthesis), and the autograd backward of all of it.
+//
+// Design: one 256-thread workgroup owns a 64x4 tile of output pixels of
+// one image.  K1 (forward) stages the target and each warped/unwarped candidate image of the
+// tile + 1-pixel reflect halo in LDS, evaluates the 3x3 SSIM windows from LDS, keeps the
+// candidates of a scale in registers and reduces min/argmin in-register; per-tile partial
+// sums go to a workspace and a single finalize kernel reduces them in a fixed order
+// (bitwise deterministic, no float atomics).  K2 (backward) recomputes the warp on a
+// 2-pixel halo, forms the SSIM adjoint coefficients on a 1-pixel halo in LDS and gathers
+// them (reflect-aware weights) per pixel, then back-propagates through bilinear sampling and
+// the projection; dL/d[R|t] is reduced per tile (wave butterfly + fixed-order wave sum).
+#include <cstdio>
+#include <string>
+
+#include "psfm_common.h"
+
+using namespace psfm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define PSFM_LAUNCH_CHECK()                                                          \
+    do {                                                                             \
+        hipError_t e_ = hipGetLastError();                                           \
+        if (e_ != hipSuccess) return fail((int)e_, std::string("launch: ") +        \
+                                                       hipGetErrorString(e_));       \
+    } while (0)
+
+struct KArgs {
+    psfm_params p;
+    psfm_inputs in;
+    psfm_workspace ws;
+    const float* grad_out;
+    float* grad_sig[MAXS];
+    const float* smooth_stats;
+};
+
+template <typename T>
+__device__ __forceinline__ T pick4(const T (&a)[4], int i) {
+    return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+
+__device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
+
+// number of candidate SOURCES per scale (warped per context, + unwarped per context with automask)
+__host__ __device__ __forceinline__ int n_src(const psfm_params& p) { return p.automask ? 2 * p.N : p.N; }
+__host__ __device__ __forceinline__ int src_warp(const psfm_params& p, int j) { return p.automask ? 2 * j : j; }
+__host__ __device__ __forceinline__ int src_unwarp(int j) { return 2 * j + 1; }
+
+struct TileGeom {
+    int b, tile, x0, y0, lx, ly, gx, gy;
+    bool inside;
+};
+
+__device__ __forceinline__ TileGeom tile_geom(int H, int W) {
+    TileGeom g;
+    g.tile = blockIdx.x;
+    g.b = blockIdx.y;
+    const int tx = tiles_x(W);
+    g.x0 = (g.tile % tx) * TX;
+    g.y0 = (g.tile / tx) * TY;
+    g.lx = threadIdx.x % TX;
+    g.ly = threadIdx.x / TX;
+    g.gx = g.x0 + g.lx;
+    g.gy = g.y0 + g.ly;
+    g.inside = g.gx < W && g.gy < H;
+    return g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SSIM (3x3, reflect) of one output pixel from LDS windows (halo stride HX); x = estimate, y =
+// target.  Returns mean_c clamp((1-SSIM_c)/2, 0, 1) and mean_c |x-y| (SSIM :15-54, :199-247).
+// ---------------------------------------------------------------------------------------------
+template <int HX, int HY>
+__device__ __forceinline__ void photo_terms(const float (&sX)[3][HY][HX], const float (&sY)[3][HY][HX],
+                                            int cy, int cx, const float my[3], const float syy[3],
+                                            float C1, float C2, float& ssim_mean, float& l1_mean,
+                                            float l1c[3]) {
+    float ls = 0.0f, as = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float mx = 0.0f, sxx = 0.0f, sxy = 0.0f;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const float xv = sX[c][cy + dy][cx + dx];
+                const float yv = sY[c][cy + dy][cx + dx];
+                mx += xv;
+                sxx += xv * xv;
+                sxy += xv * yv;
+            }
+        mx /= 9.0f;
+        sxx /= 9.0f;
+        sxy /= 9.0f;
+        const float mxy = mx * my[c], mx2 = mx * mx, my2 = my[c] * my[c];
+        const float v1 = 2.0f * (sxy - mxy) + C2;
+        const float v2 = (sxx - mx2) + (syy[c] - my2) + C2;
+        const float ssim = ((2.0f * mxy + C1) * v1) / ((mx2 + my2 + C1) * v2);
+        ls += fminf(fmaxf((1.0f - ssim) / 2.0f, 0.0f), 1.0f);
+        const float a = fabsf(sX[c][cy][cx] - sY[c][cy][cx]);
+        l1c[c] = a;
+        as += a;
+    }
+    ssim_mean = ls / 3.0f;
+    l1_mean = as / 3.0f;
+}
+
+template <int HX, int HY>
+__device__ __forceinline__ void target_stats(const float (&sY)[3][HY][HX], int cy, int cx,
+                                             float my[3], float syy[3]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float m = 0.0f, s2 = 0.0f;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const float v = sY[c][cy + dy][cx + dx];
+                m += v;
+                s2 += v * v;
+            }
+        my[c] = m / 9.0f;
+        syy[c] = s2 / 9.0f;
+    }
+}
+
+// Fill an LDS halo image (origin y0-OFF, x0-OFF; reflect-padded) from a planar [3,H,W] image.
+template <int HX, int HY, int OFF>
+__device__ __forceinline__ void fill_plain(float (&dst)[3][HY][HX], const float* __restrict__ img,
+                                           int H, int W, int y0, int x0) {
+    const size_t plane = (size_t)H * W;
+    for (int i = threadIdx.x; i < HX * HY; i += NT) {
+        const int hy = i / HX, hx = i % HX;
+        const size_t o = (size_t)reflect1(y0 - OFF + hy, H) * W + reflect1(x0 - OFF + hx, W);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dst[c][hy][hx] = img[c * plane + o];
+    }
+}
+
+// Fill an LDS halo with the view-synthesised context image (camera_utils.py:27-59).
+template <int HX, int HY, int OFF>
+__device__ __forceinline__ void fill_warped(float (&dst)[3][HY][HX], const float* __restrict__ ctx,
+                                            const float* __restrict__ sig, const CamRec& cam,
+                                            const DepthChain& dc, int H, int W, int y0, int x0) {
+    for (int i = threadIdx.x; i < HX * HY; i += NT) {
+        const int hy = i / HX, hx = i % HX;
+        const int yy = reflect1(y0 - OFF + hy, H), xx = reflect1(x0 - OFF + hx, W);
+        float d1, inv;
+        const float d = dc.warp_depth(sig[(size_t)yy * W + xx], d1, inv);
+        Proj r;
+        project(cam, (float)xx, (float)yy, d, H, W, r);
+        float w[3];
+        bilinear3(ctx, H, W, r.ix, r.iy, w);
+        dst[0][hy][hx] = w[0];
+        dst[1][hy][hx] = w[1];
+        dst[2][hy][hx] = w[2];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1: forward.  STATS=true is the clip-statistics pass (sum/sumsq per candidate map).
+// ---------------------------------------------------------------------------------------------
+template <bool L1ONLY, bool STATS>
+__global__ __launch_bounds__(NT) void k_photo_fwd(KArgs a) {
+    const psfm_params& p = a.p;
+    const int H = p.H, W = p.W, N = p.N, B = p.B;
+    const TileGeom g = tile_geom(H, W);
+    constexpr int HX = TX + 2, HY = TY + 2;
+    __shared__ float sX[3][HY][HX];
+    __shared__ float sY[3][HY][HX];
+    __shared__ float red[NWAVE * 16];
+
+    const size_t plane = (size_t)H * W;
+    const int tiles = tiles_img(H, W);
+    const int blk = g.b * tiles + g.tile;
+    const size_t pix = (size_t)g.gy * W + g.gx;
+    const int cy = g.ly + 1, cx = g.lx + 1;
+    const DepthChain dc{1.0f / fmaxf(p.max_depth, 1e-6f),
+                        (float)(1.0 / fmax((double)p.min_depth, 1e-6) - 1.0 / fmax((double)p.max_depth, 1e-6))};
+    const float l1w = 1.0f - p.ssim_w;
+    const int nsrc = n_src(p);
+
+    fill_plain<HX, HY, 1>(sY, a.in.tgt + (size_t)g.b * 3 * plane, H, W, g.y0, g.x0);
+    __syncthreads();
+    float my[3] = {0, 0, 0}, syy[3] = {0, 0, 0};
+    if (!L1ONLY) target_stats<HX, HY>(sY, cy, cx, my, syy);
+    const float mval = (a.in.mask == nullptr) ? 1.0f : (g.inside ? a.in.mask[(size_t)g.b * plane + pix] : 0.0f);
+
+    // candidate photometric values (raw: before clip and mask)
+    float cu[MAXN][3], cw[MAXN][3];
+    auto eval = [&](float (&out)[3]) {
+        float sm, lm, l1c[3];
+        photo_terms<HX, HY>(sX, sY, cy, cx, my, syy, p.C1, p.C2, sm, lm, l1c);
+        if (L1ONLY) {
+            out[0] = l1c[0]; out[1] = l1c[1]; out[2] = l1c[2];
+        } else {
+            out[0] = p.ssim_w * sm + l1w * lm;
+        }
+    };
+
+    // automask: un-warped context losses (identical for every full-res scale: computed once)
+    if (p.automask) {
+#pragma unroll
+        for (int j = 0; j < MAXN; ++j) {
+            if (j >= N) break;
+            fill_plain<HX, HY, 1>(sX, pick4(a.in.ctx, j) + (size_t)g.b * 3 * plane, H, W, g.y0, g.x0);
+            __syncthreads();
+            eval(cu[j]);
+            __syncthreads();
+        }
+    }
+
+    const int C = L1ONLY ? 3 : 1;
+    for (int s = 0; s < p.S; ++s) {
+        const float* sig = pick4(a.in.sig, s) + (size_t)g.b * plane;
+#pragma unroll
+        for (int j = 0; j < MAXN; ++j) {
+            if (j >= N) break;
+            CamRec cam;
+            load_cam(a.in.cam + ((size_t)(s * N + j) * B + g.b) * PSFM_CAMREC, cam);
+            fill_warped<HX, HY, 1>(sX, pick4(a.in.ctx, j) + (size_t)g.b * 3 * plane, sig, cam, dc,
+                                   H, W, g.y0, g.x0);
+            __syncthreads();
+            eval(cw[j]);
+            __syncthreads();
+        }
+
+        if (STATS) {
+            // per candidate map: sum and sum of squares of the raw photometric values (:251)
+            float st[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) st[k] = 0.0f;
+            if (g.inside) {
+#pragma unroll
+                for (int j = 0; j < MAXN; ++j) {
+                    if (j >= N) break;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (c >= C) break;
+                        const int sw = p.automask ? 2 * j : j;
+                        st[2 * sw] += cw[j][c];
+                        st[2 * sw + 1] += cw[j][c] * cw[j][c];
+                        if (p.automask) {
+                            st[2 * (sw + 1)] += cu[j][c];
+                            st[2 * (sw + 1) + 1] += cu[j][c] * cu[j][c];
+                        }
+                    }
+                }
+            }
+            block_sum<16>(st, red);
+            if (threadIdx.x == 0) {
+                for (int k = 0; k < nsrc; ++k) {
+                    float* o = a.ws.clip_part + (((size_t)s * nsrc + k) * (B * tiles) + blk) * 2;
+                    o[0] = st[2 * k];
+                    o[1] = st[2 * k + 1];
+                }
+            }
+            continue;
+        }
+
+        // clip (:249-253) -> mask (:256-264) -> min / mean over candidates (:284-288)
+        const float* thr = (p.clip_loss > 0.0f) ? a.ws.clip_thr + (size_t)s * nsrc : nullptr;
+        float best = INFINITY, sum = 0.0f;
+        int arg = 0, k = 0;
+#pragma unroll
+        for (int j = 0; j < MAXN; ++j) {
+            if (j >= N) break;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !p.automask) break;
+                const int src = u ? src_unwarp(j) : src_warp(p, j);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (c >= C) break;
+                    float v = u ? cu[j][c] : cw[j][c];
+                    if (thr) v = fminf(v, thr[src]);
+                    v = v * mval;
+                    sum += v;
+                    if (v < best) {
+                        best = v;
+                        arg = k;
+                    }
+                    ++k;
+                }
+            }
+        }
+        float val[1] = {0.0f};
+        if (g.inside) {
+            if (p.reduce_op == PSFM_REDUCE_MIN) {
+                val[0] = best;
+                a.ws.argmin[((size_t)s * B + g.b) * plane + pix] = (uint8_t)arg;
+            } else {
+                val[0] = sum;
+            }
+        }
+        block_sum<1>(val, red);
+        if (threadIdx.x == 0) a.ws.photo_part[(size_t)s * (B * tiles) + blk] = val[0];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: backward of the photometric term.
+// ---------------------------------------------------------------------------------------------
+template <bool L1ONLY>
+__global__ __launch_bounds__(NT) void k_photo_bwd(KArgs a) {
+    const psfm_params& p = a.p;
+    const int H = p.H, W = p.W, N = p.N, B = p.B;
+    const TileGeom g = tile_geom(H, W);
+    constexpr int HX2 = TX + 4, HY2 = TY + 4;  // warped / target: tile + 2
+    constexpr int HX1 = TX + 2, HY1 = TY + 2;  // SSIM adjoint coefficients: tile + 1
+    __shared__ float sX[3][HY2][HX2];
+    __shared__ float sY[3][HY2][HX2];
+    __shared__ float sC[10][HY1][HX1];
+    __shared__ float red[NWAVE * 12];
+
+    const size_t plane = (size_t)H * W;
+    const int tiles = tiles_img(H, W);
+    const int blk = g.b * tiles + g.tile;
+    const size_t pix = (size_t)g.gy * W + g.gx;
+    const DepthChain dc{1.0f / fmaxf(p.max_depth, 1e-6f),
+                        (float)(1.0 / fmax((double)p.min_depth, 1e-6) - 1.0 / fmax((double)p.max_depth, 1e-6))};
+    const float l1w = 1.0f - p.ssim_w;
+    const int nsrc = n_src(p);
+    const int ncand = nsrc * (L1ONLY ? 3 : 1);
+    const float gout = *a.grad_out;
+    const double cnt = (double)B * H * W;
+    const float gscale = (p.reduce_op == PSFM_REDUCE_MIN)
+                             ? (float)(gout / ((double)p.n_scales * cnt))
+                             : (float)(gout / ((double)p.n_scales * (double)nsrc * cnt * (L1ONLY ? 3.0 : 1.0)));
+    const float* mask = a.in.mask ? a.in.mask + (size_t)g.b * plane : nullptr;
+    (void)ncand;
+
+    fill_plain<HX2, HY2, 2>(sY, a.in.tgt + (size_t)g.b * 3 * plane, H, W, g.y0, g.x0);
+    __syncthreads();
+
+    for (int s = 0; s < p.S; ++s) {
+        const float* sig = pick4(a.in.sig, s) + (size_t)g.b * plane;
+        const uint8_t* am = a.ws.argmin + ((size_t)s * B + g.b) * plane;
+        const float* thr = (p.clip_loss > 0.0f) ? a.ws.clip_thr + (size_t)s * nsrc : nullptr;
+        float gs = 0.0f;
+        float qd = 1.0f, qd1 = 1.0f, qinv = 1.0f;
+        if (g.inside) qd = dc.warp_depth(sig[pix], qd1, qinv);
+
+        for (int j = 0; j < N; ++j) {
+            const int src = src_warp(p, j);
+            CamRec cam;
+            load_cam(a.in.cam + ((size_t)(s * N + j) * B + g.b) * PSFM_CAMREC, cam);
+            const float* ctx = pick4(a.in.ctx, j) + (size_t)g.b * 3 * plane;
+            float gT[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gT[k] = 0.0f;
+
+            // does any pixel whose SSIM window touches this tile select this candidate?
+            bool any = (p.reduce_op != PSFM_REDUCE_MIN);
+            if (!any) {
+                for (int i = threadIdx.x; i < HX1 * HY1; i += NT) {
+                    const int py = g.y0 - 1 + i / HX1, px = g.x0 - 1 + i % HX1;
+                    if (py < 0 || py >= H || px < 0 || px >= W) continue;
+                    const int ai = am[(size_t)py * W + px];
+                    any |= L1ONLY ? (ai / 3 == src) : (ai == src);
+                }
+            }
+            any = __syncthreads_or(any);
+
+            if (any && L1ONLY) {
+                // 3-channel L1 candidates (:246): no SSIM window, per-pixel adjoint
+                if (g.inside) {
+                    Proj r;
+                    project(cam, (float)g.gx, (float)g.gy, qd, H, W, r);
+                    float w[3];
+                    bilinear3(ctx, H, W, r.ix, r.iy, w);
+                    float gw[3];
+                    const float mv = mask ? mask[pix] : 1.0f;
+                    bool nz = false;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float y = a.in.tgt[((size_t)g.b * 3 + c) * plane + pix];
+                        const float raw = fabsf(w[c] - y);
+                        float G = gscale * mv;
+                        if (p.reduce_op == PSFM_REDUCE_MIN && am[pix] != src * 3 + c) G = 0.0f;
+                        if (thr && !(raw <= thr[src])) G = 0.0f;
+                        gw[c] = G * sgnf(w[c] - y);
+                        nz |= gw[c] != 0.0f;
+                    }
+                    if (nz) {
+                        float gix, giy;
+                        bilinear3_grad_pos(ctx, H, W, r.ix, r.iy, gw, gix, giy);
+                        const float gd = project_grad(cam, r, qd, gix, giy, H, W, gT);
+                        gs += gd * dc.dwarp_ds(qd, qd1, qinv);
+                    }
+                }
+            } else if (any) {
+                fill_warped<HX2, HY2, 2>(sX, ctx, sig, cam, dc, H, W, g.y0, g.x0);
+                __syncthreads();
+                // SSIM adjoint coefficients on the tile + 1 halo
+                for (int i = threadIdx.x; i < HX1 * HY1; i += NT) {
+                    const int hy = i / HX1, hx = i % HX1;
+                    const int py = g.y0 - 1 + hy, px = g.x0 - 1 + hx;
+                    float co[10];
+#pragma unroll
+                    for (int k = 0; k < 10; ++k) co[k] = 0.0f;
+                    if (py >= 0 && py < H && px >= 0 && px < W) {
+                        const size_t pp = (size_t)py * W + px;
+                        float G = gscale * (mask ? mask[pp] : 1.0f);
+                        if (p.reduce_op == PSFM_REDUCE_MIN && am[pp] != src) G = 0.0f;
+                        if (G != 0.0f) {
+                            const int cy = hy + 1, cx = hx + 1;  // in the tile + 2 frame
+                            float dS_dmx[3], dS_dsxx[3], dS_dsxy[3], pass[3];
+                            float ls = 0.0f, as = 0.0f;
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) {
+                                float mx = 0.0f, sxx = 0.0f, sxy = 0.0f, my = 0.0f, syy = 0.0f;
+#pragma unroll
+                                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                                    for (int dx = -1; dx <= 1; ++dx) {
+                                        const float xv = sX[c][cy + dy][cx + dx];
+                                        const float yv = sY[c][cy + dy][cx + dx];
+                                        mx += xv;
+                                        sxx += xv * xv;
+                                        sxy += xv * yv;
+                                        my += yv;
+                                        syy += yv * yv;
+                                    }
+                                mx /= 9.0f; sxx /= 9.0f; sxy /= 9.0f; my /= 9.0f; syy /= 9.0f;
+                                const float mxy = mx * my, mx2 = mx * mx, my2 = my * my;
+                                const float A1 = 2.0f * mxy + p.C1, A2 = 2.0f * (sxy - mxy) + p.C2;
+                                const float B1 = mx2 + my2 + p.C1, B2 = (sxx - mx2) + (syy - my2) + p.C2;
+                                const float Nn = A1 * A2, D = B1 * B2;
+                                const float ssim = Nn / D;
+                                const float l = (1.0f - ssim) / 2.0f;
+                                pass[c] = (l >= 0.0f && l <= 1.0f) ? 1.0f : 0.0f;
+                                ls += fminf(fmaxf(l, 0.0f), 1.0f);
+                                as += fabsf(sX[c][cy][cx] - sY[c][cy][cx]);
+                                const float iD = 1.0f / D;
+                                dS_dmx[c] = 2.0f * my * (A2 - A1) * iD - Nn * 2.0f * mx * (B2 - B1) * iD * iD;
+                                dS_dsxx[c] = -Nn * B1 * iD * iD;
+                                dS_dsxy[c] = 2.0f * A1 * iD;
+                            }
+                            if (thr) {
+                                const float raw = p.ssim_w * (ls / 3.0f) + l1w * (as / 3.0f);
+                                if (!(raw <= thr[src])) G = 0.0f;
+                            }
+                            const float kS = G * (-0.5f) * (p.ssim_w / 3.0f) / 9.0f;
+#pragma unroll
+                            for (int c = 0; c < 3; ++c) {
+                                co[c] = kS * pass[c] * dS_dmx[c];
+                                co[3 + c] = kS * pass[c] * dS_dsxx[c];
+                                co[6 + c] = kS * pass[c] * dS_dsxy[c];
+                            }
+                            co[9] = G * l1w / 3.0f;
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 10; ++k) sC[k][hy][hx] = co[k];
+                }
+                __syncthreads();
+                if (g.inside) {
+                    const int qy2 = g.ly + 2, qx2 = g.lx + 2;
+                    float gw[3] = {0.0f, 0.0f, 0.0f};
+                    bool nz = false;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float xq = sX[c][qy2][qx2], yq = sY[c][qy2][qx2];
+                        float acc = 0.0f;
+#pragma unroll
+                        for (int dy = -1; dy <= 1; ++dy) {
+                            const int py = g.gy + dy;
+                            if (py < 0 || py >= H) continue;
+                            const float wy = 1.0f + ((py == 0 && g.gy == 1) ? 1.0f : 0.0f) +
+                                             ((py == H - 1 && g.gy == H - 2) ? 1.0f : 0.0f);
+#pragma unroll
+                            for (int dx = -1; dx <= 1; ++dx) {
+                                const int px = g.gx + dx;
+                                if (px < 0 || px >= W) continue;
+                                const float wx = 1.0f + ((px == 0 && g.gx == 1) ? 1.0f : 0.0f) +
+                                                 ((px == W - 1 && g.gx == W - 2) ? 1.0f : 0.0f);
+                                const int hy = g.ly + 1 + dy, hx = g.lx + 1 + dx;
+                                acc += (wy * wx) * (sC[c][hy][hx] + 2.0f * xq * sC[3 + c][hy][hx] +
+                                                    yq * sC[6 + c][hy][hx]);
+                            }
+                        }
+                        acc += sC[9][g.ly + 1][g.lx + 1] * sgnf(xq - yq);
+                        gw[c] = acc;
+                        nz |= acc != 0.0f;
+                    }
+                    if (nz) {
+                        Proj r;
+                        project(cam, (float)g.gx, (float)g.gy, qd, H, W, r);
+                        float gix, giy;
+                        bilinear3_grad_pos(ctx, H, W, r.ix, r.iy, gw, gix, giy);
+                        const float gd = project_grad(cam, r, qd, gix, giy, H, W, gT);
+                        gs += gd * dc.dwarp_ds(qd, qd1, qinv);
+                    }
+                }
+            }
+            block_sum<12>(gT, red);  // (its barriers also retire sX / sC before the next fill)
+            if (threadIdx.x == 0) {
+                float* o = a.ws.pose_part + (((size_t)(s * N + j) * B + g.b) * tiles + g.tile) * 12;
+#pragma unroll
+                for (int k = 0; k < 12; ++k) o[k] = gT[k];
+            }
+        }
+        if (g.inside) pick4(a.grad_sig, s)[(size_t)g.b * plane + pix] = gs;
+    }
+    (void)blk;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3: smoothness (utils/depth.py:146-198, multiview_photometric_loss.py:301-327)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float edge_weight(const float* __restrict__ img, size_t plane, size_t p,
+                                             size_t q) {
+    const float m = (fabsf(img[p] - img[q]) + fabsf(img[plane + p] - img[plane + q]) +
+                     fabsf(img[2 * plane + p] - img[2 * plane + q])) / 3.0f;
+    return expf(-m);
+}
+
+__global__ __launch_bounds__(NT) void k_smooth_fwd(KArgs a) {
+    const psfm_params& p = a.p;
+    const int H = p.H, W = p.W, B = p.B;
+    const TileGeom g = tile_geom(H, W);
+    __shared__ float red[NWAVE * 4];
+    const size_t plane = (size_t)H * W;
+    const int tiles = tiles_img(H, W);
+    const size_t pix = (size_t)g.gy * W + g.gx;
+    const float* img = a.in.tgt + (size_t)g.b * 3 * plane;
+    const bool hx = g.inside && g.gx < W - 1, hy = g.inside && g.gy < H - 1;
+    const float wx = hx ? edge_weight(img, plane, pix, pix + 1) : 0.0f;
+    const float wy = hy ? edge_weight(img, plane, pix, pix + W) : 0.0f;
+    for (int s = 0; s < p.S; ++s) {
+        const float* sg = pick4(a.in.sig, s) + (size_t)g.b * plane;
+        float v[3] = {0.0f, 0.0f, 0.0f};
+        if (g.inside) {
+            const float c = sg[pix];
+            v[0] = hx ? fabsf(c - sg[pix + 1]) * wx : 0.0f;
+            v[1] = hy ? fabsf(c - sg[pix + W]) * wy : 0.0f;
+            v[2] = c;
+        }
+        block_sum<3>(v, red);
+        if (threadIdx.x == 0) {
+            float* o = a.ws.smooth_part + (((size_t)s * B + g.b) * tiles + g.tile) * 4;
+            o[0] = v[0];
+            o[1] = v[1];
+            o[2] = v[2];
+            o[3] = 0.0f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_smooth_bwd(KArgs a) {
+    const psfm_params& p = a.p;
+    const int H = p.H, W = p.W, B = p.B;
+    const TileGeom g = tile_geom(H, W);
+    if (!g.inside) return;
+    const size_t plane = (size_t)H * W;
+    const size_t pix = (size_t)g.gy * W + g.gx;
+    const float* img = a.in.tgt + (size_t)g.b * 3 * plane;
+    const float gout = *a.grad_out;
+    const bool r = g.gx < W - 1, l = g.gx > 0, d = g.gy < H - 1, u = g.gy > 0;
+    const float wr = r ? edge_weight(img, plane, pix, pix + 1) : 0.0f;
+    const float wl = l ? edge_weight(img, plane, pix - 1, pix) : 0.0f;
+    const float wd = d ? edge_weight(img, plane, pix, pix + W) : 0.0f;
+    const float wu = u ? edge_weight(img, plane, pix - W, pix) : 0.0f;
+    for (int s = 0; s < p.S; ++s) {
+        const int gsi = p.scale0 + s;
+        const float* st = a.smooth_stats + ((size_t)gsi * B + g.b) * 4;  // Ax, Ay, m, m_clamped
+        const double base = (double)gout * p.smooth_w / ((double)p.n_scales * (double)(1 << gsi));
+        const float cx = (float)(base / ((double)B * H * (W - 1)));
+        const float cy = (float)(base / ((double)B * (H - 1) * W));
+        const float mc = st[3];
+        const float* sg = pick4(a.in.sig, s) + (size_t)g.b * plane;
+        const float c = sg[pix];
+        float gx = 0.0f, gy = 0.0f;
+        if (r) gx += sgnf(c - sg[pix + 1]) * wr;
+        if (l) gx -= sgnf(sg[pix - 1] - c) * wl;
+        if (d) gy += sgnf(c - sg[pix + W]) * wd;
+        if (u) gy -= sgnf(sg[pix - W] - c) * wu;
+        float gsm = (cx * gx + cy * gy) / mc;
+        if (st[2] >= 1e-6f) gsm -= (cx * st[0] + cy * st[1]) / (mc * mc) / (float)(H * W);
+        pick4(a.grad_sig, s)[(size_t)g.b * plane + pix] += gsm;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Finalize: fixed-order reductions of the per-tile partials (one 1024-thread block, one wave per
+// item, fp64 accumulation).  out = {loss, metrics.photometric_loss, metrics.smoothness_loss}.
+// ---------------------------------------------------------------------------------------------
+struct FinCall {
+    const float* photo_part;
+    const float* smooth_part;
+    int S, scale0, B, H, W, tiles;
+    double photo_scale;
+};
+struct FinArgs {
+    FinCall c[MAXS];
+    int ncalls, n_scales, has_smooth;
+    float smooth_w;
+    float* smooth_stats;
+    float* out;
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void k_finalize(FinArgs f) {
+    // items: photo (call, s) and smooth (call, s, b); smooth item stores 3 sums
+    __shared__ double photo_item[MAXS * MAXS];
+    __shared__ double smooth_item[MAXS * MAXS * 64][3];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int item = 0;
+    for (int ci = 0; ci < f.ncalls; ++ci) {
+        const FinCall& c = f.c[ci];
+        const int nparts = c.B * c.tiles;
+        for (int s = 0; s < c.S; ++s, ++item) {
+            if (item % nw != wave) continue;
+            double acc = 0.0;
+            for (int k = lane; k < nparts; k += 64) acc += (double)c.photo_part[(size_t)s * nparts + k];
+            acc = wave_sum_d(acc);
+            if (lane == 0) photo_item[ci * MAXS + s] = acc * c.photo_scale;
+        }
+    }
+    if (f.has_smooth) {
+        item = 0;
+        for (int ci = 0; ci < f.ncalls; ++ci) {
+            const FinCall& c = f.c[ci];
+            for (int s = 0; s < c.S; ++s)
+                for (int b = 0; b < c.B; ++b, ++item) {
+                    if (item % nw != wave) continue;
+                    const float* sp = c.smooth_part + ((size_t)s * c.B + b) * c.tiles * 4;
+                    double ax = 0.0, ay = 0.0, m = 0.0;
+                    for (int k = lane; k < c.tiles; k += 64) {
+                        ax += (double)sp[k * 4];
+                        ay += (double)sp[k * 4 + 1];
+                        m += (double)sp[k * 4 + 2];
+                    }
+                    ax = wave_sum_d(ax);
+                    ay = wave_sum_d(ay);
+                    m = wave_sum_d(m);
+                    if (lane == 0 && item < MAXS * MAXS * 64) {
+                        smooth_item[item][0] = ax;
+                        smooth_item[item][1] = ay;
+                        smooth_item[item][2] = m;
+                    }
+                }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double photo = 0.0;
+    for (int ci = 0; ci < f.ncalls; ++ci)
+        for (int s = 0; s < f.c[ci].S; ++s) photo += photo_item[ci * MAXS + s];
+    double smooth = 0.0;
+    if (f.has_smooth) {
+        item = 0;
+        for (int ci = 0; ci < f.ncalls; ++ci) {
+            const FinCall& c = f.c[ci];
+            for (int s = 0; s < c.S; ++s) {
+                const int gsi = c.scale0 + s;
+                double term = 0.0;
+                for (int b = 0; b < c.B; ++b, ++item) {
+                    const double ax = smooth_item[item][0], ay = smooth_item[item][1];
+                    const float m = (float)(smooth_item[item][2] / ((double)c.H * c.W));
+                    const float mc = fmaxf(m, 1e-6f);
+                    term += ax / ((double)c.B * c.H * (c.W - 1)) / mc + ay / ((double)c.B * (c.H - 1) * c.W) / mc;
+                    float* st = f.smooth_stats + ((size_t)gsi * c.B + b) * 4;
+                    st[0] = (float)ax;
+                    st[1] = (float)ay;
+                    st[2] = m;
+                    st[3] = mc;
+                }
+                smooth += term / (double)(1 << gsi);
+            }
+        }
+        smooth = (double)f.smooth_w * (smooth / (double)f.n_scales);
+    }
+    const float photo_f = (float)photo;
+    const float smooth_f = (float)smooth;
+    const float loss = f.has_smooth ? photo_f + smooth_f : photo_f;
+    f.out[0] = loss;
+    f.out[1] = loss;  // metrics['photometric_loss'] aliases the loss storage
+    f.out[2] = smooth_f;
+}
+
+// clip thresholds: thr[s][src] = mean + clip * std (unbiased) of each candidate map (:251-253)
+struct ThrArgs {
+    const float* part;
+    float* thr;
+    int S, nsrc, nparts;
+    double count;
+    float clip;
+};
+
+__global__ __launch_bounds__(1024) void k_clip_thr(ThrArgs t) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int item = wave; item < t.S * t.nsrc; item += nw) {
+        const float* pp = t.part + (size_t)item * t.nparts * 2;
+        double s1 = 0.0, s2 = 0.0;
+        for (int k = lane; k < t.nparts; k += 64) {
+            s1 += (double)pp[2 * k];
+            s2 += (double)pp[2 * k + 1];
+        }
+        s1 = wave_sum_d(s1);
+        s2 = wave_sum_d(s2);
+        if (lane == 0) {
+            const double mean = s1 / t.count;
+            const double var = fmax((s2 - s1 * mean) / (t.count - 1.0), 0.0);
+            t.thr[item] = (float)(mean + (double)t.clip * sqrt(var));
+        }
+    }
+}
+
+// dL/dT: sum over calls, scales and tiles (fixed order) -> grad_T [N][B][12]
+struct PoseRedCall {
+    const float* part;
+    int S, N, B, tiles;
+};
+struct PoseRedArgs {
+    PoseRedCall c[MAXS];
+    int ncalls, N, B;
+    float* grad_T;
+};
+
+__global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int item = blockIdx.x * nw + wave; item < r.N * r.B * 12; item += gridDim.x * nw) {
+        const int k = item % 12, jb = item / 12, b = jb % r.B, j = jb / r.B;
+        double acc = 0.0;
+        for (int ci = 0; ci < r.ncalls; ++ci) {
+            const PoseRedCall& c = r.c[ci];
+            for (int s = 0; s < c.S; ++s) {
+                const float* pp = c.part + (((size_t)(s * c.N + j) * c.B + b) * c.tiles) * 12;
+                double part = 0.0;
+                for (int t = lane; t < c.tiles; t += 64) part += (double)pp[(size_t)t * 12 + k];
+                acc += wave_sum_d(part);
+            }
+        }
+        if (lane == 0) r.grad_T[item] = (float)acc;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// standalone view_synthesis (camera_utils.py:27-59) forward / backward
+// ---------------------------------------------------------------------------------------------
+struct VSArgs {
+    int B, H, W;
+    const float* ref;
+    const float* depth;
+    const float* cam;
+    const float* grad_warped;
+    float* warped;
+    float* grad_depth;
+    float* pose_part;
+};
+
+__global__ __launch_bounds__(NT) void k_vs_fwd(VSArgs v) {
+    const TileGeom g = tile_geom(v.H, v.W);
+    if (!g.inside) return;
+    const size_t plane = (size_t)v.H * v.W, pix = (size_t)g.gy * v.W + g.gx;
+    CamRec cam;
+    load_cam(v.cam + (size_t)g.b * PSFM_CAMREC, cam);
+    Proj r;
+    project(cam, (float)g.gx, (float)g.gy, v.depth[(size_t)g.b * plane + pix], v.H, v.W, r);
+    float w[3];
+    bilinear3(v.ref + (size_t)g.b * 3 * plane, v.H, v.W, r.ix, r.iy, w);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v.warped[((size_t)g.b * 3 + c) * plane + pix] = w[c];
+}
+
+__global__ __launch_bounds__(NT) void k_vs_bwd(VSArgs v) {
+    const TileGeom g = tile_geom(v.H, v.W);
+    __shared__ float red[NWAVE * 12];
+    const size_t plane = (size_t)v.H * v.W, pix = (size_t)g.gy * v.W + g.gx;
+    CamRec cam;
+    load_cam(v.cam + (size_t)g.b * PSFM_CAMREC, cam);
+    float gT[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) gT[k] = 0.0f;
+    if (g.inside) {
+        const float d = v.depth[(size_t)g.b * plane + pix];
+        Proj r;
+        project(cam, (float)g.gx, (float)g.gy, d, v.H, v.W, r);
+        float gw[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) gw[c] = v.grad_warped[((size_t)g.b * 3 + c) * plane + pix];
+        float gix, giy;
+        bilinear3_grad_pos(v.ref + (size_t)g.b * 3 * plane, v.H, v.W, r.ix, r.iy, gw, gix, giy);
+        v.grad_depth[(size_t)g.b * plane + pix] = project_grad(cam, r, d, gix, giy, v.H, v.W, gT);
+    }
+    block_sum<12>(gT, red);
+    if (threadIdx.x == 0) {
+        float* o = v.pose_part + ((size_t)g.b * tiles_img(v.H, v.W) + g.tile) * 12;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) o[k] = gT[k];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+int validate(const psfm_params* p, const psfm_inputs* in) {
+    if (!p || !in) return fail(-1, "null params/inputs");
+    if (p->B < 1 || p->H < 2 || p->W < 2) return fail(-2, "bad B/H/W (need B>=1, H>=2, W>=2)");
+    if (p->N < 1 || p->N > MAXN) return fail(-3, "N (contexts) must be in [1, 4]");
+    if (p->S < 1 || p->S > MAXS) return fail(-4, "S (scales per call) must be in [1, 4]");
+    if (p->n_scales < 1 || p->n_scales > MAXS || p->scale0 < 0 || p->scale0 + p->S > p->n_scales)
+        return fail(-5, "scale0/S/n_scales inconsistent");
+    if (p->reduce_op != PSFM_REDUCE_MIN && p->reduce_op != PSFM_REDUCE_MEAN)
+        return fail(-6, "unknown reduce_op");
+    if (p->automask && p->reduce_op != PSFM_REDUCE_MIN)
+        return fail(-7, "For automasking only the min photometric_reduce_op is supported.");
+    if (!in->tgt || !in->cam) return fail(-8, "null tgt/cam");
+    for (int j = 0; j < p->N; ++j)
+        if (!in->ctx[j]) return fail(-9, "null context pointer");
+    for (int s = 0; s < p->S; ++s)
+        if (!in->sig[s]) return fail(-10, "null sigmoid pointer");
+    if ((long long)p->B * p->H * p->W > (1LL << 31)) return fail(-11, "image too large");
+    return 0;
+}
+
+dim3 tile_grid(const psfm_params* p) { return dim3(tiles_img(p->H, p->W), p->B); }
+
+}  // namespace
+
+extern "C" {
+
+int psfm_tiles_per_image(int H, int W) { return tiles_img(H, W); }
+
+int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes) {
+    if (!p) return fail(-1, "null params");
+    const size_t t = (size_t)tiles_img(p->H, p->W) * p->B;
+    const size_t ns = (size_t)n_src(*p);
+    if (photo) *photo = (size_t)p->S * t;
+    if (smooth) *smooth = (size_t)p->S * t * 4;
+    if (clip) *clip = (size_t)p->S * ns * t * 2;
+    if (clip_thr) *clip_thr = (size_t)p->S * ns;
+    if (pose) *pose = (size_t)p->S * p->N * t * 12;
+    if (argmin_bytes) *argmin_bytes = (size_t)p->S * p->B * p->H * p->W;
+    return 0;
+}
+
+int psfm_photometric_clip_stats(const psfm_params* p, const psfm_inputs* in,
+                                const psfm_workspace* ws, void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!ws || !ws->clip_part || !ws->clip_thr) return fail(-12, "null clip workspace");
+    KArgs a{};
+    a.p = *p;
+    a.in = *in;
+    a.ws = *ws;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->l1_only)
+        hipLaunchKernelGGL((k_photo_fwd<true, true>), tile_grid(p), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_photo_fwd<false, true>), tile_grid(p), dim3(NT), 0, st, a);
+    PSFM_LAUNCH_CHECK();
+    ThrArgs t{ws->clip_part, ws->clip_thr, p->S, n_src(*p), p->B * tiles_img(p->H, p->W),
+              (double)p->B * p->H * p->W * (p->l1_only ? 3.0 : 1.0), p->clip_loss};
+    hipLaunchKernelGGL(k_clip_thr, dim3(1), dim3(1024), 0, st, t);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_photometric_fwd(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                         void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!ws || !ws->photo_part || (p->reduce_op == PSFM_REDUCE_MIN && !ws->argmin))
+        return fail(-12, "null workspace");
+    if (p->clip_loss > 0.0f && !ws->clip_thr) return fail(-12, "clip needs clip_thr");
+    KArgs a{};
+    a.p = *p;
+    a.in = *in;
+    a.ws = *ws;
+    hipStream_t st = (hipStream_t)stream;
+    if (p->l1_only)
+        hipLaunchKernelGGL((k_photo_fwd<true, false>), tile_grid(p), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_photo_fwd<false, false>), tile_grid(p), dim3(NT), 0, st, a);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_smoothness_fwd(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                        void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!ws || !ws->smooth_part) return fail(-12, "null smoothness workspace");
+    KArgs a{};
+    a.p = *p;
+    a.in = *in;
+    a.ws = *ws;
+    hipLaunchKernelGGL(k_smooth_fwd, tile_grid(p), dim3(NT), 0, (hipStream_t)stream, a);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_finalize(int ncalls, const psfm_params* const* calls, const psfm_workspace* const* ws,
+                  float* smooth_stats, float* out, void* stream) {
+    if (ncalls < 1 || ncalls > MAXS || !calls || !ws || !out) return fail(-1, "bad finalize args");
+    FinArgs f{};
+    f.ncalls = ncalls;
+    f.n_scales = calls[0]->n_scales;
+    f.smooth_w = calls[0]->smooth_w;
+    f.has_smooth = calls[0]->smooth_w > 0.0f;
+    f.smooth_stats = smooth_stats;
+    f.out = out;
+    int items = 0;
+    for (int i = 0; i < ncalls; ++i) {
+        const psfm_params& p = *calls[i];
+        FinCall& c = f.c[i];
+        c.photo_part = ws[i]->photo_part;
+        c.smooth_part = ws[i]->smooth_part;
+        c.S = p.S;
+        c.scale0 = p.scale0;
+        c.B = p.B;
+        c.H = p.H;
+        c.W = p.W;
+        c.tiles = tiles_img(p.H, p.W);
+        const double cnt = (double)p.B * p.H * p.W;
+        c.photo_scale = (p.reduce_op == PSFM_REDUCE_MIN)
+                            ? 1.0 / ((double)p.n_scales * cnt)
+                            : 1.0 / ((double)p.n_scales * n_src(p) * cnt * (p.l1_only ? 3.0 : 1.0));
+        items += p.S * p.B;
+        if (f.has_smooth && (!c.smooth_part || !smooth_stats)) return fail(-12, "null smoothness buffers");
+    }
+    if (items > MAXS * MAXS * 64) return fail(-13, "too many (scale, batch) items");
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, (hipStream_t)stream, f);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                         const float* grad_out, float* const* grad_sig, void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!ws || !ws->pose_part || (p->reduce_op == PSFM_REDUCE_MIN && !ws->argmin))
+        return fail(-12, "null workspace");
+    if (!grad_out || !grad_sig) return fail(-14, "null grad buffers");
+    KArgs a{};
+    a.p = *p;
+    a.in = *in;
+    a.ws = *ws;
+    a.grad_out = grad_out;
+    for (int s = 0; s < p->S; ++s) {
+        if (!grad_sig[s]) return fail(-14, "null grad_sig");
+        a.grad_sig[s] = grad_sig[s];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (p->l1_only)
+        hipLaunchKernelGGL((k_photo_bwd<true>), tile_grid(p), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_photo_bwd<false>), tile_grid(p), dim3(NT), 0, st, a);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float* smooth_stats,
+                        const float* grad_out, float* const* grad_sig, void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!smooth_stats || !grad_out || !grad_sig) return fail(-14, "null smoothness grad buffers");
+    KArgs a{};
+    a.p = *p;
+    a.in = *in;
+    a.grad_out = grad_out;
+    a.smooth_stats = smooth_stats;
+    for (int s = 0; s < p->S; ++s) {
+        if (!grad_sig[s]) return fail(-14, "null grad_sig");
+        a.grad_sig[s] = grad_sig[s];
+    }
+    hipLaunchKernelGGL(k_smooth_bwd, tile_grid(p), dim3(NT), 0, (hipStream_t)stream, a);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
+                          const psfm_workspace* const* ws, float* grad_T, void* stream) {
+    if (ncalls < 1 || ncalls > MAXS || !calls || !ws || !grad_T) return fail(-1, "bad pose reduce args");
+    PoseRedArgs r{};
+    r.ncalls = ncalls;
+    r.N = calls[0]->N;
+    r.B = calls[0]->B;
+    r.grad_T = grad_T;
+    for (int i = 0; i < ncalls; ++i) {
+        if (calls[i]->N != r.N || calls[i]->B != r.B) return fail(-1, "calls disagree on N/B");
+        r.c[i] = PoseRedCall{ws[i]->pose_part, calls[i]->S, calls[i]->N, calls[i]->B,
+                             tiles_img(calls[i]->H, calls[i]->W)};
+    }
+    const int items = r.N * r.B * 12;
+    hipLaunchKernelGGL(k_pose_reduce, dim3((items + 3) / 4), dim3(256), 0, (hipStream_t)stream, r);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_view_synthesis_fwd(int B, int H, int W, const float* ref, const float* depth,
+                            const float* cam, float* warped, void* stream) {
+    if (B < 1 || H < 2 || W < 2 || !ref || !depth || !cam || !warped) return fail(-1, "bad view_synthesis args");
+    VSArgs v{B, H, W, ref, depth, cam, nullptr, warped, nullptr, nullptr};
+    hipLaunchKernelGGL(k_vs_fwd, dim3(tiles_img(H, W), B), dim3(NT), 0, (hipStream_t)stream, v);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_view_synthesis_bwd(int B, int H, int W, const float* ref, const float* depth,
+                            const float* cam, const float* grad_warped, float* grad_depth,
+                            float* pose_part, float* grad_T, void* stream) {
+    if (B < 1 || H < 2 || W < 2 || !ref || !depth || !cam || !grad_warped || !grad_depth || !pose_part || !grad_T)
+        return fail(-1, "bad view_synthesis_bwd args");
+    VSArgs v{B, H, W, ref, depth, cam, grad_warped, nullptr, grad_depth, pose_part};
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_vs_bwd, dim3(tiles_img(H, W), B), dim3(NT), 0, st, v);
+    PSFM_LAUNCH_CHECK();
+    PoseRedArgs r{};
+    r.ncalls = 1;
+    r.N = 1;
+    r.B = B;
+    r.grad_T = grad_T;
+    r.c[0] = PoseRedCall{pose_part, 1, 1, B, tiles_img(H, W)};
+    hipLaunchKernelGGL(k_pose_reduce, dim3((B * 12 + 3) / 4), dim3(256), 0, st, r);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+const char* psfm_last_error(void) { return g_err.c_str(); }
+const char* psfm_version(void) { return "psfm-gfx950 0.1"; }
+
+}  // extern "C"

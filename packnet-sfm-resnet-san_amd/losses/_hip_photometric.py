@@ -1,0 +1,195 @@
+"""torch.autograd.Function over the HIP photometric kernels (K1 forward, K2 backward,
+K3 smoothness, finalize / pose reduction) — DESIGN.md §Kernels.
+
+Replaces the autograd graph that the reference builds out of ~1.2k ATen ops per step in
+`MultiViewPhotometricLoss.forward` (losses/multiview_photometric_loss.py:331-410).
+Gradients flow to the sigmoid depth maps and to the [R|t] pose matrices (the images are
+data).
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from .. import _hip
+from ..geometry.camera_utils import scale_intrinsics, pinhole_inverse
+
+
+class _Call:
+    """One ABI call: scales that share an image size (one call for the full-res case)."""
+
+    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask):
+        B, _, H, W = image.shape
+        p = _hip.Params()
+        p.B, p.H, p.W, p.N, p.S = B, H, W, len(contexts), S
+        p.scale0, p.n_scales = scale0, cfg["n"]
+        p.automask, p.reduce_op = int(cfg["automask"]), cfg["reduce_op"]
+        p.l1_only = int(cfg["ssim_w"] <= 0.0)
+        p.ssim_w, p.C1, p.C2 = cfg["ssim_w"], cfg["C1"], cfg["C2"]
+        p.min_depth, p.max_depth = cfg["min_depth"], cfg["max_depth"]
+        p.clip_loss, p.smooth_w = cfg["clip"], cfg["smooth_w"]
+        self.params = p
+        self.image, self.contexts, self.sigs, self.cam, self.mask = image, contexts, sigs, cam, mask
+        inp = _hip.Inputs()
+        inp.tgt = image.data_ptr()
+        for j, c in enumerate(contexts):
+            inp.ctx[j] = c.data_ptr()
+        for s, t in enumerate(sigs):
+            inp.sig[s] = t.data_ptr()
+        inp.cam = cam.data_ptr()
+        inp.mask = mask.data_ptr() if mask is not None else None
+        self.inputs = inp
+        # workspace (caller-owned; sized by the library)
+        n = [ctypes.c_size_t() for _ in range(6)]
+        _hip.check(_hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]),
+                   "psfm_workspace_floats")
+        sizes = [x.value for x in n[:5]]
+        total = sum(sizes)
+        self.fbuf = torch.empty(total, device=image.device, dtype=torch.float32)
+        self.abuf = torch.empty(max(n[5].value, 1), device=image.device, dtype=torch.uint8)
+        ws = _hip.Workspace()
+        off = 0
+        base = self.fbuf.data_ptr()
+        for name, sz in zip(("photo_part", "smooth_part", "clip_part", "clip_thr", "pose_part"), sizes):
+            setattr(ws, name, base + 4 * off if sz else None)
+            off += sz
+        ws.argmin = self.abuf.data_ptr()
+        self.ws = ws
+
+
+def _to_size(t, hw, mode):
+    if tuple(t.shape[-2:]) == tuple(hw):
+        return t
+    if mode == "nearest":
+        return F.interpolate(t, size=tuple(hw), mode="nearest").contiguous()
+    return F.interpolate(t, size=tuple(hw), mode="bilinear", align_corners=True).contiguous()
+
+
+class PhotometricLossFn(torch.autograd.Function):
+    """loss, photometric metric, smoothness metric = f(sigs, T) given images and intrinsics."""
+
+    @staticmethod
+    def forward(ctx, cfg, image, mask, K, ref_K, T, n_ctx, *rest):
+        contexts = [c.contiguous() for c in rest[:n_ctx]]
+        sigs = [s.contiguous() for s in rest[n_ctx:]]
+        image = image.contiguous()
+        _hip.require_device(image, mask, T, *contexts, *sigs)
+        dev = image.device
+        B, _, H, W = image.shape
+        N, n = len(contexts), len(sigs)
+        Tf = T.detach().reshape(N, B, 12).float()
+
+        # group consecutive scales of equal size into one call (full-res: one call for all)
+        groups, s0 = [], 0
+        while s0 < n:
+            s1 = s0 + 1
+            while s1 < n and sigs[s1].shape[-2:] == sigs[s0].shape[-2:] and s1 - s0 < _hip.MAX_SCALES:
+                s1 += 1
+            groups.append((s0, s1))
+            s0 = s1
+        calls = []
+        for (a, b) in groups:
+            hw = sigs[a].shape[-2:]
+            scale = hw[1] / float(W)  # Camera.scaled(DW/W) (camera.py:84-108)
+            Kt = scale_intrinsics(K.clone(), scale, scale) if scale != 1.0 else K
+            Kr = scale_intrinsics(ref_K.clone(), scale, scale) if scale != 1.0 else ref_K
+            kinv = pinhole_inverse(Kt.float()).reshape(1, 1, B, 9).expand(b - a, N, B, 9)
+            kref = Kr.float().reshape(1, 1, B, 9).expand(b - a, N, B, 9)
+            tt = Tf.reshape(1, N, B, 12).expand(b - a, N, B, 12)
+            pad = torch.zeros(b - a, N, B, _hip.CAMREC - 30, device=dev, dtype=torch.float32)
+            cam = torch.cat([kinv, kref, tt, pad], -1).contiguous()
+            im = _to_size(image, hw, "bilinear")
+            cx = [_to_size(c, hw, "bilinear") for c in contexts]
+            mk = _to_size(mask, hw, "nearest").contiguous() if mask is not None else None
+            calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk))
+
+        L = _hip.lib()
+        st = _hip.stream(dev)
+        for c in calls:
+            if cfg["clip"] > 0.0:
+                _hip.check(L.psfm_photometric_clip_stats(ctypes.byref(c.params), ctypes.byref(c.inputs),
+                                                          ctypes.byref(c.ws), st), "clip_stats")
+            _hip.check(L.psfm_photometric_fwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
+                                              ctypes.byref(c.ws), st), "photometric_fwd")
+            if cfg["smooth_w"] > 0.0:
+                _hip.check(L.psfm_smoothness_fwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
+                                                 ctypes.byref(c.ws), st), "smoothness_fwd")
+        smooth_stats = torch.empty(cfg["n"] * B * 4, device=dev, dtype=torch.float32)
+        out = torch.empty(3, device=dev, dtype=torch.float32)
+        pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
+        wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
+        _hip.check(L.psfm_finalize(len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st),
+                   "finalize")
+        ctx.calls, ctx.smooth_stats, ctx.cfg, ctx.n_ctx, ctx.T_shape = calls, smooth_stats, cfg, N, T.shape
+        ctx.sig_shapes = [s.shape for s in sigs]
+        loss, photo, smooth = out[0:1], out[1].clone(), out[2].clone()
+        ctx.mark_non_differentiable(photo, smooth)
+        return loss, photo, smooth
+
+    @staticmethod
+    def backward(ctx, g_loss, g_photo, g_smooth):
+        calls, cfg = ctx.calls, ctx.cfg
+        dev = calls[0].image.device
+        gout = (g_loss if g_loss is not None else torch.zeros(1, device=dev)).reshape(1).float().contiguous()
+        L = _hip.lib()
+        st = _hip.stream(dev)
+        grads = []
+        for c in calls:
+            gsig = [torch.empty(sh, device=dev, dtype=torch.float32) for sh in
+                    ctx.sig_shapes[c.params.scale0:c.params.scale0 + c.params.S]]
+            arr = (ctypes.c_void_p * _hip.MAX_SCALES)(*([g.data_ptr() for g in gsig] +
+                                                         [None] * (_hip.MAX_SCALES - len(gsig))))
+            _hip.check(L.psfm_photometric_bwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
+                                              ctypes.byref(c.ws), _hip.ptr(gout), arr, st), "photometric_bwd")
+            if cfg["smooth_w"] > 0.0:
+                _hip.check(L.psfm_smoothness_bwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
+                                                 _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st),
+                           "smoothness_bwd")
+            grads.extend(gsig)
+        N, B = ctx.n_ctx, calls[0].params.B
+        gT = torch.empty(N, B, 12, device=dev, dtype=torch.float32)
+        pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
+        wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
+        _hip.check(L.psfm_pose_grad_reduce(len(calls), pp, wp, _hip.ptr(gT), st), "pose_grad_reduce")
+        return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
+
+
+def photometric_loss_hip(image, contexts, sigs, K, ref_K, T, mask, cfg):
+    """Returns (loss[1], metrics.photometric_loss, metrics.smoothness_loss)."""
+    return PhotometricLossFn.apply(cfg, image, mask, K, ref_K, T, len(contexts), *contexts, *sigs)
+
+
+# -------------------------------------------------------------------------------------------------
+class ViewSynthesisFn(torch.autograd.Function):
+    """view_synthesis (geometry/camera_utils.py:27-59) on HIP: grads to depth and [R|t]."""
+
+    @staticmethod
+    def forward(ctx, ref_image, depth, Kinv, Kref, T):
+        ref_image, depth = ref_image.contiguous(), depth.contiguous()
+        _hip.require_device(ref_image, depth)
+        B, _, H, W = ref_image.shape
+        pad = torch.zeros(B, _hip.CAMREC - 30, device=depth.device)
+        cam = torch.cat([Kinv.reshape(B, 9).float(), Kref.reshape(B, 9).float(),
+                         T.detach().reshape(B, 12).float(), pad], -1).contiguous()
+        warped = torch.empty_like(ref_image)
+        _hip.check(_hip.lib().psfm_view_synthesis_fwd(B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
+                                                      _hip.ptr(cam), _hip.ptr(warped),
+                                                      _hip.stream(depth.device)), "view_synthesis_fwd")
+        ctx.save_for_backward(ref_image, depth, cam)
+        ctx.T_shape = T.shape
+        return warped
+
+    @staticmethod
+    def backward(ctx, g):
+        ref_image, depth, cam = ctx.saved_tensors
+        B, _, H, W = ref_image.shape
+        g = g.contiguous().float()
+        gd = torch.empty_like(depth)
+        tiles = _hip.tiles_per_image(H, W)
+        part = torch.empty(B * tiles * 12, device=depth.device)
+        gT = torch.empty(B, 12, device=depth.device)
+        _hip.check(_hip.lib().psfm_view_synthesis_bwd(B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
+                                                      _hip.ptr(cam), _hip.ptr(g), _hip.ptr(gd),
+                                                      _hip.ptr(part), _hip.ptr(gT),
+                                                      _hip.stream(depth.device)), "view_synthesis_bwd")
+        return None, gd, None, None, gT.reshape(ctx.T_shape)

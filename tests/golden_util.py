@@ -1,0 +1,101 @@
+"""Shared, reference-independent helpers for golden fixtures.
+
+Used by `tools/gen_goldens.py` (which produces the fixtures from the reference
+in the build container) and by the tests that consume them.  Nothing here
+imports the reference.
+"""
+import math
+import zlib
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+GOLDEN_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden")
+
+# Normalised KITTI intrinsics: fx=0.58W, fy=1.92H, cx=cy=0.5.
+KITTI_FX, KITTI_FY = 0.58, 1.92
+
+
+def kitti_K(B, H, W, dtype=torch.float32):
+    K = torch.tensor([[KITTI_FX * W, 0.0, 0.5 * W],
+                      [0.0, KITTI_FY * H, 0.5 * H],
+                      [0.0, 0.0, 1.0]], dtype=dtype)
+    return K.unsqueeze(0).repeat(B, 1, 1).contiguous()
+
+
+def smooth_texture(g, B, C, H, W):
+    """Smooth image in [0,1]: bilinear-upsampled coarse U[0,1] noise + fine detail."""
+    h, w = max(H // 8, 2), max(W // 8, 2)
+    base = torch.rand(B, C, h, w, generator=g)
+    img = F.interpolate(base, size=(H, W), mode="bilinear", align_corners=False)
+    img = img + 0.05 * torch.randn(B, C, H, W, generator=g)
+    return img.clamp(0.0, 1.0).contiguous()
+
+
+def pose_vecs(g, B, N=2):
+    """[B,N,6] pose vectors: context 0 backward (-tz), context 1 forward (+tz)."""
+    tz = 0.5 + torch.rand(B, generator=g)
+    vec = torch.zeros(B, N, 6)
+    for j in range(N):
+        sign = -1.0 if j % 2 == 0 else 1.0
+        vec[:, j, 2] = sign * tz
+        vec[:, j, 0:2] = 0.05 * torch.randn(B, 2, generator=g)
+        vec[:, j, 3:6] = 0.005 * torch.randn(B, 3, generator=g)
+    return vec
+
+
+def sigmoid_maps(g, B, H, W, lo=0.01, hi=0.2, smooth=True):
+    """Sigmoid-space depth maps in [lo, hi]; smooth so that depth varies gently."""
+    if smooth:
+        t = smooth_texture(g, B, 1, H, W)
+    else:
+        t = torch.rand(B, 1, H, W, generator=g)
+    return (lo + (hi - lo) * t).contiguous()
+
+
+def det_init_(module):
+    """Deterministic, RNG-order-independent parameter fill keyed by parameter name.
+
+    Lets the build's network (same parameter names as the reference, see
+    `packnet_sfm_amd/networks`) be loaded with the exact weights the golden
+    was generated with, without shipping a checkpoint.
+    """
+    with torch.no_grad():
+        for name, p in sorted(module.named_parameters()):
+            g = torch.Generator().manual_seed(zlib.crc32(name.encode()) & 0x7FFFFFFF)
+            if p.dim() >= 2:
+                fan_in = p[0].numel()
+                fan_out = p.shape[0] * (p[0].numel() // max(p.shape[1], 1))
+                bound = math.sqrt(6.0 / (fan_in + fan_out))
+                p.copy_((torch.rand(p.shape, generator=g) * 2 - 1) * bound)
+            elif name.endswith("weight"):
+                p.copy_(1.0 + 0.1 * (torch.rand(p.shape, generator=g) - 0.5))
+            else:
+                p.copy_(0.02 * (torch.rand(p.shape, generator=g) - 0.5))
+
+
+def load_golden(name):
+    path = __import__("os").path.join(GOLDEN_DIR, name + ".npz")
+    with np.load(path, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+def grad_check(got, ref, sensitive=None, tol=1e-3):
+    """Per-pixel gradient parity: |got-ref| <= tol*max|ref| on every pixel that is not flagged
+    sensitive (oracle.sensitive_pixels: bilinear kinks / min near-ties).  Returns (ok, msg)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    d = np.abs(got - ref)
+    lim = tol * max(np.abs(ref).max(), 1e-20)
+    bad = d > lim
+    if sensitive is not None:
+        bad &= ~np.asarray(sensitive, dtype=bool)
+    n = int(bad.sum())
+    return n == 0, f"{n} pixels over {tol:g}*max (max err {d.max():.3e}, lim {lim:.3e})"

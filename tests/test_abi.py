@@ -1,0 +1,74 @@
+"""CPU checks of the drop-in boundary: the C-ABI library builds, loads, exports every symbol
+include/psfm.h declares, and rejects bad arguments without touching a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd import _hip
+    return _hip
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "psfm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_every_declared_symbol_is_exported(hip):
+    L = hip.lib()
+    decl = declared_functions()
+    assert len(decl) >= 12
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(hip.EXPORTED) == decl
+
+
+def test_workspace_sizes(hip):
+    p = hip.Params(B=4, H=192, W=640, N=2, S=4, scale0=0, n_scales=4, automask=1, reduce_op=0)
+    n = [ctypes.c_size_t() for _ in range(6)]
+    assert hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]) == 0
+    tiles = hip.tiles_per_image(192, 640)
+    assert tiles == 10 * 48
+    assert n[0].value == 4 * 4 * tiles
+    assert n[4].value == 4 * 2 * 4 * tiles * 12
+    assert n[5].value == 4 * 4 * 192 * 640
+
+
+@pytest.mark.parametrize("field,value,code", [("N", 0, -3), ("N", 5, -3), ("S", 0, -4), ("H", 1, -2),
+                                              ("reduce_op", 7, -6)])
+def test_bad_arguments_are_rejected(hip, field, value, code):
+    p = hip.Params(B=1, H=8, W=8, N=2, S=1, scale0=0, n_scales=1, automask=1, reduce_op=0)
+    setattr(p, field, value)
+    inp, ws = hip.Inputs(), hip.Workspace()
+    rc = hip.lib().psfm_photometric_fwd(ctypes.byref(p), ctypes.byref(inp), ctypes.byref(ws), None)
+    assert rc == code
+    assert hip.lib().psfm_last_error()
+
+
+def test_automask_requires_min(hip):
+    p = hip.Params(B=1, H=8, W=8, N=2, S=1, scale0=0, n_scales=1, automask=1, reduce_op=1)
+    rc = hip.lib().psfm_photometric_fwd(ctypes.byref(p), ctypes.byref(hip.Inputs()),
+                                        ctypes.byref(hip.Workspace()), None)
+    assert rc == -7
+    assert b"min" in hip.lib().psfm_last_error()
+
+
+def test_product_path_refuses_cpu_tensors(hip):
+    import torch
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    B, H, W = 1, 8, 16
+    fn = MultiViewPhotometricLoss(photometric_reduce_op="min", automask_loss=True)
+    with pytest.raises(RuntimeError, match="ROCm"):
+        fn(torch.rand(B, 3, H, W), [torch.rand(B, 3, H, W)] * 2, [torch.rand(B, 1, H, W)] * 4,
+           torch.eye(3).expand(B, 3, 3), torch.eye(3).expand(B, 3, 3),
+           [Pose.identity(B)] * 2)

@@ -1,0 +1,203 @@
+"""GPU parity of the HIP photometric path (K1/K2/K3 via the C-ABI) against the reference's
+golden fixtures and the CPU oracle.
+
+Tolerances (BASELINE.json north_star: 1e-4 rel fp32):
+  * loss / metrics: 1e-4 relative;
+  * dL/dsig: every pixel within 1e-3 * max|g|, except pixels that oracle.sensitive_pixels flags
+    (bilinear kinks: a sampling coordinate within 1e-5 px of an integer, where grid_sample's
+    derivative jumps; min-reprojection near-ties within 1e-5 and their SSIM window).  There two
+    fp32 implementations legitimately differ — ATen-GPU vs ATen-CPU shows the same effect
+    (tools/debug_grads.py);
+  * dL/dpose: 1e-3 relative on inputs with no sensitive pixel (test_kink_free_*); on golden
+    inputs that contain kinks, 2e-2 (one kink pixel moves the 24x80 pose gradient by ~1e-2).
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+LOSS_TOL, GRAD_TOL = 1e-4, 1e-3
+CASES = ["default", "mindepth0", "no_automask", "reduce_mean", "rand_mask", "clip", "l1_only",
+         "multires", "one_ctx", "wide_motion"]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import __graft_entry__
+    __graft_entry__.build()
+    return torch.device("cuda:0")
+
+
+def _T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _kw(z):
+    return {k: eval(v) for k, v in zip(z["kwargs_keys"], z["kwargs_vals"])}
+
+
+def run_hip_case(z, dev, mask_none=False):
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    kw = _kw(z)
+    nctx = sum(1 for k in z if k.startswith("ctx"))
+    S = kw["num_scales"]
+    sigs = [_T(z[f"sig{i}"], dev).requires_grad_(True) for i in range(S)]
+    vec = _T(z["vec"], dev).requires_grad_(True)
+    loss_fn = MultiViewPhotometricLoss(**kw)
+    out = loss_fn(_T(z["image"], dev), [_T(z[f"ctx{j}"], dev) for j in range(nctx)], sigs,
+                  _T(z["K"], dev), _T(z["K"], dev), [Pose.from_vec(vec[:, j], "euler") for j in range(nctx)],
+                  mask=None if mask_none else _T(z["mask"], dev))
+    out["loss"].sum().backward()
+    torch.cuda.synchronize()
+    return out, sigs, vec
+
+
+def _sensitive(z):
+    from oracle import photometric_oracle as O
+    kw = _kw(z)
+    nctx = sum(1 for k in z if k.startswith("ctx"))
+    T = torch.from_numpy
+    sigs = [T(z[f"sig{i}"]) for i in range(kw["num_scales"])]
+    if any(s.shape[-2:] != sigs[0].shape[-2:] for s in sigs):
+        return None  # multi-resolution: check without exclusions
+    return [m.numpy() for m in O.sensitive_pixels(
+        T(z["image"]), [T(z[f"ctx{j}"]) for j in range(nctx)], sigs, T(z["K"]),
+        [O.pose_vec_to_mat(T(z["vec"])[:, j]) for j in range(nctx)], kw["min_depth"], kw["max_depth"],
+        kw["automask_loss"], kw["ssim_loss_weight"])]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_loss_and_grads_match_reference_golden(dev, case):
+    z = gu.load_golden(f"loss_{case}")
+    out, sigs, vec = run_hip_case(z, dev)
+    assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
+    assert gu.rel_err(out["metrics"]["photometric_loss"].cpu(), z["photometric_loss"]) < LOSS_TOL
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < LOSS_TOL
+    sens = _sensitive(z)
+    for i, s in enumerate(sigs):
+        ok, msg = gu.grad_check(s.grad.cpu(), z[f"grad_sig{i}"], None if sens is None else sens[i], GRAD_TOL)
+        assert ok, f"dL/dsig{i}: {msg}"
+    n_sens = 0 if sens is None else int(sum(m.sum() for m in sens))
+    assert gu.rel_err(vec.grad.cpu(), z["grad_vec"]) < (GRAD_TOL if n_sens == 0 else 2e-2)
+
+
+def _seeded_inputs(seed, B, H, W, nctx=2):
+    g = torch.Generator().manual_seed(seed)
+    image = gu.smooth_texture(g, B, 3, H, W)
+    ctx = [gu.smooth_texture(g, B, 3, H, W) for _ in range(nctx)]
+    return image, ctx, gu.kitti_K(B, H, W), gu.pose_vecs(g, B, nctx), [gu.sigmoid_maps(g, B, H, W) for _ in range(4)]
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 24, 80), (1, 37, 101), (3, 12, 64), (1, 48, 130)])
+def test_kink_free_inputs_match_oracle_tightly(dev, B, H, W):
+    """Seeded inputs with NO kink / near-tie pixel: every gradient entry within 1e-3 of the oracle."""
+    from oracle import photometric_oracle as O
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    for seed in range(100, 160):
+        image, ctx, K, vec, sigs = _seeded_inputs(seed, B, H, W)
+        mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+        sens = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0)
+        if not any(bool(m.any()) for m in sens):
+            break
+    else:
+        pytest.skip("no kink-free seed found")
+    s_c = [s.clone().requires_grad_(True) for s in sigs]
+    v_c = vec.clone().requires_grad_(True)
+    ref = O.photometric_loss(image, ctx, s_c, K, K, [O.pose_vec_to_mat(v_c[:, j]) for j in range(2)], None)
+    ref[0].sum().backward()
+    s_d = [s.to(dev).requires_grad_(True) for s in sigs]
+    v_d = vec.to(dev).requires_grad_(True)
+    fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
+                                  photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
+                                  min_depth=0.5, max_depth=80.0)
+    out = fn(image.to(dev), [c.to(dev) for c in ctx], s_d, K.to(dev), K.to(dev),
+             [Pose.from_vec(v_d[:, j], "euler") for j in range(2)])
+    out["loss"].sum().backward()
+    assert gu.rel_err(out["loss"].detach().cpu(), ref[0].detach()) < LOSS_TOL
+    for i in range(4):
+        ok, msg = gu.grad_check(s_d[i].grad.cpu(), s_c[i].grad, None, GRAD_TOL)
+        assert ok, f"seed {seed} dL/dsig{i}: {msg}"
+    assert gu.rel_err(v_d.grad.cpu(), v_c.grad) < GRAD_TOL, f"seed {seed}"
+
+
+def test_mask_none_equals_ones_mask(dev):
+    z = gu.load_golden("loss_default")
+    a, _, _ = run_hip_case(z, dev, mask_none=True)
+    assert gu.rel_err(a["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
+
+
+def test_deterministic_bitwise(dev):
+    z = gu.load_golden("loss_default")
+    a, sa, va = run_hip_case(z, dev)
+    b, sb, vb = run_hip_case(z, dev)
+    assert torch.equal(a["loss"], b["loss"])
+    assert all(torch.equal(x.grad, y.grad) for x, y in zip(sa, sb))
+    assert torch.equal(va.grad, vb.grad)
+
+
+def test_kitti_full_res_golden(dev):
+    """B=1, 192x640 (BASELINE config shape): scalars, grad norms and sampled pixels."""
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    z = gu.load_golden("loss_kitti_1img")
+    B, H, W = 1, 192, 640
+    g = torch.Generator().manual_seed(int(z["seed"]))
+    image = gu.smooth_texture(g, B, 3, H, W)
+    ctx = [gu.smooth_texture(g, B, 3, H, W) for _ in range(2)]
+    K = gu.kitti_K(B, H, W)
+    vec = gu.pose_vecs(g, B, 2)
+    sigs = [gu.sigmoid_maps(g, B, H, W) for _ in range(4)]
+    s_d = [s.to(dev).requires_grad_(True) for s in sigs]
+    v_d = vec.to(dev).requires_grad_(True)
+    fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
+                                  photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
+                                  min_depth=0.5, max_depth=80.0)
+    out = fn(image.to(dev), [c.to(dev) for c in ctx], s_d, K.to(dev), K.to(dev),
+             [Pose.from_vec(v_d[:, j], "euler") for j in range(2)], mask=torch.ones(B, 1, H, W, device=dev))
+    out["loss"].sum().backward()
+    assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < LOSS_TOL
+    # 983k warp evaluations: kinks and near-ties always exist at this size; ATen-GPU vs the CPU
+    # golden differs by 2.8e-3 on this pose gradient (tools/debug_grads.py) -> 5e-3 here
+    assert gu.rel_err(v_d.grad.cpu(), z["grad_vec"]) < 5e-3
+    from oracle import photometric_oracle as O
+    sens = O.sensitive_pixels(image, ctx, sigs, K, [O.pose_vec_to_mat(vec[:, j]) for j in range(2)], 0.5, 80.0)
+    s_c = [s.clone().requires_grad_(True) for s in sigs]
+    ref = O.photometric_loss(image, ctx, s_c, K, K, [O.pose_vec_to_mat(vec[:, j]) for j in range(2)], None)
+    ref[0].sum().backward()
+    idx = torch.from_numpy(z["sample_idx"])
+    for i in range(4):
+        g_cpu = s_c[i].grad.reshape(-1)
+        assert gu.rel_err(g_cpu[idx], z[f"grad_sig{i}_samples"]) < 1e-3   # oracle == reference here
+        ok, msg = gu.grad_check(s_d[i].grad.cpu(), s_c[i].grad, sens[i], GRAD_TOL)
+        assert ok, f"dL/dsig{i}: {msg}"
+
+
+def test_view_synthesis_matches_reference(dev):
+    from packnet_sfm_amd.geometry.camera import Camera
+    from packnet_sfm_amd.geometry.camera_utils import view_synthesis
+    from packnet_sfm_amd.geometry.pose import Pose
+    z = gu.load_golden("geom_small")
+    K = _T(z["K"], dev)
+    depth = _T(z["depth"], dev).requires_grad_(True)
+    vec = _T(z["vec"], dev).requires_grad_(True)
+    warped = view_synthesis(_T(z["ref"], dev), depth, Camera(K=K, Tcw=Pose.from_vec(vec, "euler")), Camera(K=K))
+    assert gu.rel_err(warped.detach().cpu(), z["warped"]) < 1e-4
+    # gradient against the oracle's autograd
+    from oracle import photometric_oracle as O
+    d_c = torch.from_numpy(z["depth"]).requires_grad_(True)
+    v_c = torch.from_numpy(z["vec"]).requires_grad_(True)
+    ref = O.synthesize(torch.from_numpy(z["ref"]), d_c, torch.from_numpy(z["K"]), torch.from_numpy(z["K"]),
+                       O.pose_vec_to_mat(v_c))
+    wgt = torch.linspace(0.5, 1.5, ref.numel()).reshape(ref.shape)
+    (ref * wgt).sum().backward()
+    (warped * wgt.to(dev)).sum().backward()
+    assert gu.rel_err(depth.grad.cpu(), d_c.grad) < GRAD_TOL
+    assert gu.rel_err(vec.grad.cpu(), v_c.grad) < GRAD_TOL

@@ -1,0 +1,101 @@
+"""Pin the CPU oracle (oracle/photometric_oracle.py) to the reference's golden fixtures.
+
+The fixtures were produced by importing /root/reference in the build container
+(tools/gen_goldens.py).  Tolerance: 1e-4 relative, fp32 (BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+from oracle import photometric_oracle as O
+
+TOL = 1e-4
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def test_geometry_matches_reference():
+    z = gu.load_golden("geom_small")
+    mat = O.pose_vec_to_mat(T(z["vec"]))
+    assert gu.rel_err(mat, z["pose_mat"]) < 1e-6
+    X = O.lift(T(z["depth"]), T(z["K"]))
+    assert gu.rel_err(X, z["points"]) < 1e-6
+    grid = O.project_to_grid(X, T(z["K"]), mat)
+    assert gu.rel_err(grid, z["coords"]) < 1e-5
+    warped = O.synthesize(T(z["ref"]), T(z["depth"]), T(z["K"]), T(z["K"]), mat)
+    assert gu.rel_err(warped, z["warped"]) < 1e-5
+    assert gu.rel_err(O.scale_K(T(z["K"]), 0.5), z["K_half"]) < 1e-7
+
+
+def test_ssim_matches_reference():
+    z = gu.load_golden("ssim_small")
+    x, y = T(z["x"]), T(z["y"])
+    assert gu.rel_err(O.ssim_map(x, y), z["ssim"]) < 1e-5
+    assert gu.rel_err(O.photometric_map(x, y, 0.85, 1e-4, 9e-4), z["photo"]) < 1e-5
+
+
+def _kwargs(z):
+    kw = {k: eval(v) for k, v in zip(z["kwargs_keys"], z["kwargs_vals"])}  # repr of literals only
+    return dict(num_scales_=kw["num_scales"], ssim_loss_weight=kw["ssim_loss_weight"],
+                smooth_loss_weight=kw["smooth_loss_weight"], C1=kw["C1"], C2=kw["C2"],
+                photometric_reduce_op=kw["photometric_reduce_op"], clip_loss=kw["clip_loss"],
+                automask_loss=kw["automask_loss"], min_depth=kw["min_depth"], max_depth=kw["max_depth"])
+
+
+LOSS_CASES = ["default", "mindepth0", "no_automask", "reduce_mean", "rand_mask", "clip", "l1_only",
+              "multires", "one_ctx", "wide_motion"]
+
+
+@pytest.mark.parametrize("case", LOSS_CASES)
+def test_loss_matches_reference(case):
+    z = gu.load_golden(f"loss_{case}")
+    kw = _kwargs(z)
+    nctx = sum(1 for k in z if k.startswith("ctx"))
+    S = kw["num_scales_"]
+    sigs = [T(z[f"sig{i}"]).requires_grad_(True) for i in range(S)]
+    vec = T(z["vec"]).requires_grad_(True)
+    mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(nctx)]
+    loss, photo, smooth, reduced = O.photometric_loss(
+        T(z["image"]), [T(z[f"ctx{j}"]) for j in range(nctx)], sigs, T(z["K"]), T(z["K"]), mats,
+        mask=T(z["mask"]), **kw)
+    loss.sum().backward()
+    assert gu.rel_err(loss.detach(), z["loss"]) < TOL
+    assert gu.rel_err(photo.detach(), z["photometric_loss"]) < TOL
+    assert gu.rel_err(smooth.detach(), z["smoothness_loss"]) < TOL
+    for i in range(S):
+        assert gu.rel_err(sigs[i].grad, z[f"grad_sig{i}"]) < 1e-3, i
+        if f"min{i}" in z:
+            assert gu.rel_err(reduced[i].detach(), z[f"min{i}"]) < TOL
+    assert gu.rel_err(vec.grad, z["grad_vec"]) < 1e-3
+
+
+def test_depth_conversions_known_answers():
+    # reference docstring known answers: utils/post_process_depth.py:44-49, :96-100
+    s = torch.tensor([0.0, 0.5, 1.0])
+    assert torch.allclose(O.sigmoid_to_depth(s, 0.05, 80.0), torch.tensor([80.0, 0.0999, 0.05]), rtol=1e-3)
+    assert torch.allclose(O.sigmoid_to_inv(s, 0.05, 80.0), torch.tensor([0.0125, 10.00625, 20.0]), rtol=1e-5)
+    z = gu.load_golden("depth_metrics")
+    sg = T(z["sig"])
+    assert gu.rel_err(O.sigmoid_to_depth(sg, 0.05, 80.0), z["depth_lin"]) < 1e-6
+    assert gu.rel_err(O.sigmoid_to_depth(sg, 0.0, 80.0), z["depth_lin_0"]) < 1e-6
+    assert gu.rel_err(O.sigmoid_to_inv(sg, 0.05, 80.0), z["inv_lin"]) < 1e-6
+
+
+def _metrics_inputs():
+    g = torch.Generator().manual_seed(31)
+    B, H, W = 2, 192, 640
+    gt = 1.0 + 79.0 * torch.rand(B, 1, H, W, generator=g)
+    gt[torch.rand(B, 1, H, W, generator=g) < 0.6] = 0.0
+    pred = gt.clamp(min=1.0) * (1.0 + 0.1 * torch.randn(B, 1, H, W, generator=g)) * 1.3
+    return gt, pred.clamp(0.5, 90.0)
+
+
+def test_depth_metrics_match_reference():
+    z = gu.load_golden("depth_metrics")
+    gt, pred = _metrics_inputs()
+    assert gu.rel_err(O.depth_metrics(gt, pred, 0.0, 80.0, "garg", True), z["with_scale"]) < 1e-5
+    assert gu.rel_err(O.depth_metrics(gt, pred, 0.0, 80.0, "garg", False), z["no_scale"]) < 1e-5
+    assert gu.rel_err(O.depth_metrics(gt, pred, 1e-3, 80.0, "", True), z["no_crop"]) < 1e-5
