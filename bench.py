@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Self-supervised depth training step throughput (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE.json configs[1]): SelfSupModel = ResNetSAN01('18A') depth net + PoseNet,
+KITTI-shaped 192x640 RGB triplets (target + 2 contexts), per-GPU batch 4, 4 full-resolution
+scales, automask + min-reprojection, Adam.  Nets under bf16 autocast (MIOpen); the photometric
+loss (view synthesis + SSIM/L1 + min + smoothness, fwd+bwd) runs in fp32 on the HIP kernels.
+
+  python bench.py [--gpus N --steps K --warmup W]          (N>1: launched by torch.distributed.run)
+
+Prints ONE JSON line on rank 0 with `roofline` (live HIP-event timing of the photometric kernel
+group K1+K2+K3) and `cpu_baseline` (the CPU restatement — same nets on CPU + oracle loss — timed
+on this host, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training images/sec (whole node), KITTI 640x192; Abs Rel parity vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LOSS_KW = dict(num_scales=4, ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4,
+               C2=9e-4, photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
+               padding_mode="zeros", automask_loss=True, min_depth=0.5, max_depth=80.0)
+N_CTX, N_SCALES = 2, 4
+
+
+def algorithmic_bytes_per_image(H, W, N=N_CTX, S=N_SCALES):
+    """fwd reads target 12 + contexts 12N + sigmoids 4S B/px; bwd re-reads
+    them and writes dL/dsig 4S B/px -> H*W*(2*12*(1+N) + 12*S) (= 120 B/px at N=2, S=4)."""
+    return H * W * (2 * 12 * (1 + N) + 12 * S)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4, help="per-GPU batch (train_resnet_san_kitti_tiny.yaml: 4)")
+    ap.add_argument("--height", type=int, default=192)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--depth-net", default="ResNetSAN01", choices=["ResNetSAN01", "PackNet01", "DepthResNet"])
+    ap.add_argument("--pose-net", default="PoseNet", choices=["PoseNet", "PoseResNet"])
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-kernel-timing", action="store_true", help="for rocprofv3 runs")
+    return ap.parse_args()
+
+
+def synthetic_batch(B, H, W, device, seed):
+    """Seeded KITTI-shaped batch (BASELINE.md plan): smooth textures in [0,1], 2 contexts, K."""
+    g = torch.Generator().manual_seed(seed)
+
+    def tex():
+        base = torch.rand(B, 3, max(H // 8, 2), max(W // 8, 2), generator=g)
+        img = torch.nn.functional.interpolate(base, size=(H, W), mode="bilinear", align_corners=False)
+        return (img + 0.05 * torch.randn(B, 3, H, W, generator=g)).clamp(0, 1)
+
+    rgb, ctx = tex(), [tex() for _ in range(N_CTX)]
+    K = torch.tensor([[0.58 * W, 0, 0.5 * W], [0, 1.92 * H, 0.5 * H], [0, 0, 1.0]]).repeat(B, 1, 1)
+    to = lambda t: t.to(device).contiguous()  # noqa: E731
+    rgb, ctx, K = to(rgb), [to(c) for c in ctx], to(K)
+    return dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K)
+
+
+def build_model(args, device):
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.models.SelfSupModel import SelfSupModel
+    from packnet_sfm_amd.networks import load_depth_net, load_pose_net
+    model = SelfSupModel(**LOSS_KW, upsample_depth_maps=True, rotation_mode="euler")
+    dkw = {"ResNetSAN01": dict(version="18A", min_depth=0.5, max_depth=80.0),
+           "PackNet01": dict(version="1A"), "DepthResNet": dict(version="18pt")}[args.depth_net]
+    model.add_depth_net(load_depth_net(args.depth_net, **dkw))
+    model.add_pose_net(load_pose_net(args.pose_net, **({"nb_ref_imgs": 2} if args.pose_net == "PoseNet"
+                                                        else {"version": "18pt"})))
+    return model.to(device).train()
+
+
+def cpu_baseline(args):
+    """The reference's CPU training step restated: the same nets on CPU in fp32 + the oracle loss
+    (oracle/photometric_oracle.py, fixture-proven equal to the reference), Adam step."""
+    from oracle import photometric_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    dev = torch.device("cpu")
+    model = build_model(args, dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=1234)
+    kw = dict(num_scales_=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
+              automask_loss=True, clip_loss=0.0, min_depth=0.5, max_depth=80.0)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        inv = model.depth_net(batch["rgb"])["inv_depths"]
+        inv = [torch.nn.functional.interpolate(i, size=(args.height, args.width), mode="nearest") for i in inv]
+        vec = model.pose_net(batch["rgb"], batch["rgb_context"])
+        mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(N_CTX)]
+        loss = O.photometric_loss(batch["rgb"], batch["rgb_context"], inv, batch["intrinsics"],
+                                  batch["intrinsics"], mats, None, **kw)[0]
+        loss.sum().backward()
+        opt.step()
+
+    def loss_only():
+        sig = [torch.rand(args.batch, 1, args.height, args.width, generator=torch.Generator().manual_seed(i))
+               .mul(0.19).add(0.01).requires_grad_(True) for i in range(4)]
+        vec = torch.zeros(args.batch, N_CTX, 6)
+        vec[:, :, 2] = torch.tensor([-1.0, 1.0])
+        vec.requires_grad_(True)
+        mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(N_CTX)]
+        O.photometric_loss(batch["rgb"], batch["rgb_context"], sig, batch["intrinsics"], batch["intrinsics"],
+                           mats, None, **kw)[0].sum().backward()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    loss_only()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        loss_only()
+    dl = (time.perf_counter() - t0) / 3
+    return {"value": round(args.batch / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of the full SelfSupModel step "
+                      f"({args.depth_net}+{args.pose_net}, fp32, B={args.batch}, {args.height}x{args.width}, "
+                      f"Adam) with the oracle loss",
+            "s_per_step": round(dt, 3), "loss_only_images_per_s": round(args.batch / dl, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus or (world == 1 and args.gpus == 1), \
+        f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run"
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import __graft_entry__
+    if rank == 0 or world == 1:
+        __graft_entry__.build()
+    if world > 1:
+        dist.barrier()
+        __graft_entry__.build()
+    from packnet_sfm_amd.losses import _hip_photometric as HP
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+
+    torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
+    torch.backends.cudnn.benchmark = True
+    model = build_model(args, device)
+    opt = make_optimizer(model, 1e-4, 1e-4)
+    trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None)
+    batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank)
+
+    for _ in range(args.warmup):
+        trainer.train_step(batch)
+    trainer.check_finite()
+
+    HP.KERNEL_TIMING["enabled"] = not args.no_kernel_timing
+    HP.KERNEL_TIMING["events"].clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.train_step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    HP.KERNEL_TIMING["enabled"] = False
+    ktimes = HP.kernel_times_ms() if not args.no_kernel_timing else {}
+    trainer.check_finite()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    if rank == 0:
+        images = args.batch * world * args.steps
+        value = images / elapsed
+        per_step_ms = 1000.0 * elapsed / args.steps
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_step_ms, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "bf16" if args.amp == "bf16" else "fp32", "data": "synthetic",
+               "config": {"workload": f"SelfSupModel {args.depth_net}('18A' if ResNetSAN01) + {args.pose_net}, "
+                                      f"KITTI {args.width}x{args.height}, 2 contexts, 4 full-res scales, automask "
+                                      f"min-reprojection, Adam (train_resnet_san_kitti_tiny.yaml shapes)",
+                          "model": f"{args.depth_net}+{args.pose_net}", "global_batch": args.batch * world,
+                          "per_gpu_batch": args.batch, "image_hw": [args.height, args.width],
+                          "parallelism": f"dp{world}", "net_dtype": args.amp, "loss_dtype": "fp32",
+                          "weights": "random init (no network / checkpoints)"}}
+        if ktimes:
+            group = ("K1_photometric_fwd", "K2_photometric_bwd", "K3_smoothness_fwd", "K3_smoothness_bwd")
+            per_step_us = {k: round(1000.0 * t / args.steps, 2) for k, (t, n) in ktimes.items()}
+            group_s = sum(ktimes[k][0] for k in group if k in ktimes) / 1000.0 / args.steps
+            bytes_step = algorithmic_bytes_per_image(args.height, args.width) * args.batch
+            achieved = bytes_step / group_s / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    traffic = json.load(f).get("bytes_per_step")
+            out["roofline"] = {"bound": "hbm", "kernel": "photometric K1 fwd + K2 bwd + K3 smoothness fwd/bwd",
+                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                               "algorithmic_bytes_per_step": bytes_step,
+                               "group_us_per_step": round(group_s * 1e6, 2), "kernels_us_per_step": per_step_us}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

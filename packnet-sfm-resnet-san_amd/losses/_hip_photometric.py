@@ -15,6 +15,34 @@ from .. import _hip
 from ..geometry.camera_utils import scale_intrinsics, pinhole_inverse
 
 
+# Optional live kernel timing (bench.py roofline): HIP events recorded on the stream the kernels
+# are launched on (torch's current stream, which is also what we pass to the C-ABI).
+KERNEL_TIMING = {"enabled": False, "events": []}
+
+
+def _run(name, fn, *args):
+    if KERNEL_TIMING["enabled"]:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn(*args)
+        e.record()
+        KERNEL_TIMING["events"].append((name, s, e))
+    else:
+        rc = fn(*args)
+    _hip.check(rc, name)
+
+
+def kernel_times_ms():
+    """Sum of recorded durations per kernel name (synchronises); clears the record."""
+    torch.cuda.synchronize()
+    out = {}
+    for name, s, e in KERNEL_TIMING["events"]:
+        t, n = out.get(name, (0.0, 0))
+        out[name] = (t + s.elapsed_time(e), n + 1)
+    KERNEL_TIMING["events"].clear()
+    return out
+
+
 class _Call:
     """One ABI call: scales that share an image size (one call for the full-res case)."""
 
@@ -107,19 +135,18 @@ class PhotometricLossFn(torch.autograd.Function):
         st = _hip.stream(dev)
         for c in calls:
             if cfg["clip"] > 0.0:
-                _hip.check(L.psfm_photometric_clip_stats(ctypes.byref(c.params), ctypes.byref(c.inputs),
-                                                          ctypes.byref(c.ws), st), "clip_stats")
-            _hip.check(L.psfm_photometric_fwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
-                                              ctypes.byref(c.ws), st), "photometric_fwd")
+                _run("clip_stats", L.psfm_photometric_clip_stats, ctypes.byref(c.params),
+                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st)
+            _run("K1_photometric_fwd", L.psfm_photometric_fwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
+                 ctypes.byref(c.ws), st)
             if cfg["smooth_w"] > 0.0:
-                _hip.check(L.psfm_smoothness_fwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
-                                                 ctypes.byref(c.ws), st), "smoothness_fwd")
+                _run("K3_smoothness_fwd", L.psfm_smoothness_fwd, ctypes.byref(c.params),
+                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st)
         smooth_stats = torch.empty(cfg["n"] * B * 4, device=dev, dtype=torch.float32)
         out = torch.empty(3, device=dev, dtype=torch.float32)
         pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
         wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
-        _hip.check(L.psfm_finalize(len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st),
-                   "finalize")
+        _run("finalize", L.psfm_finalize, len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st)
         ctx.calls, ctx.smooth_stats, ctx.cfg, ctx.n_ctx, ctx.T_shape = calls, smooth_stats, cfg, N, T.shape
         ctx.sig_shapes = [s.shape for s in sigs]
         loss, photo, smooth = out[0:1], out[1].clone(), out[2].clone()
@@ -139,18 +166,17 @@ class PhotometricLossFn(torch.autograd.Function):
                     ctx.sig_shapes[c.params.scale0:c.params.scale0 + c.params.S]]
             arr = (ctypes.c_void_p * _hip.MAX_SCALES)(*([g.data_ptr() for g in gsig] +
                                                          [None] * (_hip.MAX_SCALES - len(gsig))))
-            _hip.check(L.psfm_photometric_bwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
-                                              ctypes.byref(c.ws), _hip.ptr(gout), arr, st), "photometric_bwd")
+            _run("K2_photometric_bwd", L.psfm_photometric_bwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
+                 ctypes.byref(c.ws), _hip.ptr(gout), arr, st)
             if cfg["smooth_w"] > 0.0:
-                _hip.check(L.psfm_smoothness_bwd(ctypes.byref(c.params), ctypes.byref(c.inputs),
-                                                 _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st),
-                           "smoothness_bwd")
+                _run("K3_smoothness_bwd", L.psfm_smoothness_bwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
+                     _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st)
             grads.extend(gsig)
         N, B = ctx.n_ctx, calls[0].params.B
         gT = torch.empty(N, B, 12, device=dev, dtype=torch.float32)
         pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
         wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
-        _hip.check(L.psfm_pose_grad_reduce(len(calls), pp, wp, _hip.ptr(gT), st), "pose_grad_reduce")
+        _run("pose_grad_reduce", L.psfm_pose_grad_reduce, len(calls), pp, wp, _hip.ptr(gT), st)
         return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
 
 

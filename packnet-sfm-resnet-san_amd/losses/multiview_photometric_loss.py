@@ -64,7 +64,7 @@ class MultiViewPhotometricLoss(LossBase):
             raise NotImplementedError("FisheyeCamera (VADAS dict intrinsics) is a SURVEY §8f 'next' row; "
                                       "pass pinhole K [B,3,3]")
         self.n = self.progressive_scaling(progress)
-        sigs = list(inv_depths[:self.n])
+        sigs = [s.float() for s in inv_depths[:self.n]]  # nets may run under bf16 autocast
         T = torch.stack([p.mat[:, :3, :] for p in poses], 0)  # [N,B,3,4], differentiable
         cfg = dict(n=self.n, automask=bool(self.automask_loss),
                    reduce_op=_hip.REDUCE_MIN if self.photometric_reduce_op == "min" else _hip.REDUCE_MEAN,
@@ -73,8 +73,10 @@ class MultiViewPhotometricLoss(LossBase):
                    clip=float(self.clip_loss), smooth_w=float(self.smooth_loss_weight))
         if mask is not None:
             mask = mask.float()
-        loss, photo, smooth = photometric_loss_hip(image.float(), [c.float() for c in context], sigs,
-                                                   intrinsics.float(), ref_intrinsics.float(), T, mask, cfg)
+        with torch.autocast("cuda", enabled=False):   # the photometric path is fp32 end to end
+            loss, photo, smooth = photometric_loss_hip(image.float(), [c.float() for c in context], sigs,
+                                                       intrinsics.float(), ref_intrinsics.float(), T.float(),
+                                                       mask, cfg)
         self.add_metric("photometric_loss", photo)
         if self.smooth_loss_weight > 0.0:
             self.add_metric("smoothness_loss", smooth)

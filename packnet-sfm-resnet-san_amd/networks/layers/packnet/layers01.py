@@ -1,0 +1,122 @@
+"""PackNet building blocks (packnet_sfm/networks/layers/packnet/layers01.py:10-286), PyTorch-ROCm
+(MIOpen convolutions).  Parameter names match the reference so its checkpoints load as-is.
+
+`packing` (space-to-depth) is a pure index permutation; the fused pack+Conv3d HIP op is the
+SURVEY §8f "next" row 1.
+"""
+from functools import partial
+
+import torch
+import torch.nn as nn
+
+
+class Conv2D(nn.Module):
+    """zero-pad(k//2) -> Conv2d -> GroupNorm(16) -> ELU."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.conv_base = nn.Conv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride)
+        self.pad = nn.ConstantPad2d([kernel_size // 2] * 4, value=0)
+        self.normalize = nn.GroupNorm(16, out_channels)
+        self.activ = nn.ELU(inplace=True)
+
+    def forward(self, x):
+        return self.activ(self.normalize(self.conv_base(self.pad(x))))
+
+
+class ResidualConv(nn.Module):
+    """Two Conv2D + 1x1 shortcut, GroupNorm + ELU after the sum."""
+
+    def __init__(self, in_channels, out_channels, stride, dropout=None):
+        super().__init__()
+        self.conv1 = Conv2D(in_channels, out_channels, 3, stride)
+        self.conv2 = Conv2D(out_channels, out_channels, 3, 1)
+        shortcut = nn.Conv2d(in_channels, out_channels, kernel_size=1, stride=stride)
+        self.conv3 = nn.Sequential(shortcut, nn.Dropout2d(dropout)) if dropout else shortcut
+        self.normalize = nn.GroupNorm(16, out_channels)
+        self.activ = nn.ELU(inplace=True)
+
+    def forward(self, x):
+        return self.activ(self.normalize(self.conv2(self.conv1(x)) + self.conv3(x)))
+
+
+def ResidualBlock(in_channels, out_channels, num_blocks, stride, dropout=None):
+    blocks = [ResidualConv(in_channels, out_channels, stride, dropout=dropout)]
+    blocks += [ResidualConv(out_channels, out_channels, 1, dropout=dropout) for _ in range(1, num_blocks)]
+    return nn.Sequential(*blocks)
+
+
+class InvDepth(nn.Module):
+    """3x3 conv -> sigmoid / min_depth."""
+
+    def __init__(self, in_channels, out_channels=1, min_depth=0.5):
+        super().__init__()
+        self.min_depth = min_depth
+        self.conv1 = nn.Conv2d(in_channels, out_channels, kernel_size=3, stride=1)
+        self.pad = nn.ConstantPad2d([1] * 4, value=0)
+        self.activ = nn.Sigmoid()
+
+    def forward(self, x):
+        return self.activ(self.conv1(self.pad(x))) / self.min_depth
+
+
+def packing(x, r=2):
+    """[B,C,H,W] -> [B,C*r*r,H/r,W/r]; channel index = c*r*r + dy*r + dx (inverse of PixelShuffle)."""
+    b, c, h, w = x.shape
+    x = x.contiguous().view(b, c, h // r, r, w // r, r)
+    return x.permute(0, 1, 3, 5, 2, 4).reshape(b, c * r * r, h // r, w // r)
+
+
+class PackLayerConv2d(nn.Module):
+    def __init__(self, in_channels, kernel_size, r=2):
+        super().__init__()
+        self.conv = Conv2D(in_channels * (r ** 2), in_channels, kernel_size, 1)
+        self.pack = partial(packing, r=r)
+
+    def forward(self, x):
+        return self.conv(self.pack(x))
+
+
+class UnpackLayerConv2d(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size, r=2):
+        super().__init__()
+        self.conv = Conv2D(in_channels, out_channels * (r ** 2), kernel_size, 1)
+        self.unpack = nn.PixelShuffle(r)
+
+    def forward(self, x):
+        return self.unpack(self.conv(x))
+
+
+def _conv3d_d(d):
+    return nn.Conv3d(1, d, kernel_size=(3, 3, 3), stride=(1, 1, 1), padding=(1, 1, 1))
+
+
+class PackLayerConv3d(nn.Module):
+    """pack -> Conv3d(1->d) over (channel, y, x) -> fold d into channels -> Conv2D."""
+
+    def __init__(self, in_channels, kernel_size, r=2, d=8):
+        super().__init__()
+        self.conv = Conv2D(in_channels * (r ** 2) * d, in_channels, kernel_size, 1)
+        self.pack = partial(packing, r=r)
+        self.conv3d = _conv3d_d(d)
+
+    def forward(self, x):
+        x = self.conv3d(self.pack(x).unsqueeze(1))
+        b, c, d, h, w = x.shape
+        return self.conv(x.reshape(b, c * d, h, w))
+
+
+class UnpackLayerConv3d(nn.Module):
+    """Conv2D -> Conv3d(1->d) -> fold -> PixelShuffle."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, r=2, d=8):
+        super().__init__()
+        self.conv = Conv2D(in_channels, out_channels * (r ** 2) // d, kernel_size, 1)
+        self.unpack = nn.PixelShuffle(r)
+        self.conv3d = _conv3d_d(d)
+
+    def forward(self, x):
+        x = self.conv3d(self.conv(x).unsqueeze(1))
+        b, c, d, h, w = x.shape
+        return self.unpack(x.reshape(b, c * d, h, w))

@@ -1,0 +1,101 @@
+"""Networks (PyTorch-ROCm side of the step): parameter layout and numerics vs the reference.
+
+PackNet01/PoseNet have the reference's parameter names; loading the golden's deterministic
+weights (golden_util.det_init_) must reproduce the reference's inverse-depth outputs and, with
+the oracle loss, the reference's SelfSupModel loss (tests/golden/step_packnet_tiny.npz).
+ResNet encoders follow torchvision's layout (torchvision is absent here: parity unpinned for
+the trunk, which is the standard architecture)."""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+
+
+def _batch(B=1, H=64, W=192):
+    g = torch.Generator().manual_seed(77)
+    rgb = gu.smooth_texture(g, B, 3, H, W)
+    ctx = [gu.smooth_texture(g, B, 3, H, W) for _ in range(2)]
+    return rgb, ctx, gu.kitti_K(B, H, W)
+
+
+def _packnet_model():
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.networks.depth.PackNet01 import PackNet01
+    from packnet_sfm_amd.networks.pose.PoseNet import PoseNet
+    depth, pose = PackNet01(version="1A"), PoseNet(nb_ref_imgs=2)
+    gu.det_init_(depth)
+    gu.det_init_(pose)
+    return depth, pose
+
+
+def test_packnet_parameter_count_matches_survey():
+    depth, pose = _packnet_model()
+    n_depth = sum(p.numel() for p in depth.parameters())
+    n_pose = sum(p.numel() for p in pose.parameters())
+    assert abs(n_depth / 1e6 - 128.29) < 0.01
+    assert abs(n_pose / 1e6 - 1.59) < 0.01
+
+
+def test_resnet_san_parameter_layout():
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.networks.depth.ResNetSAN01 import ResNetSAN01
+    net = ResNetSAN01(version="18A")
+    names = dict(net.named_parameters())
+    assert "encoder.encoder.layer4.1.bn2.weight" in names
+    assert "decoder.decoder.0.conv.conv.weight" in names
+    n = sum(p.numel() for p in net.parameters())
+    assert abs(n / 1e6 - 14.33) < 0.02            # SURVEY.md §2.4 (ResNet18 depth)
+
+
+def test_packnet_step_matches_reference_cpu():
+    """PackNet01 + PoseNet forward (ours, CPU) + oracle loss == the reference SelfSupModel step."""
+    from oracle import photometric_oracle as O
+    z = gu.load_golden("step_packnet_tiny")
+    depth, pose = _packnet_model()
+    depth.train()
+    pose.train()
+    rgb, ctx, K = _batch()
+    torch.set_num_threads(8)
+    inv = depth(rgb)["inv_depths"]
+    inv_up = [torch.nn.functional.interpolate(i, size=rgb.shape[-2:], mode="nearest") for i in inv]
+    assert abs(float(inv_up[0].double().sum()) - float(z["inv0_sum"])) / float(z["inv0_sum"]) < 1e-4
+    np.testing.assert_allclose(inv_up[0].reshape(-1)[::997].detach().numpy(), z["inv0_samples"], rtol=1e-4)
+    vec = pose(rgb, ctx)
+    mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+    np.testing.assert_allclose(torch.stack(mats, 1).detach().numpy(), z["pose_mats"], rtol=1e-4, atol=1e-6)
+    loss, photo, smooth, _ = O.photometric_loss(rgb, ctx, inv_up, K, K, mats, torch.ones(1, 1, 64, 192))
+    assert gu.rel_err(loss.detach(), z["loss"]) < 1e-4
+    assert gu.rel_err(smooth.detach(), z["smoothness_loss"]) < 1e-4
+
+
+@pytest.mark.gpu
+def test_selfsup_step_on_gpu_matches_reference():
+    """Full SelfSupModel step on the GPU (MIOpen nets + HIP loss) vs the reference golden."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.models.SelfSupModel import SelfSupModel
+    z = gu.load_golden("step_packnet_tiny")
+    dev = torch.device("cuda:0")
+    depth, pose = _packnet_model()
+    model = SelfSupModel(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
+                         automask_loss=True, clip_loss=0.0, min_depth=0.5, max_depth=80.0,
+                         upsample_depth_maps=True, rotation_mode="euler")
+    model.add_depth_net(depth)
+    model.add_pose_net(pose)
+    model = model.to(dev).train()
+    rgb, ctx, K = _batch()
+    rgb, ctx, K = rgb.to(dev), [c.to(dev) for c in ctx], K.to(dev)
+    batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K,
+                 mask=torch.ones(1, 1, 64, 192, device=dev))
+    out = model(batch, progress=0.0)
+    out["loss"].sum().backward()
+    assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < 1e-4
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < 1e-4
+    params = {f"depth_net.{n}": p for n, p in model.depth_net.named_parameters()}
+    params.update({f"pose_net.{n}": p for n, p in model.pose_net.named_parameters()})
+    for name, ref in zip(z["grad_names"], z["grad_norms"]):
+        got = float(params[str(name)].grad.double().norm())
+        assert abs(got - ref) / ref < 2e-2, (name, got, ref)

@@ -1,0 +1,36 @@
+#!/bin/bash
+# GPU-box driver: tests, bench, rocprof kernel trace.  Stops at the first crash-like exit
+# (abort/segfault/timeout: 124, 134, 137, 139) so nothing else runs on a faulted GPU.
+# usage: tools/gpu_run.sh [tests] [bench] [prof] [pmc]
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+crash() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 500 python -m pytest "$ROOT/tests" -m gpu -q -rs > "$OUT/gpu_tests.log" 2>&1; rc=$?
+      echo "[tests] rc=$rc"; tail -3 "$OUT/gpu_tests.log"; crash $rc && exit $rc ;;
+    smoke)
+      (cd "$ROOT" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") > "$OUT/smoke.log" 2>&1; rc=$?
+      echo "[smoke] rc=$rc"; tail -2 "$OUT/smoke.log"; crash $rc && exit $rc ;;
+    bench)
+      (cd "$ROOT" && timeout -k 10 600 python bench.py) > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+      echo "[bench] rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; crash $rc && exit $rc ;;
+    prof)
+      rm -rf "$OUT/prof"
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+         -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing) > "$OUT/prof.log" 2>&1; rc=$?
+      echo "[prof] rc=$rc"; tail -3 "$OUT/prof.log"; crash $rc && exit $rc ;;
+    pmc)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        rm -rf "$OUT/pmc_$ctr"
+        (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run \
+           -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --no-kernel-timing) > "$OUT/pmc_$ctr.log" 2>&1; rc=$?
+        echo "[pmc $ctr] rc=$rc"; tail -2 "$OUT/pmc_$ctr.log"; crash $rc && exit $rc
+      done ;;
+  esac
+done
+exit 0
