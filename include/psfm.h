@@ -76,11 +76,13 @@ typedef struct psfm_workspace {
     float* clip_thr;     /* [S][2N]                 clip thresholds (written by finalize)  */
     float* pose_part;    /* [S][N][B][tiles][12]    per-tile dL/dT partials                */
     uint8_t* argmin;     /* [S][B][H][W]            selected candidate per pixel ('min')   */
+    float* unwarp;       /* [N][B][H][W]            automask: photometric loss of each
+                                                    UN-warped context (scale independent)  */
 } psfm_workspace;
 
 /* number of floats (and argmin bytes) the workspace of this call needs */
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
-                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes);
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp);
 
 /* Clip statistics pass (only when clip_loss > 0): per-candidate-map sum / sum of squares
  * (calc_photometric_loss :249-253), then thresholds mean + clip*std (unbiased). */
@@ -89,7 +91,10 @@ int psfm_photometric_clip_stats(const psfm_params* p, const psfm_inputs* in,
 
 /* K1 forward: lift -> transform -> project -> bilinear gather (view_synthesis), SSIM+L1
  * (calc_photometric_loss), automask candidates, min/mean reduction (reduce_photometric_loss).
- * Writes ws->photo_part and (op 'min') ws->argmin. */
+ * Writes ws->photo_part, (op 'min') ws->argmin and — fused K3 forward — ws->smooth_part when
+ * smooth_w > 0 (psfm_smoothness_fwd is then a no-op; it launches only for l1_only calls).
+ * With automask it first runs K0, the un-warped candidates into ws->unwarp (skipped when
+ * clip_loss > 0: psfm_photometric_clip_stats, which must precede, already produced them). */
 int psfm_photometric_fwd(const psfm_params* p, const psfm_inputs* in,
                          const psfm_workspace* ws, void* stream);
 

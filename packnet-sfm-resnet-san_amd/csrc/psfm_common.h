@@ -47,6 +47,20 @@ __device__ __forceinline__ void load_cam(const float* __restrict__ p, CamRec& c)
     for (int i = 0; i < 12; ++i) c.T[i] = p[18 + i];
 }
 
+// Wave-uniform camera record kept in SGPRs (the record address is uniform; readfirstlane
+// tells the compiler the values are too, so they leave the VGPR budget).
+__device__ __forceinline__ float sgpr(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ void load_cam_uniform(const float* __restrict__ p, CamRec& c) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) c.Ki[i] = sgpr(p[i]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) c.Kr[i] = sgpr(p[9 + i]);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) c.T[i] = sgpr(p[18 + i]);
+}
+
 // sigmoid -> depth (post_process_depth.py:101-106) -> inv (:369) -> warp depth (depth.py:120)
 struct DepthChain {
     float lo, rng;
@@ -114,29 +128,60 @@ __device__ __forceinline__ Taps make_taps(float ix, float iy, int H, int W) {
     return t;
 }
 
+// Branch-free tap setup: out-of-bounds taps read a clamped (valid) address and are zeroed by a
+// select, so all 12 loads of a bilinear sample issue back to back (no exec-masked branches,
+// one wait) — the per-tap zero padding of grid_sample(padding_mode='zeros') is unchanged.
+struct TapAddr {
+    size_t nw, ne, sw, se;
+    bool vnw, vne, vsw, vse;
+    float ax, bx, ay, by;  // (x0+1-ix), (ix-x0), (y0+1-iy), (iy-y0)
+};
+
+__device__ __forceinline__ TapAddr tap_addr(float ix, float iy, int H, int W) {
+    const Taps t = make_taps(ix, iy, H, W);
+    TapAddr a;
+    const int x0 = t.x0, y0 = t.y0;
+    const bool xw = t.ok && x0 >= 0 && x0 < W, xe = t.ok && x0 + 1 >= 0 && x0 + 1 < W;
+    const bool yn = t.ok && y0 >= 0 && y0 < H, ys = t.ok && y0 + 1 >= 0 && y0 + 1 < H;
+    const int cx0 = min(max(x0, 0), W - 1), cx1 = min(max(x0 + 1, 0), W - 1);
+    const int cy0 = min(max(y0, 0), H - 1), cy1 = min(max(y0 + 1, 0), H - 1);
+    a.nw = (size_t)cy0 * W + cx0;
+    a.ne = (size_t)cy0 * W + cx1;
+    a.sw = (size_t)cy1 * W + cx0;
+    a.se = (size_t)cy1 * W + cx1;
+    a.vnw = yn && xw;
+    a.vne = yn && xe;
+    a.vsw = ys && xw;
+    a.vse = ys && xe;
+    a.ax = (t.fx0 + 1.0f) - ix;
+    a.bx = ix - t.fx0;
+    a.ay = (t.fy0 + 1.0f) - iy;
+    a.by = iy - t.fy0;
+    return a;
+}
+
 // warped[c] = sum_tap w_tap * img[c](tap)  (ATen grid_sampler_2d bilinear, nw,ne,sw,se order)
 __device__ __forceinline__ void bilinear3(const float* __restrict__ img, int H, int W, float ix,
                                           float iy, float out[3]) {
-    out[0] = out[1] = out[2] = 0.0f;
-    const Taps t = make_taps(ix, iy, H, W);
-    if (!t.ok) return;
-    const float ixe = t.fx0 + 1.0f, iys = t.fy0 + 1.0f;
-    const float nw = (ixe - ix) * (iys - iy);
-    const float ne = (ix - t.fx0) * (iys - iy);
-    const float sw = (ixe - ix) * (iy - t.fy0);
-    const float se = (ix - t.fx0) * (iy - t.fy0);
-    const bool xw = t.x0 >= 0 && t.x0 < W, xe = t.x0 + 1 >= 0 && t.x0 + 1 < W;
-    const bool yn = t.y0 >= 0 && t.y0 < H, ys = t.y0 + 1 >= 0 && t.y0 + 1 < H;
+    const TapAddr t = tap_addr(ix, iy, H, W);
     const size_t plane = (size_t)H * W;
-    const size_t base = (size_t)t.y0 * W + t.x0;
+    float v[3][4];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const float* p = img + c * plane;
+        v[c][0] = p[t.nw];
+        v[c][1] = p[t.ne];
+        v[c][2] = p[t.sw];
+        v[c][3] = p[t.se];
+    }
+    const float wnw = t.ax * t.ay, wne = t.bx * t.ay, wsw = t.ax * t.by, wse = t.bx * t.by;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
         float acc = 0.0f;
-        if (yn && xw) acc += p[base] * nw;
-        if (yn && xe) acc += p[base + 1] * ne;
-        if (ys && xw) acc += p[base + W] * sw;
-        if (ys && xe) acc += p[base + W + 1] * se;
+        acc += (t.vnw ? v[c][0] : 0.0f) * wnw;
+        acc += (t.vne ? v[c][1] : 0.0f) * wne;
+        acc += (t.vsw ? v[c][2] : 0.0f) * wsw;
+        acc += (t.vse ? v[c][3] : 0.0f) * wse;
         out[c] = acc;
     }
 }

@@ -16,10 +16,12 @@
 // 2-pixel halo, forms the SSIM adjoint coefficients on a 1-pixel halo in LDS and gathers
 // them (reflect-aware weights) per pixel, then back-propagates through bilinear sampling and
 // the projection; dL/d[R|t] is reduced per tile (wave butterfly + fixed-order wave sum).
+#include <algorithm>
 #include <cstdio>
 #include <string>
 
 #include "psfm_common.h"
+#include "psfm_sweep.h"
 
 using namespace psfm;
 
@@ -837,6 +839,41 @@ int validate(const psfm_params* p, const psfm_inputs* in) {
 
 dim3 tile_grid(const psfm_params* p) { return dim3(tiles_img(p->H, p->W), p->B); }
 
+// partial-sum units per image: the v2 sweep kernels handle every config except the 3-channel
+// L1-only candidates (ssim_loss_weight == 0), which keep the v1 tile kernels.
+bool use_sweep(const psfm_params* p) { return !p->l1_only; }
+int fwd_units(const psfm_params* p) { return use_sweep(p) ? sweep::k1_units(p->H, p->W) : tiles_img(p->H, p->W); }
+int bwd_units(const psfm_params* p) { return use_sweep(p) ? sweep::k2_units(p->H, p->W) : tiles_img(p->H, p->W); }
+
+sweep::SweepArgs sweep_args(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws) {
+    sweep::SweepArgs a{};
+    a.p = *p;
+    a.in = *in;
+    if (ws) a.ws = *ws;
+    return a;
+}
+
+void launch_k0(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
+    const dim3 grid(sweep::k1_units(p->H, p->W), p->B);
+    switch (p->N) {
+        case 1: hipLaunchKernelGGL((sweep::k0_unwarped<1>), grid, dim3(64), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((sweep::k0_unwarped<2>), grid, dim3(64), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((sweep::k0_unwarped<3>), grid, dim3(64), 0, st, a); break;
+        default: hipLaunchKernelGGL((sweep::k0_unwarped<4>), grid, dim3(64), 0, st, a); break;
+    }
+}
+
+template <bool STATS>
+void launch_k1(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
+    const dim3 grid(sweep::k1_units(p->H, p->W), p->B, p->S);
+    switch (p->N) {
+        case 1: hipLaunchKernelGGL((sweep::k1_forward<1, STATS>), grid, dim3(64), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((sweep::k1_forward<2, STATS>), grid, dim3(64), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((sweep::k1_forward<3, STATS>), grid, dim3(64), 0, st, a); break;
+        default: hipLaunchKernelGGL((sweep::k1_forward<4, STATS>), grid, dim3(64), 0, st, a); break;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -844,9 +881,10 @@ extern "C" {
 int psfm_tiles_per_image(int H, int W) { return tiles_img(H, W); }
 
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
-                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes) {
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp) {
     if (!p) return fail(-1, "null params");
-    const size_t t = (size_t)tiles_img(p->H, p->W) * p->B;
+    const size_t t = (size_t)std::max(tiles_img(p->H, p->W), std::max(sweep::k1_units(p->H, p->W),
+                                                                         sweep::k2_units(p->H, p->W))) * p->B;
     const size_t ns = (size_t)n_src(*p);
     if (photo) *photo = (size_t)p->S * t;
     if (smooth) *smooth = (size_t)p->S * t * 4;
@@ -854,6 +892,7 @@ int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, s
     if (clip_thr) *clip_thr = (size_t)p->S * ns;
     if (pose) *pose = (size_t)p->S * p->N * t * 12;
     if (argmin_bytes) *argmin_bytes = (size_t)p->S * p->B * p->H * p->W;
+    if (unwarp) *unwarp = (p->automask && !p->l1_only) ? (size_t)p->N * p->B * p->H * p->W : 0;
     return 0;
 }
 
@@ -866,12 +905,16 @@ int psfm_photometric_clip_stats(const psfm_params* p, const psfm_inputs* in,
     a.in = *in;
     a.ws = *ws;
     hipStream_t st = (hipStream_t)stream;
-    if (p->l1_only)
+    if (p->l1_only) {
         hipLaunchKernelGGL((k_photo_fwd<true, true>), tile_grid(p), dim3(NT), 0, st, a);
-    else
-        hipLaunchKernelGGL((k_photo_fwd<false, true>), tile_grid(p), dim3(NT), 0, st, a);
+    } else {
+        if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
+        const sweep::SweepArgs sa = sweep_args(p, in, ws);
+        if (p->automask) launch_k0(p, sa, st);
+        launch_k1<true>(p, sa, st);
+    }
     PSFM_LAUNCH_CHECK();
-    ThrArgs t{ws->clip_part, ws->clip_thr, p->S, n_src(*p), p->B * tiles_img(p->H, p->W),
+    ThrArgs t{ws->clip_part, ws->clip_thr, p->S, n_src(*p), p->B * fwd_units(p),
               (double)p->B * p->H * p->W * (p->l1_only ? 3.0 : 1.0), p->clip_loss};
     hipLaunchKernelGGL(k_clip_thr, dim3(1), dim3(1024), 0, st, t);
     PSFM_LAUNCH_CHECK();
@@ -889,10 +932,15 @@ int psfm_photometric_fwd(const psfm_params* p, const psfm_inputs* in, const psfm
     a.in = *in;
     a.ws = *ws;
     hipStream_t st = (hipStream_t)stream;
-    if (p->l1_only)
+    if (p->l1_only) {
         hipLaunchKernelGGL((k_photo_fwd<true, false>), tile_grid(p), dim3(NT), 0, st, a);
-    else
-        hipLaunchKernelGGL((k_photo_fwd<false, false>), tile_grid(p), dim3(NT), 0, st, a);
+    } else {
+        if (p->smooth_w > 0.0f && !ws->smooth_part) return fail(-12, "null smoothness workspace");
+        if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
+        const sweep::SweepArgs sa = sweep_args(p, in, ws);
+        if (p->automask && !(p->clip_loss > 0.0f)) launch_k0(p, sa, st);  // clip: done by clip_stats
+        launch_k1<false>(p, sa, st);  // also writes the smoothness partials
+    }
     PSFM_LAUNCH_CHECK();
     return 0;
 }
@@ -901,6 +949,7 @@ int psfm_smoothness_fwd(const psfm_params* p, const psfm_inputs* in, const psfm_
                         void* stream) {
     if (int e = validate(p, in)) return e;
     if (!ws || !ws->smooth_part) return fail(-12, "null smoothness workspace");
+    if (use_sweep(p)) return 0;  // fused into psfm_photometric_fwd (K1 sweep)
     KArgs a{};
     a.p = *p;
     a.in = *in;
@@ -931,7 +980,7 @@ int psfm_finalize(int ncalls, const psfm_params* const* calls, const psfm_worksp
         c.B = p.B;
         c.H = p.H;
         c.W = p.W;
-        c.tiles = tiles_img(p.H, p.W);
+        c.tiles = fwd_units(&p);
         const double cnt = (double)p.B * p.H * p.W;
         c.photo_scale = (p.reduce_op == PSFM_REDUCE_MIN)
                             ? 1.0 / ((double)p.n_scales * cnt)
@@ -961,10 +1010,15 @@ int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm
         a.grad_sig[s] = grad_sig[s];
     }
     hipStream_t st = (hipStream_t)stream;
-    if (p->l1_only)
+    if (p->l1_only) {
         hipLaunchKernelGGL((k_photo_bwd<true>), tile_grid(p), dim3(NT), 0, st, a);
-    else
-        hipLaunchKernelGGL((k_photo_bwd<false>), tile_grid(p), dim3(NT), 0, st, a);
+    } else {
+        sweep::SweepArgs sa = sweep_args(p, in, ws);
+        sa.grad_out = grad_out;
+        for (int s = 0; s < p->S; ++s) sa.grad_sig[s] = grad_sig[s];
+        hipLaunchKernelGGL(sweep::k2_backward, dim3(sweep::k2_units(p->H, p->W), p->B, p->S), dim3(64 * p->N),
+                           0, st, sa);
+    }
     PSFM_LAUNCH_CHECK();
     return 0;
 }
@@ -997,8 +1051,7 @@ int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
     r.grad_T = grad_T;
     for (int i = 0; i < ncalls; ++i) {
         if (calls[i]->N != r.N || calls[i]->B != r.B) return fail(-1, "calls disagree on N/B");
-        r.c[i] = PoseRedCall{ws[i]->pose_part, calls[i]->S, calls[i]->N, calls[i]->B,
-                             tiles_img(calls[i]->H, calls[i]->W)};
+        r.c[i] = PoseRedCall{ws[i]->pose_part, calls[i]->S, calls[i]->N, calls[i]->B, bwd_units(calls[i])};
     }
     const int items = r.N * r.B * 12;
     hipLaunchKernelGGL(k_pose_reduce, dim3((items + 3) / 4), dim3(256), 0, (hipStream_t)stream, r);

@@ -1,11 +1,19 @@
-"""Data-parallel trainer: one process per GPU, DDP with RCCL bucketed all-reduce over xGMI
-(replaces packnet_sfm/trainers/horovod_trainer.py, whose Horovod is a mock — SURVEY.md §0.2).
+"""Data-parallel trainer: one process per GPU, RCCL all-reduce of gradients over xGMI (replaces
+packnet_sfm/trainers/horovod_trainer.py, whose Horovod is a mock — SURVEY.md §0.2).
 
 Per step (horovod_trainer.py:222-284): zero_grad -> forward (depth/pose nets under bf16
-autocast, photometric loss in fp32 on the HIP kernels) -> loss.backward() (DDP overlaps the
-gradient all-reduce with backward) -> optimizer.step().  The reference's per-step
-`torch.autograd.set_detect_anomaly(True)` and per-step `.item()` host syncs are not on the hot
-path: the non-finite check accumulates on the device and is checked every `check_every` steps.
+autocast, photometric loss in fp32 on the HIP kernels) -> backward -> gradient average across
+ranks -> optimizer.step().
+
+Two execution modes:
+  * graph (default on a ROCm device): the step is captured into HIP graphs once and replayed —
+    the eager step is host-bound (~1.5k launches, MIOpen host overhead).
+    Gradients live in ONE flat fp32 buffer (every `p.grad` is a view of it), so the cross-rank
+    average is a single RCCL all-reduce of that buffer between two graph replays
+    (fwd+bwd graph | all_reduce | scale+Adam graph); at world size 1 the whole step is one graph.
+  * eager: torch DDP (bucketed all-reduce overlapped with backward) — CPU/gloo and debugging.
+The reference's per-step anomaly detection and `.item()` syncs are not on the hot path: the
+non-finite check accumulates on the device and is tested every `check_every` steps.
 """
 import contextlib
 
@@ -29,7 +37,7 @@ def make_optimizer(model, depth_lr=1e-4, pose_lr=1e-4, name="Adam", **kw):
 
 class DDPTrainer:
     def __init__(self, model, optimizer, device, amp_dtype=torch.bfloat16, bucket_cap_mb=64,
-                 check_every=0):
+                 check_every=0, graph=None, flat=None):
         self.device = device
         self.model = model
         self.optimizer = optimizer
@@ -38,27 +46,115 @@ class DDPTrainer:
         self.step_idx = 0
         self.nonfinite = torch.zeros((), device=device)
         self.world = hvd.world_size()
-        if self.world > 1:
-            # static_graph: unused parameters (e.g. ResNetSAN01's LiDAR fusion weights) are
-            # detected once; gradient buckets then reduce in a fixed order, overlapped with backward
+        self.use_graph = (device.type == "cuda") if graph is None else graph
+        # flat: one flat gradient buffer + one all-reduce per step (the graph mode's algebra;
+        # also runnable eagerly, e.g. on CPU/gloo for tests)
+        self.flat = self.use_graph if flat is None else (flat or self.use_graph)
+        self.graphs = None
+        if self.flat:
+            self._flatten_grads()
+            self.ddp = model
+        elif self.world > 1:
+            # static_graph: unused parameters (ResNetSAN01's LiDAR fusion weights) are detected once
             self.ddp = DDP(model, device_ids=[device.index] if device.type == "cuda" else None,
                            bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
         else:
             self.ddp = model
 
+    # ------------------------------------------------------------------------------------------
+    def _flatten_grads(self):
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        n = sum(p.numel() for p in params)
+        self.flat_grad = torch.zeros(n, device=self.device, dtype=torch.float32)
+        off = 0
+        for p in params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.params = params
+        if self.world > 1:  # identical initial weights on every rank
+            for p in params:
+                dist.broadcast(p.data, src=0)
+            for b in self.model.buffers():
+                dist.broadcast(b, src=0)
+
     def autocast(self):
         if self.amp_dtype is None or self.device.type != "cuda":
             return contextlib.nullcontext()
-        return torch.autocast(device_type="cuda", dtype=self.amp_dtype)
+        # no weight-cast cache: casts must be re-done inside every graph replay
+        return torch.autocast(device_type="cuda", dtype=self.amp_dtype, cache_enabled=False)
 
-    def train_step(self, batch, progress=0.0):
-        self.optimizer.zero_grad(set_to_none=True)
+    def _forward_backward(self, batch, progress):
         with self.autocast():
             output = self.ddp(batch, progress=progress)
         loss = output["loss"]
         loss.sum().backward()
-        self.optimizer.step()
         self.nonfinite += (~torch.isfinite(loss.detach())).any().float()
+        return output
+
+    # ------------------------------------------------------------------------------------------
+    def capture(self, static_batch, warmup=3, progress=0.0):
+        """Warm up on a side stream (MIOpen algorithm selection, allocator), then capture."""
+        assert self.use_graph
+        self.static_batch = static_batch
+        inv_world = 1.0 / self.world
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.flat_grad.zero_()
+                self._forward_backward(static_batch, progress)
+                self._allreduce()
+                self.optimizer.step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.nonfinite.zero_()
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.flat_grad.zero_()
+                self.static_output = self._forward_backward(static_batch, progress)
+                self.optimizer.step()
+            self.graphs = (g,)
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self.flat_grad.zero_()
+                self.static_output = self._forward_backward(static_batch, progress)
+            pool = g1.pool()
+            with torch.cuda.graph(g2, pool=pool):
+                self.flat_grad.mul_(inv_world)
+                self.optimizer.step()
+            self.graphs = (g1, g2)
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+            if self.graphs is None:
+                self.flat_grad.mul_(1.0 / self.world)
+
+    # ------------------------------------------------------------------------------------------
+    def train_step(self, batch, progress=0.0):
+        if self.use_graph:
+            if self.graphs is None:
+                self.capture(batch, progress=progress)
+            elif batch is not self.static_batch:
+                _copy_into(self.static_batch, batch)
+            if self.world == 1:
+                self.graphs[0].replay()
+            else:
+                self.graphs[0].replay()
+                dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+                self.graphs[1].replay()
+            output = self.static_output
+        elif self.flat:
+            self.flat_grad.zero_()
+            output = self._forward_backward(batch, progress)
+            self._allreduce()
+            self.optimizer.step()
+        else:
+            self.optimizer.zero_grad(set_to_none=True)
+            output = self._forward_backward(batch, progress)
+            self.optimizer.step()
         self.step_idx += 1
         if self.check_every and self.step_idx % self.check_every == 0:
             self.check_finite()
@@ -70,3 +166,14 @@ class DDPTrainer:
             dist.all_reduce(flag)
         if float(flag) > 0:
             raise ValueError(f"Non-finite loss within the last steps (step {self.step_idx})")
+
+
+def _copy_into(dst, src):
+    if torch.is_tensor(dst):
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _copy_into(dst[k], src[k])
+    elif isinstance(dst, (list, tuple)):
+        for d, s in zip(dst, src):
+            _copy_into(d, s)

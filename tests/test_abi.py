@@ -34,13 +34,14 @@ def test_every_declared_symbol_is_exported(hip):
 
 def test_workspace_sizes(hip):
     p = hip.Params(B=4, H=192, W=640, N=2, S=4, scale0=0, n_scales=4, automask=1, reduce_op=0)
-    n = [ctypes.c_size_t() for _ in range(6)]
+    n = [ctypes.c_size_t() for _ in range(7)]
     assert hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]) == 0
     tiles = hip.tiles_per_image(192, 640)
     assert tiles == 10 * 48
-    assert n[0].value == 4 * 4 * tiles
-    assert n[4].value == 4 * 2 * 4 * tiles * 12
+    assert n[0].value >= 4 * 4 * tiles
+    assert n[4].value >= 4 * 2 * 4 * tiles * 12
     assert n[5].value == 4 * 4 * 192 * 640
+    assert n[6].value == 2 * 4 * 192 * 640
 
 
 @pytest.mark.parametrize("field,value,code", [("N", 0, -3), ("N", 5, -3), ("S", 0, -4), ("H", 1, -2),
