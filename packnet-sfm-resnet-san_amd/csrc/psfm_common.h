@@ -227,15 +227,17 @@ __device__ __forceinline__ void bilinear3_grad_pos(const float* __restrict__ img
 }
 
 // Adjoint of project() for one pixel: from (gix, giy) to dL/dd and dL/dT (12, accumulated).
+// Gradient-only arithmetic: 1/z via v_rcp_f32 (the forward values keep IEEE division).
 __device__ __forceinline__ float project_grad(const CamRec& c, const Proj& r, float d, float gix,
                                               float giy, int H, int W, float gT[12]) {
-    // ix = ((2u/(W-1) - 1 + 1)/2)(W-1) with u = p0/z  ->  d ix/du = (W-1)/2 * 2/(W-1)
-    const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
-    const float gu = gix * (wm1 / 2.0f) * (2.0f / wm1);
-    const float gv = giy * (hm1 / 2.0f) * (2.0f / hm1);
-    const float gp0 = gu / r.z;
-    const float gp1 = gv / r.z;
-    const float gp2 = (r.p2 >= 1e-5f) ? -(gu * (r.p0 / r.z) + gv * (r.p1 / r.z)) / r.z : 0.0f;
+    // ix = ((2u/(W-1) - 1 + 1)/2)(W-1) with u = p0/z  ->  d ix/du = 1 (and likewise for v)
+    (void)H;
+    (void)W;
+    const float iz = __builtin_amdgcn_rcpf(r.z);
+    const float gu = gix, gv = giy;
+    const float gp0 = gu * iz;
+    const float gp1 = gv * iz;
+    const float gp2 = (r.p2 >= 1e-5f) ? -(gu * r.p0 + gv * r.p1) * (iz * iz) : 0.0f;
     // c = K_ref^-1 p  -> gc = K_ref^T gp
     const float gc0 = c.Kr[0] * gp0 + c.Kr[3] * gp1 + c.Kr[6] * gp2;
     const float gc1 = c.Kr[1] * gp0 + c.Kr[4] * gp1 + c.Kr[7] * gp2;

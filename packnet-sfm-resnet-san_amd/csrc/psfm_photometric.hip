@@ -1017,7 +1017,7 @@ int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm
         sa.grad_out = grad_out;
         for (int s = 0; s < p->S; ++s) sa.grad_sig[s] = grad_sig[s];
         hipLaunchKernelGGL(sweep::k2_backward, dim3(sweep::k2_units(p->H, p->W), p->B, p->S), dim3(64 * p->N),
-                           0, st, sa);
+                           sweep::k2_lds_bytes(p->N), st, sa);
     }
     PSFM_LAUNCH_CHECK();
     return 0;

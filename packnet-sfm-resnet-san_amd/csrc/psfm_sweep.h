@@ -417,9 +417,16 @@ __global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
 // K2: backward of the photometric term.  Workgroup = N waves (wave j = context j).
 // ---------------------------------------------------------------------------------------------
 struct K2State {
-    float X[3][3], Y[3][3], DI[3][6], SG[3];
-    float CO[3][10];  // per p-row: cA[3] cB[3] cC[3] (SSIM adjoint x 1/9 x dL/dSSIM) and the L1 factor
+    float X[3][3], Y[3][3], SG[3];
     float gT[12];
+};
+
+// Wave-private LDS rows (each lane reads back only its own column, so no barrier is needed):
+//   co[slot][m] : p-row coefficients cA[3] cB[3] cC[3] (SSIM adjoint x 1/9 x dL/dSSIM) + L1 factor
+//   di[slot][m] : d(warp_c)/d(ix), d(warp_c)/d(iy) of the row, used two rows later at q
+struct K2Lds {
+    float co[3][10][64];
+    float di[3][6][64];
 };
 
 struct K2 {
@@ -474,7 +481,7 @@ struct K2 {
                          cam);
     }
 
-    __device__ __forceinline__ void load_row(int v, float (&x)[3], float (&y)[3], float (&di)[6], float& sg) const {
+    __device__ __forceinline__ void load_row(int v, float (&x)[3], float (&y)[3], float (&di)[6][64], float& sg) const {
         const int r = reflect1(v, H);
         const size_t pix = (size_t)r * W + colr;
 #pragma unroll
@@ -488,16 +495,16 @@ struct K2 {
         bilinear3_vd(ctx, H, W, pr.ix, pr.iy, x, dix, diy);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            di[c] = dix[c];
-            di[3 + c] = diy[c];
+            di[c][lane] = dix[c];
+            di[3 + c][lane] = diy[c];
         }
     }
 
     // slots: IA = row v-2 (q), IB = row v-1 (p), IC = row v (newest)
     template <int IA, int IB, int IC>
-    __device__ __forceinline__ float step(K2State& S, int k) const {
+    __device__ __forceinline__ float step(K2State& S, K2Lds& L, int k) const {
         const int v = y0 - 2 + k;
-        load_row(v, S.X[IC], S.Y[IC], S.DI[IC], S.SG[IC]);
+        load_row(v, S.X[IC], S.Y[IC], L.di[IC], S.SG[IC]);
         if (k < 2) return 0.0f;
         // ---- SSIM adjoint coefficients of p-row pv = v-1 (cross-lane: every lane active) ----
         const int pv = v - 1;
@@ -524,11 +531,11 @@ struct K2 {
             const float kS = G * (-0.5f / 27.0f) * p.ssim_w;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                S.CO[IC][c] = kS * dmx[c];
-                S.CO[IC][3 + c] = kS * dsxx[c];
-                S.CO[IC][6 + c] = kS * dsxy[c];
+                L.co[IC][c][lane] = kS * dmx[c];
+                L.co[IC][3 + c][lane] = kS * dsxx[c];
+                L.co[IC][6 + c][lane] = kS * dsxy[c];
             }
-            S.CO[IC][9] = G * l1w * (1.0f / 3.0f);
+            L.co[IC][9][lane] = G * l1w * (1.0f / 3.0f);
         }
         if (k < 4) return 0.0f;
         // ---- adjoint of q-row qv = v-2: weighted 3x3 gather of the coefficients ----
@@ -538,7 +545,7 @@ struct K2 {
         float Sm[9];
 #pragma unroll
         for (int m = 0; m < 9; ++m) {
-            const float vsum = wyu * S.CO[IA][m] + S.CO[IB][m] + wyd * S.CO[IC][m];
+            const float vsum = wyu * L.co[IA][m][lane] + L.co[IB][m][lane] + wyd * L.co[IC][m][lane];
             Sm[m] = wxl * from_prev(vsum) + vsum + wxr * from_next(vsum);
         }
         if (!qcol) return 0.0f;
@@ -546,11 +553,10 @@ struct K2 {
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             const float xq = S.X[IA][c], yq = S.Y[IA][c];
-            const float dx = Sm[c] + 2.0f * xq * Sm[3 + c] + yq * Sm[6 + c] + S.CO[IB][9] * sgnf(xq - yq);
-            gix += dx * S.DI[IA][c];
-            giy += dx * S.DI[IA][3 + c];
+            const float dx = Sm[c] + 2.0f * xq * Sm[3 + c] + yq * Sm[6 + c] + L.co[IB][9][lane] * sgnf(xq - yq);
+            gix += dx * L.di[IA][c][lane];
+            giy += dx * L.di[IA][3 + c][lane];
         }
-        if (gix == 0.0f && giy == 0.0f) return 0.0f;
         float d1, inv;
         const float d = dc.warp_depth(S.SG[IA], d1, inv);
         Proj pr;
@@ -560,9 +566,14 @@ struct K2 {
     }
 };
 
+// dynamic LDS: N x K2Lds (wave-private rows) followed by the [2][N][64] context-sum ring
+__host__ __device__ inline size_t k2_lds_bytes(int N) { return (size_t)N * sizeof(K2Lds) + 2 * N * 64 * sizeof(float); }
+
 __global__ __launch_bounds__(256) void k2_backward(SweepArgs a) {
-    __shared__ float ring[2][PSFM_MAX_CTX][64];
+    extern __shared__ __attribute__((aligned(16))) char k2_smem[];
     const K2 K(a);
+    K2Lds& L = reinterpret_cast<K2Lds*>(k2_smem)[K.j];
+    float* ring = reinterpret_cast<float*>(k2_smem + (size_t)K.N * sizeof(K2Lds));  // [2][N][64]
     K2State S;
 #pragma unroll
     for (int m = 0; m < 12; ++m) S.gT[m] = 0.0f;
@@ -577,18 +588,18 @@ __global__ __launch_bounds__(256) void k2_backward(SweepArgs a) {
             if (K.qcol) gsig[(size_t)qv * K.W + K.col] = gs;
             return;
         }
-        ring[k & 1][K.j][K.lane] = gs;
+        ring[((k & 1) * N + K.j) * 64 + K.lane] = gs;
         __syncthreads();
         if (K.j == 0 && K.qcol) {
             float t = 0.0f;
-            for (int jj = 0; jj < N; ++jj) t += ring[k & 1][jj][K.lane];
+            for (int jj = 0; jj < N; ++jj) t += ring[((k & 1) * N + jj) * 64 + K.lane];
             gsig[(size_t)qv * K.W + K.col] = t;
         }
     };
     for (int k = 0; k < nk; k += 3) {
-        emit(k, K.step<1, 2, 0>(S, k));
-        if (k + 1 < nk) emit(k + 1, K.step<2, 0, 1>(S, k + 1));
-        if (k + 2 < nk) emit(k + 2, K.step<0, 1, 2>(S, k + 2));
+        emit(k, K.step<1, 2, 0>(S, L, k));
+        if (k + 1 < nk) emit(k + 1, K.step<2, 0, 1>(S, L, k + 1));
+        if (k + 2 < nk) emit(k + 2, K.step<0, 1, 2>(S, L, k + 2));
     }
     const int units = k2_units(a.p.H, a.p.W);
     float* o = a.ws.pose_part + ((((size_t)K.s * N + K.j) * a.p.B + K.b) * units + blockIdx.x) * 12;
