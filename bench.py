@@ -53,12 +53,15 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-kernel-timing", action="store_true", help="for rocprofv3 runs")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
+    ap.add_argument("--nchw", action="store_true", help="keep the nets in NCHW (default: channels_last)")
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
     return ap.parse_args()
 
 
-def synthetic_batch(B, H, W, device, seed):
-    """Seeded KITTI-shaped batch (BASELINE.md plan): smooth textures in [0,1], 2 contexts, K."""
+def synthetic_batch(B, H, W, device, seed, channels_last=False):
+    """Seeded KITTI-shaped batch (BASELINE.md plan): smooth textures in [0,1], 2 contexts, K.
+    Net inputs (`rgb`, `rgb_context`) optionally channels_last (MIOpen NHWC kernels, no layout
+    transposes); the loss inputs (`*_original`) stay NCHW for the HIP kernels."""
     g = torch.Generator().manual_seed(seed)
 
     def tex():
@@ -70,7 +73,11 @@ def synthetic_batch(B, H, W, device, seed):
     K = torch.tensor([[0.58 * W, 0, 0.5 * W], [0, 1.92 * H, 0.5 * H], [0, 0, 1.0]]).repeat(B, 1, 1)
     to = lambda t: t.to(device).contiguous()  # noqa: E731
     rgb, ctx, K = to(rgb), [to(c) for c in ctx], to(K)
-    return dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K)
+    batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K)
+    if channels_last:
+        cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
+        batch["rgb"], batch["rgb_context"] = cl(rgb), [cl(c) for c in ctx]
+    return batch
 
 
 def build_model(args, device):
@@ -181,10 +188,12 @@ def main():
     torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
     torch.backends.cudnn.benchmark = True
     model = build_model(args, device)
-    opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager)
+    if not args.nchw:
+        model = model.to(memory_format=torch.channels_last)
+    opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
                          graph=not args.eager)
-    batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank)
+    batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank, channels_last=not args.nchw)
 
     for _ in range(args.warmup):
         trainer.train_step(batch)
@@ -221,6 +230,8 @@ def main():
                           "model": f"{args.depth_net}+{args.pose_net}", "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "image_hw": [args.height, args.width],
                           "parallelism": f"dp{world}", "net_dtype": args.amp, "loss_dtype": "fp32",
+                          "net_layout": "NCHW" if args.nchw else "channels_last",
+                          "step": "eager" if args.eager else "hip_graph",
                           "weights": "random init (no network / checkpoints)"}}
         if ktimes:
             group = ("K1_photometric_fwd", "K2_photometric_bwd", "K3_smoothness_fwd", "K3_smoothness_bwd")

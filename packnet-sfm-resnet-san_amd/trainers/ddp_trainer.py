@@ -8,9 +8,10 @@ ranks -> optimizer.step().
 Two execution modes:
   * graph (default on a ROCm device): the step is captured into HIP graphs once and replayed —
     the eager step is host-bound (~1.5k launches, MIOpen host overhead).
-    Gradients live in ONE flat fp32 buffer (every `p.grad` is a view of it), so the cross-rank
-    average is a single RCCL all-reduce of that buffer between two graph replays
-    (fwd+bwd graph | all_reduce | scale+Adam graph); at world size 1 the whole step is one graph.
+    Autograd writes each gradient into its own (graph-static) tensor; for world size > 1 they are
+    packed into ONE flat fp32 buffer (one batched copy), averaged by a single RCCL all-reduce
+    between two graph replays (fwd+bwd+pack graph | all_reduce | unpack+Adam graph) and unpacked
+    (one foreach copy).  At world size 1 the whole step is one graph.
   * eager: torch DDP (bucketed all-reduce overlapped with backward) — CPU/gloo and debugging.
 The reference's per-step anomaly detection and `.item()` syncs are not on the hot path: the
 non-finite check accumulates on the device and is tested every `check_every` steps.
@@ -47,12 +48,13 @@ class DDPTrainer:
         self.nonfinite = torch.zeros((), device=device)
         self.world = hvd.world_size()
         self.use_graph = (device.type == "cuda") if graph is None else graph
-        # flat: one flat gradient buffer + one all-reduce per step (the graph mode's algebra;
-        # also runnable eagerly, e.g. on CPU/gloo for tests)
+        # flat: gradients packed into one flat buffer + one all-reduce per step (the graph mode's
+        # algebra; also runnable eagerly, e.g. on CPU/gloo for tests)
         self.flat = self.use_graph if flat is None else (flat or self.use_graph)
         self.graphs = None
+        self.params = [p for p in model.parameters() if p.requires_grad]
         if self.flat:
-            self._flatten_grads()
+            self._broadcast_initial()
             self.ddp = model
         elif self.world > 1:
             # static_graph: unused parameters (ResNetSAN01's LiDAR fusion weights) are detected once
@@ -62,20 +64,34 @@ class DDPTrainer:
             self.ddp = model
 
     # ------------------------------------------------------------------------------------------
-    def _flatten_grads(self):
-        params = [p for p in self.model.parameters() if p.requires_grad]
-        n = sum(p.numel() for p in params)
-        self.flat_grad = torch.zeros(n, device=self.device, dtype=torch.float32)
-        off = 0
-        for p in params:
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self.params = params
+    def _broadcast_initial(self):
         if self.world > 1:  # identical initial weights on every rank
-            for p in params:
+            for p in self.params:
                 dist.broadcast(p.data, src=0)
             for b in self.model.buffers():
                 dist.broadcast(b, src=0)
+
+    def _grads(self):
+        """(params with a gradient, their grads) — unused parameters keep grad None, like the
+        reference (Adam then skips them)."""
+        ps = [p for p in self.params if p.grad is not None]
+        return ps, [p.grad for p in ps]
+
+    def _pack(self):
+        _, grads = self._grads()
+        if not hasattr(self, "flat_grad") or self.flat_grad.numel() != sum(g.numel() for g in grads):
+            self.flat_grad = torch.empty(sum(g.numel() for g in grads), device=self.device, dtype=torch.float32)
+        torch.cat([g.reshape(-1).float() for g in grads], out=self.flat_grad)
+
+    def _unpack(self, scale):
+        _, grads = self._grads()
+        views, off = [], 0
+        for g in grads:
+            views.append(self.flat_grad[off:off + g.numel()].view_as(g))
+            off += g.numel()
+        if scale != 1.0:
+            self.flat_grad.mul_(scale)
+        torch._foreach_copy_(grads, views)
 
     def autocast(self):
         if self.amp_dtype is None or self.device.type != "cuda":
@@ -101,36 +117,37 @@ class DDPTrainer:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self.flat_grad.zero_()
+                self.optimizer.zero_grad(set_to_none=True)
                 self._forward_backward(static_batch, progress)
                 self._allreduce()
                 self.optimizer.step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.nonfinite.zero_()
+        # grads None before capture: autograd allocates them from the graph pool (static
+        # addresses, no accumulate kernels); every replay rewrites them
+        self.optimizer.zero_grad(set_to_none=True)
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.flat_grad.zero_()
                 self.static_output = self._forward_backward(static_batch, progress)
                 self.optimizer.step()
             self.graphs = (g,)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
-                self.flat_grad.zero_()
                 self.static_output = self._forward_backward(static_batch, progress)
-            pool = g1.pool()
-            with torch.cuda.graph(g2, pool=pool):
-                self.flat_grad.mul_(inv_world)
+                self._pack()
+            with torch.cuda.graph(g2, pool=g1.pool()):
+                self._unpack(inv_world)
                 self.optimizer.step()
             self.graphs = (g1, g2)
 
     def _allreduce(self):
         if self.world > 1:
+            self._pack()
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-            if self.graphs is None:
-                self.flat_grad.mul_(1.0 / self.world)
+            self._unpack(1.0 / self.world)
 
     # ------------------------------------------------------------------------------------------
     def train_step(self, batch, progress=0.0):
@@ -147,7 +164,7 @@ class DDPTrainer:
                 self.graphs[1].replay()
             output = self.static_output
         elif self.flat:
-            self.flat_grad.zero_()
+            self.optimizer.zero_grad(set_to_none=True)
             output = self._forward_backward(batch, progress)
             self._allreduce()
             self.optimizer.step()

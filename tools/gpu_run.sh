@@ -22,8 +22,10 @@ for step in "$@"; do
     prof)
       rm -rf "$OUT/prof"
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-         -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing) > "$OUT/prof.log" 2>&1; rc=$?
-      echo "[prof] rc=$rc"; tail -3 "$OUT/prof.log"; crash $rc && exit $rc ;;
+         -- python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing) > "$OUT/prof.log" 2>&1; rc=$?
+      echo "[prof] rc=$rc"; crash $rc && exit $rc
+      python3 "$ROOT/tools/summarize_trace.py" "$OUT/prof/run_kernel_trace.csv" "$OUT/prof/step_summary.txt"
+      rm -f "$OUT/prof/run_kernel_trace.csv" ;;
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
         rm -rf "$OUT/pmc_$ctr"

@@ -1,0 +1,29 @@
+"""Summarise a rocprofv3 kernel-trace CSV of bench.py: steady-state per-step kernel time by name
+(steps delimited by the K1 launches of the last N steps).  Writes a small text summary."""
+import collections
+import csv
+import sys
+
+trace, out = sys.argv[1], sys.argv[2]
+rows = list(csv.DictReader(open(trace)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+k1 = [i for i, r in enumerate(rows) if "k1_forward" in r["Kernel_Name"]]
+lines = [f"rows {len(rows)}  k1 launches {len(k1)}"]
+if len(k1) >= 3:
+    n = min(len(k1) - 1, 8)  # the last graph replays only (warm-up includes MIOpen find)
+    i0, i1 = k1[-n - 1], k1[-1]
+    t0, t1 = int(rows[i0]["Start_Timestamp"]), int(rows[i1]["Start_Timestamp"])
+    agg = collections.defaultdict(lambda: [0, 0])
+    busy = 0
+    for r in rows[i0:i1]:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        busy += d
+        a = agg[r["Kernel_Name"][:110]]
+        a[0] += d
+        a[1] += 1
+    lines.append(f"steps {n}  wall ms/step {(t1 - t0) / 1e6 / n:.3f}  busy ms/step {busy / 1e6 / n:.3f}  "
+                 f"kernels/step {(i1 - i0) / n:.1f}")
+    for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
+        lines.append(f"{v[0] / 1e3 / n:9.1f} us/step  n/step={v[1] / n:6.1f}  {k}")
+open(out, "w").write("\n".join(lines) + "\n")
+print("\n".join(lines[:3]))
