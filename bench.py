@@ -192,7 +192,7 @@ def main():
         model = model.to(memory_format=torch.channels_last)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
-                         graph=not args.eager)
+                         graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager))
     batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank, channels_last=not args.nchw)
 
     for _ in range(args.warmup):
@@ -232,6 +232,8 @@ def main():
                           "parallelism": f"dp{world}", "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
+                          "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
+                          else "fp32",
                           "weights": "random init (no network / checkpoints)"}}
         if ktimes:
             group = ("K1_photometric_fwd", "K2_photometric_bwd", "K3_smoothness_fwd", "K3_smoothness_bwd")

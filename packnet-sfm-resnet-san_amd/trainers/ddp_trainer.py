@@ -38,7 +38,7 @@ def make_optimizer(model, depth_lr=1e-4, pose_lr=1e-4, name="Adam", **kw):
 
 class DDPTrainer:
     def __init__(self, model, optimizer, device, amp_dtype=torch.bfloat16, bucket_cap_mb=64,
-                 check_every=0, graph=None, flat=None):
+                 check_every=0, graph=None, flat=None, bf16_weights=False):
         self.device = device
         self.model = model
         self.optimizer = optimizer
@@ -53,6 +53,11 @@ class DDPTrainer:
         self.flat = self.use_graph if flat is None else (flat or self.use_graph)
         self.graphs = None
         self.params = [p for p in model.parameters() if p.requires_grad]
+        self.mp = None
+        if bf16_weights:
+            from .mixed_precision import Bf16MasterWeights
+            assert self.flat, "bf16 master weights need the flat (graph) gradient path"
+            self.mp = Bf16MasterWeights(model, optimizer, dtype=amp_dtype or torch.bfloat16)
         if self.flat:
             self._broadcast_initial()
             self.ddp = model
@@ -72,9 +77,9 @@ class DDPTrainer:
                 dist.broadcast(b, src=0)
 
     def _grads(self):
-        """(params with a gradient, their grads) — unused parameters keep grad None, like the
-        reference (Adam then skips them)."""
-        ps = [p for p in self.params if p.grad is not None]
+        """(optimizer params with a gradient, their grads) — unused parameters keep grad None,
+        like the reference (Adam then skips them).  With bf16 weights these are the fp32 masters."""
+        ps = [p for g in self.optimizer.param_groups for p in g["params"] if p.grad is not None]
         return ps, [p.grad for p in ps]
 
     def _pack(self):
@@ -105,7 +110,14 @@ class DDPTrainer:
         loss = output["loss"]
         loss.sum().backward()
         self.nonfinite += (~torch.isfinite(loss.detach())).any().float()
+        if self.mp is not None:
+            self.mp.grads_to_master()
         return output
+
+    def _opt_step(self):
+        self.optimizer.step()
+        if self.mp is not None:
+            self.mp.master_to_model()
 
     # ------------------------------------------------------------------------------------------
     def capture(self, static_batch, warmup=3, progress=0.0):
@@ -117,21 +129,21 @@ class DDPTrainer:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self.optimizer.zero_grad(set_to_none=True)
+                self._zero_grad()
                 self._forward_backward(static_batch, progress)
                 self._allreduce()
-                self.optimizer.step()
+                self._opt_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.nonfinite.zero_()
         # grads None before capture: autograd allocates them from the graph pool (static
         # addresses, no accumulate kernels); every replay rewrites them
-        self.optimizer.zero_grad(set_to_none=True)
+        self._zero_grad()
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.static_output = self._forward_backward(static_batch, progress)
-                self.optimizer.step()
+                self._opt_step()
             self.graphs = (g,)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -140,8 +152,16 @@ class DDPTrainer:
                 self._pack()
             with torch.cuda.graph(g2, pool=g1.pool()):
                 self._unpack(inv_world)
-                self.optimizer.step()
+                self._opt_step()
             self.graphs = (g1, g2)
+
+    def _zero_grad(self):
+        """Model grads -> None (autograd then owns fresh, graph-static tensors); the fp32 master
+        grads of the bf16 path are persistent buffers, overwritten every step."""
+        for p in self.params:
+            p.grad = None
+        if self.mp is None:
+            self.optimizer.zero_grad(set_to_none=True)
 
     def _allreduce(self):
         if self.world > 1:
@@ -164,10 +184,10 @@ class DDPTrainer:
                 self.graphs[1].replay()
             output = self.static_output
         elif self.flat:
-            self.optimizer.zero_grad(set_to_none=True)
+            self._zero_grad()
             output = self._forward_backward(batch, progress)
             self._allreduce()
-            self.optimizer.step()
+            self._opt_step()
         else:
             self.optimizer.zero_grad(set_to_none=True)
             output = self._forward_backward(batch, progress)
