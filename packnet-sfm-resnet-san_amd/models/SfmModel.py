@@ -2,6 +2,8 @@
 inverse-depth scales to full resolution) and pose net (vectors -> Pose)."""
 import random
 
+import torch
+
 from ..geometry.pose import Pose
 from .base_model import BaseModel
 from .model_utils import flip_batch_input, flip_output, upsample_output
@@ -9,9 +11,16 @@ from ..utils.misc import filter_dict
 
 
 class SfmModel(BaseModel):
+    """`overlap_pose_net`: on a ROCm device, run the pose net on a side HIP stream forked from the
+    current one (it depends only on the input images), concurrently with the depth net; its
+    backward runs on the same side stream.  Captured into the training-step HIP graph as a
+    parallel branch.  Numerically identical to the serial order."""
+
     def __init__(self, depth_net=None, pose_net=None, rotation_mode="euler", flip_lr_prob=0.0,
-                 upsample_depth_maps=False, **kwargs):
+                 upsample_depth_maps=False, overlap_pose_net=True, **kwargs):
         super().__init__()
+        self.overlap_pose_net = overlap_pose_net
+        self._side_streams = {}
         self.depth_net = depth_net
         self.pose_net = pose_net
         self.rotation_mode = rotation_mode
@@ -42,9 +51,26 @@ class SfmModel(BaseModel):
         pose_vec = self.pose_net(image, contexts).float()  # pose algebra in fp32 (nets may be bf16)
         return [Pose.from_vec(pose_vec[:, i], self.rotation_mode) for i in range(pose_vec.shape[1])]
 
+    def _side_stream(self, device):
+        if device not in self._side_streams:
+            self._side_streams[device] = torch.cuda.Stream(device=device)
+        return self._side_streams[device]
+
     def forward(self, batch, return_logs=False, force_flip=False, **kwargs):
-        depth_output = self.compute_depth_net(batch, force_flip=force_flip, **kwargs)
         poses = None
-        if "rgb_context" in batch and self.pose_net is not None:
-            poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
+        want_pose = "rgb_context" in batch and self.pose_net is not None
+        if want_pose and self.overlap_pose_net and batch["rgb"].is_cuda:
+            cur = torch.cuda.current_stream(batch["rgb"].device)
+            side = self._side_stream(batch["rgb"].device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
+            depth_output = self.compute_depth_net(batch, force_flip=force_flip, **kwargs)
+            cur.wait_stream(side)
+            for p in poses:  # allocated on the side stream, consumed on the current one
+                p.mat.record_stream(cur)
+        else:
+            depth_output = self.compute_depth_net(batch, force_flip=force_flip, **kwargs)
+            if want_pose:
+                poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
         return {**depth_output, "poses": poses}

@@ -23,14 +23,15 @@ def native_bn_forward(self, x):
 
 
 res = {}
-variants = [("base", {}), ("bf16w", {"bf16_weights": True})]
+variants = [("serial", {"overlap": False}), ("overlap", {"overlap": True})]
 for name, kw in variants:
     torch.nn.BatchNorm2d.forward = native_bn_forward if kw.get("native_bn") else _orig_bn
     torch.manual_seed(0)
     model = bench.build_model(args, dev).to(memory_format=torch.channels_last)
+    model.overlap_pose_net = kw.get("overlap", True)
     batch = bench.synthetic_batch(4, 192, 640, dev, 0, channels_last=True)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=True)
-    tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16, bf16_weights=kw.get("bf16_weights", False))
+    tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16, bf16_weights=True)
     try:
         for _ in range(5):
             tr.train_step(batch)
