@@ -73,6 +73,12 @@ def lib():
         "psfm_tiles_per_image": ([c_int, c_int], c_int),
         "psfm_last_error": ([], ctypes.c_char_p),
         "psfm_version": ([], ctypes.c_char_p),
+        # include/psfm_optim.h
+        "psfm_optim_plan_chunks": ([c_int, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32), c_int],
+                                   c_int),
+        "psfm_grad_pack": ([V, V, c_int, V, V], c_int),
+        "psfm_adam_step": ([V, V, c_int, V, V, V, c_float, V, V, V, V], c_int),
+        "psfm_optim_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -84,12 +90,15 @@ def lib():
 EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photometric_fwd",
             "psfm_smoothness_fwd", "psfm_finalize", "psfm_photometric_bwd", "psfm_smoothness_bwd",
             "psfm_pose_grad_reduce", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
-            "psfm_tiles_per_image", "psfm_last_error", "psfm_version")
+            "psfm_tiles_per_image", "psfm_last_error", "psfm_version",
+            "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error")
 
 
 def check(rc, what):
     if rc != 0:
-        raise RuntimeError(f"{what} failed ({rc}): {lib().psfm_last_error().decode()}")
+        err = lib().psfm_optim_last_error if what.startswith(("psfm_optim", "psfm_grad", "psfm_adam")) \
+            else lib().psfm_last_error
+        raise RuntimeError(f"{what} failed ({rc}): {err().decode()}")
 
 
 def require_device(*tensors):

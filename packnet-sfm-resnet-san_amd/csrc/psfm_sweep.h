@@ -26,24 +26,55 @@
 namespace psfm {
 namespace sweep {
 
-constexpr int RB = 16;   // output rows per band
-constexpr int K1W = 62;  // output columns per K1 stripe (halo 1)
-constexpr int K2W = 60;  // output columns per K2 stripe (halo 2)
+#ifndef PSFM_K1_RB
+#define PSFM_K1_RB 12
+#endif
+#ifndef PSFM_K2_RB
+#define PSFM_K2_RB 24
+#endif
+#ifndef PSFM_XCD_REMAP
+#define PSFM_XCD_REMAP 1
+#endif
+constexpr int K1RB = PSFM_K1_RB;  // output rows per K0/K1 band
+constexpr int K2RB = PSFM_K2_RB;  // output rows per K2 band
+constexpr int K1W = 62;           // output columns per K1 stripe (halo 1)
+constexpr int K2W = 60;           // output columns per K2 stripe (halo 2)
 
-__host__ __device__ inline int bands(int H) { return (H + RB - 1) / RB; }
 __host__ __device__ inline int k1_stripes(int W) { return (W + K1W - 1) / K1W; }
 __host__ __device__ inline int k2_stripes(int W) { return (W + K2W - 1) / K2W; }
-__host__ __device__ inline int k1_units(int H, int W) { return k1_stripes(W) * bands(H); }
-__host__ __device__ inline int k2_units(int H, int W) { return k2_stripes(W) * bands(H); }
+__host__ __device__ inline int k1_units(int H, int W) { return k1_stripes(W) * ((H + K1RB - 1) / K1RB); }
+__host__ __device__ inline int k2_units(int H, int W) { return k2_stripes(W) * ((H + K2RB - 1) / K2RB); }
+
+// Which (unit, batch, scale) this workgroup sweeps.  Grid = (units, B, S).  With PSFM_XCD_REMAP
+// the linear block id is re-dealt so that the blocks one XCD receives (round-robin dealing:
+// blocks i and i+8 share an XCD) form one contiguous run of (b, s, unit) -> one image's context
+// frames stay in that XCD's L2 (speed only: any placement is correct).
+struct WorkItem {
+    int unit, b, s;
+};
+__device__ __forceinline__ WorkItem work_item() {
+#if PSFM_XCD_REMAP
+    const int units = gridDim.x, B = gridDim.y, S = gridDim.z;
+    const int T = units * B * S;
+    const int L = blockIdx.x + units * (blockIdx.y + B * blockIdx.z);
+    const int xcd = L & 7, i = L >> 3, q = T >> 3, r = T & 7;
+    const int w = xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+    const int bs = w / units;
+    return WorkItem{w - bs * units, bs / S, bs % S};
+#else
+    return WorkItem{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+#endif
+}
 
 template <int I>
 using Slot = std::integral_constant<int, I>;
 
+// bound_ctrl: the lane without a source reads 0 (no `old` operand to materialise)
 __device__ __forceinline__ float from_prev(float v) {  // lane l <- lane l-1 (lane 0 <- 0)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float from_next(float v) {  // lane l <- lane l+1 (lane 63 <- 0)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float hsum3(float v) { return from_prev(v) + v + from_next(v); }
 
@@ -156,9 +187,10 @@ __global__ __launch_bounds__(64) void k0_unwarped(SweepArgs a) {
     const psfm_params& p = a.p;
     const int H = p.H, W = p.W, B = p.B;
     const size_t plane = (size_t)H * W;
-    const int nst = k1_stripes(W), b = blockIdx.y;
-    const int y0 = (blockIdx.x / nst) * RB;
-    const int col = (blockIdx.x % nst) * K1W - 1 + (int)threadIdx.x;
+    const WorkItem wi = work_item();
+    const int nst = k1_stripes(W), b = wi.b;
+    const int y0 = (wi.unit / nst) * K1RB;
+    const int col = (wi.unit % nst) * K1W - 1 + (int)threadIdx.x;
     const int colr = reflect1(col, W);
     const bool pcol = threadIdx.x >= 1 && threadIdx.x <= K1W && col < W;
     const float l1w = 1.0f - p.ssim_w;
@@ -176,7 +208,7 @@ __global__ __launch_bounds__(64) void k0_unwarped(SweepArgs a) {
     auto emit = [&](int k, float (&ya)[3], float (&yb)[3], float (&yc)[3], float (&xa)[NC][3],
                     float (&xb)[NC][3], float (&xc)[NC][3]) {
         const int pv = y0 - 2 + k;
-        if (k < 2 || pv >= H || pv >= y0 + RB) return;  // wave-uniform
+        if (k < 2 || pv >= H || pv >= y0 + K1RB) return;  // wave-uniform
         float my[3], syy[3];
         target_window(ya, yb, yc, my, syy);
 #pragma unroll
@@ -195,7 +227,7 @@ __global__ __launch_bounds__(64) void k0_unwarped(SweepArgs a) {
             if (pcol) a.ws.unwarp[((size_t)j * B + b) * plane + (size_t)pv * W + col] = val;
         }
     };
-    const int nk = RB + 2;
+    const int nk = K1RB + 2;
     for (int k = 0; k < nk; k += 3) {
         load(y0 - 1 + k, Y[0], X[0]);
         emit(k, Y[1], Y[2], Y[0], X[1], X[2], X[0]);
@@ -225,7 +257,7 @@ template <int NC, bool STATS>
 struct K1 {
     const SweepArgs& a;
     const psfm_params& p;
-    int H, W, b, s, y0, col, colr, B;
+    int H, W, b, s, unit, y0, col, colr, B;
     size_t plane;
     bool pcol;
     DepthChain dc;
@@ -242,10 +274,12 @@ struct K1 {
         B = p.B;
         plane = (size_t)H * W;
         const int nst = k1_stripes(W);
-        b = blockIdx.y;
-        s = blockIdx.z;
-        y0 = (blockIdx.x / nst) * RB;
-        col = (blockIdx.x % nst) * K1W - 1 + (int)threadIdx.x;
+        const WorkItem wi = work_item();
+        b = wi.b;
+        s = wi.s;
+        unit = wi.unit;
+        y0 = (unit / nst) * K1RB;
+        col = (unit % nst) * K1W - 1 + (int)threadIdx.x;
         colr = reflect1(col, W);
         pcol = threadIdx.x >= 1 && threadIdx.x <= K1W && col < W;
         dc = depth_chain(p);
@@ -283,7 +317,7 @@ struct K1 {
         load_row(v, S.Y[IC], S.XW[IC], S.SG[IC]);
         if (k < 2) return;
         const int pv = v - 1;
-        if (pv >= H || pv >= y0 + RB) return;  // wave-uniform
+        if (pv >= H || pv >= y0 + K1RB) return;  // wave-uniform
         // ---- cross-lane phase (every lane active) ----
         float my[3], syy[3];
         target_window(S.Y[IA], S.Y[IB], S.Y[IC], my, syy);
@@ -378,7 +412,7 @@ __global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;
 #pragma unroll
     for (int k = 0; k < 2 * NC; ++k) S.st[k][0] = S.st[k][1] = 0.0f;
-    const int nk = RB + 2;  // rows y0-1 .. y0+RB
+    const int nk = K1RB + 2;  // rows y0-1 .. y0+K1RB
     for (int k = 0; k < nk; k += 3) {
         K.template step<1, 2, 0>(S, k);
         if (k + 1 < nk) K.template step<2, 0, 1>(S, k + 1);
@@ -386,7 +420,7 @@ __global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
     }
     const psfm_params& p = a.p;
     const int units = k1_units(p.H, p.W);
-    const int blk = K.b * units + blockIdx.x;
+    const int blk = K.b * units + K.unit;
     if (STATS) {
         const int nsrc = p.automask ? 2 * NC : NC;
         for (int k = 0; k < nsrc; ++k) {
@@ -404,7 +438,7 @@ __global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
     if (threadIdx.x == 0) {
         a.ws.photo_part[(size_t)K.s * (p.B * units) + blk] = ph;
         if (p.smooth_w > 0.0f) {
-            float* o = a.ws.smooth_part + (((size_t)K.s * p.B + K.b) * units + blockIdx.x) * 4;
+            float* o = a.ws.smooth_part + (((size_t)K.s * p.B + K.b) * units + K.unit) * 4;
             o[0] = ax;
             o[1] = ay;
             o[2] = m;
@@ -432,7 +466,7 @@ struct K2Lds {
 struct K2 {
     const SweepArgs& a;
     const psfm_params& p;
-    int H, W, B, N, b, s, j, y0, col, colr, lane, src;
+    int H, W, B, N, b, s, unit, j, y0, col, colr, lane, src;
     size_t plane;
     bool pcol, qcol;
     DepthChain dc;
@@ -452,12 +486,14 @@ struct K2 {
         N = p.N;
         plane = (size_t)H * W;
         const int nst = k2_stripes(W);
-        b = blockIdx.y;
-        s = blockIdx.z;
+        const WorkItem wi = work_item();
+        b = wi.b;
+        s = wi.s;
+        unit = wi.unit;
         lane = threadIdx.x & 63;
         j = threadIdx.x >> 6;
-        y0 = (blockIdx.x / nst) * RB;
-        col = (blockIdx.x % nst) * K2W - 2 + lane;
+        y0 = (unit / nst) * K2RB;
+        col = (unit % nst) * K2W - 2 + lane;
         colr = reflect1(col, W);
         pcol = lane >= 1 && lane <= K2W + 2 && col >= 0 && col < W;
         qcol = lane >= 2 && lane <= K2W + 1 && col < W;
@@ -540,7 +576,7 @@ struct K2 {
         if (k < 4) return 0.0f;
         // ---- adjoint of q-row qv = v-2: weighted 3x3 gather of the coefficients ----
         const int qv = v - 2;
-        if (qv >= H || qv >= y0 + RB) return 0.0f;  // wave-uniform
+        if (qv >= H || qv >= y0 + K2RB) return 0.0f;  // wave-uniform
         const float wyu = (qv == 1) ? 2.0f : 1.0f, wyd = (qv == H - 2) ? 2.0f : 1.0f;
         float Sm[9];
 #pragma unroll
@@ -577,13 +613,13 @@ __global__ __launch_bounds__(256) void k2_backward(SweepArgs a) {
     K2State S;
 #pragma unroll
     for (int m = 0; m < 12; ++m) S.gT[m] = 0.0f;
-    const int nk = RB + 4;  // rows y0-2 .. y0+RB+1
+    const int nk = K2RB + 4;  // rows y0-2 .. y0+K2RB+1
     float* gsig = pick4(a.grad_sig, K.s) + (size_t)K.b * K.plane;
     const int N = K.N;
     auto emit = [&](int k, float gs) {
         if (k < 4) return;
         const int qv = K.y0 - 4 + k;
-        if (qv >= K.H || qv >= K.y0 + RB) return;
+        if (qv >= K.H || qv >= K.y0 + K2RB) return;
         if (N == 1) {
             if (K.qcol) gsig[(size_t)qv * K.W + K.col] = gs;
             return;
@@ -602,7 +638,7 @@ __global__ __launch_bounds__(256) void k2_backward(SweepArgs a) {
         if (k + 2 < nk) emit(k + 2, K.step<0, 1, 2>(S, L, k + 2));
     }
     const int units = k2_units(a.p.H, a.p.W);
-    float* o = a.ws.pose_part + ((((size_t)K.s * N + K.j) * a.p.B + K.b) * units + blockIdx.x) * 12;
+    float* o = a.ws.pose_part + ((((size_t)K.s * N + K.j) * a.p.B + K.b) * units + K.unit) * 12;
 #pragma unroll
     for (int m = 0; m < 12; ++m) {
         const float t = wave_sum64(S.gT[m]);

@@ -38,7 +38,7 @@ def make_optimizer(model, depth_lr=1e-4, pose_lr=1e-4, name="Adam", **kw):
 
 class DDPTrainer:
     def __init__(self, model, optimizer, device, amp_dtype=torch.bfloat16, bucket_cap_mb=64,
-                 check_every=0, graph=None, flat=None, bf16_weights=False):
+                 check_every=0, graph=None, flat=None, bf16_weights=False, fused_optim=None):
         self.device = device
         self.model = model
         self.optimizer = optimizer
@@ -53,11 +53,17 @@ class DDPTrainer:
         self.flat = self.use_graph if flat is None else (flat or self.use_graph)
         self.graphs = None
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.mp = None
+        self.mp = self.fused = None
         if bf16_weights:
-            from .mixed_precision import Bf16MasterWeights
             assert self.flat, "bf16 master weights need the flat (graph) gradient path"
-            self.mp = Bf16MasterWeights(model, optimizer, dtype=amp_dtype or torch.bfloat16)
+            if fused_optim is None:
+                fused_optim = device.type == "cuda"
+            if fused_optim:  # one HIP kernel: grad widening + Adam + weight rounding (fused_adam.py)
+                from .fused_adam import FusedMixedAdam
+                self.fused = FusedMixedAdam(model, optimizer, device, lowp_dtype=amp_dtype or torch.bfloat16)
+            else:
+                from .mixed_precision import Bf16MasterWeights
+                self.mp = Bf16MasterWeights(model, optimizer, dtype=amp_dtype or torch.bfloat16)
         if self.flat:
             self._broadcast_initial()
             self.ddp = model
@@ -75,6 +81,11 @@ class DDPTrainer:
                 dist.broadcast(p.data, src=0)
             for b in self.model.buffers():
                 dist.broadcast(b, src=0)
+            if self.fused is not None:
+                dist.broadcast(self.fused.master, src=0)
+            if self.mp is not None:
+                for mp in self.mp.master:
+                    dist.broadcast(mp, src=0)
 
     def _grads(self):
         """(optimizer params with a gradient, their grads) — unused parameters keep grad None,
@@ -82,7 +93,12 @@ class DDPTrainer:
         ps = [p for g in self.optimizer.param_groups for p in g["params"] if p.grad is not None]
         return ps, [p.grad for p in ps]
 
-    def _pack(self):
+    def _pack(self, capturing=False):
+        if self.fused is not None:
+            if not hasattr(self, "flat_grad"):
+                self.flat_grad = self.fused.new_flat_grad()
+            self.fused.pack(self.flat_grad, capturing)
+            return
         _, grads = self._grads()
         if not hasattr(self, "flat_grad") or self.flat_grad.numel() != sum(g.numel() for g in grads):
             self.flat_grad = torch.empty(sum(g.numel() for g in grads), device=self.device, dtype=torch.float32)
@@ -114,7 +130,13 @@ class DDPTrainer:
             self.mp.grads_to_master()
         return output
 
-    def _opt_step(self):
+    def _opt_step(self, capturing=False):
+        if self.fused is not None:  # world > 1: Adam reads the all-reduced flat buffer directly
+            if self.world > 1:
+                self.fused.step(self.flat_grad, 1.0 / self.world, capturing)
+            else:
+                self.fused.step(None, 1.0, capturing)
+            return
         self.optimizer.step()
         if self.mp is not None:
             self.mp.master_to_model()
@@ -124,6 +146,7 @@ class DDPTrainer:
         """Warm up on a side stream (MIOpen algorithm selection, allocator), then capture."""
         assert self.use_graph
         self.static_batch = static_batch
+        self._detach_bn_counters(warmup)
         inv_world = 1.0 / self.world
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -143,34 +166,60 @@ class DDPTrainer:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.static_output = self._forward_backward(static_batch, progress)
-                self._opt_step()
+                self._opt_step(capturing=True)
             self.graphs = (g,)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self.static_output = self._forward_backward(static_batch, progress)
-                self._pack()
+                self._pack(capturing=True)
             with torch.cuda.graph(g2, pool=g1.pool()):
-                self._unpack(inv_world)
-                self._opt_step()
+                if self.fused is None:
+                    self._unpack(inv_world)
+                self._opt_step(capturing=True)
             self.graphs = (g1, g2)
+        if self.fused is not None:  # gradient addresses of the captured graph -> kernel tables
+            self.fused.finish_capture()
+
+    def _detach_bn_counters(self, warmup):
+        """BatchNorm's `num_batches_tracked += 1` is one kernel per BN layer per step and is only
+        read when momentum is None (cumulative average).  With a fixed momentum the counters are
+        taken out of the replayed step and kept on the host; `bn_counters_to_model()` writes them
+        back (state_dict compatible with the reference's checkpoints)."""
+        self._bn = []
+        for m in self.model.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.track_running_stats \
+                    and m.momentum is not None and m.num_batches_tracked is not None:
+                self._bn.append((m, m.num_batches_tracked))
+                m.num_batches_tracked = None
+        self._bn_warmup, self._bn_step0 = warmup, self.step_idx
+
+    def bn_counters_to_model(self):
+        """Re-attach the BatchNorm step counters (value = counter at capture + steps run)."""
+        for m, t in getattr(self, "_bn", []):
+            t.add_(self._bn_warmup + self.step_idx - self._bn_step0)
+            m.num_batches_tracked = t
+        self._bn = []
 
     def _zero_grad(self):
         """Model grads -> None (autograd then owns fresh, graph-static tensors); the fp32 master
         grads of the bf16 path are persistent buffers, overwritten every step."""
         for p in self.params:
             p.grad = None
-        if self.mp is None:
+        if self.mp is None and self.fused is None:
             self.optimizer.zero_grad(set_to_none=True)
 
     def _allreduce(self):
         if self.world > 1:
             self._pack()
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-            self._unpack(1.0 / self.world)
+            if self.fused is None:
+                self._unpack(1.0 / self.world)
 
     # ------------------------------------------------------------------------------------------
     def train_step(self, batch, progress=0.0):
+        if self.fused is not None:
+            self.fused.sync_hparams()  # lr schedulers act on optimizer.param_groups
         if self.use_graph:
             if self.graphs is None:
                 self.capture(batch, progress=progress)

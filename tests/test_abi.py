@@ -18,9 +18,12 @@ def hip():
 
 
 def declared_functions():
-    src = open(os.path.join(ROOT, "include", "psfm.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src)))
+    names = set()
+    for h in ("psfm.h", "psfm_optim.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_every_declared_symbol_is_exported(hip):
@@ -73,3 +76,18 @@ def test_product_path_refuses_cpu_tensors(hip):
         fn(torch.rand(B, 3, H, W), [torch.rand(B, 3, H, W)] * 2, [torch.rand(B, 1, H, W)] * 4,
            torch.eye(3).expand(B, 3, 3), torch.eye(3).expand(B, 3, 3),
            [Pose.identity(B)] * 2)
+
+
+def test_optim_plan_chunks(hip):
+    """host-side work split of the fused Adam step (include/psfm_optim.h)"""
+    L = hip.lib()
+    numel = (ctypes.c_int64 * 4)(1, 1024, 1025, 3000)
+    n = L.psfm_optim_plan_chunks(4, numel, None, 0)
+    assert n == 1 + 1 + 2 + 3
+    buf = (ctypes.c_int32 * (2 * n))()
+    assert L.psfm_optim_plan_chunks(4, numel, buf, n) == n
+    assert list(buf) == [0, 0, 1, 0, 2, 0, 2, 1024, 3, 0, 3, 1024, 3, 2048]
+    assert L.psfm_optim_plan_chunks(4, numel, buf, n - 1) == -3
+    assert L.psfm_optim_last_error()
+    assert L.psfm_grad_pack(None, None, 1, None, None) == -1
+    assert L.psfm_adam_step(None, None, 1, None, None, None, ctypes.c_float(1.0), None, None, None, None) == -1
