@@ -11,7 +11,7 @@ crash() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 for step in "$@"; do
   case $step in
     tests)
-      timeout -k 10 500 python -m pytest "$ROOT/tests" -m gpu -q -rs > "$OUT/gpu_tests.log" 2>&1; rc=$?
+      timeout -k 10 500 python -u -m pytest "$ROOT/tests" -m gpu -x -v -rs --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1; rc=$?
       echo "[tests] rc=$rc"; tail -3 "$OUT/gpu_tests.log"; crash $rc && exit $rc ;;
     smoke)
       (cd "$ROOT" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()") > "$OUT/smoke.log" 2>&1; rc=$?
@@ -33,6 +33,17 @@ for step in "$@"; do
            -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --no-kernel-timing) > "$OUT/pmc_$ctr.log" 2>&1; rc=$?
         echo "[pmc $ctr] rc=$rc"; tail -2 "$OUT/pmc_$ctr.log"; crash $rc && exit $rc
       done ;;
+    kpmc)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        rm -rf "$OUT/kpmc_$ctr"
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/kpmc_$ctr" -o run \
+           -- python3 "$ROOT/tools/kbench.py" --iters 3) > "$OUT/kpmc_$ctr.log" 2>&1; rc=$?
+        echo "[kpmc $ctr] rc=$rc"; tail -2 "$OUT/kpmc_$ctr.log"; crash $rc && exit $rc
+      done
+      python3 "$ROOT/tools/pmc_traffic.py" "$OUT/kpmc_FETCH_SIZE" "$OUT/kpmc_WRITE_SIZE" "$OUT/pmc_traffic.json" 4 > /dev/null; echo "[kpmc] agg rc=$?" ;;
+    kbench)
+      (cd "$ROOT" && timeout -k 10 300 python tools/kbench.py --iters 30) > "$OUT/kbench.log" 2>&1; rc=$?
+      echo "[kbench] rc=$rc"; tail -3 "$OUT/kbench.log"; crash $rc && exit $rc ;;
   esac
 done
 exit 0

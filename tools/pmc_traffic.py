@@ -1,0 +1,57 @@
+"""Aggregate rocprofv3 FETCH_SIZE / WRITE_SIZE passes over tools/kbench.py into per-launch HBM
+traffic of the photometric kernels, written to profiles/pmc_traffic.json (read by bench.py's
+`roofline.traffic`).
+
+Corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE is in KiB and, on gfx950, reports
+half the bytes of wide coalesced reads -> bytes = 2 * 1024 * FETCH_SIZE.  WRITE_SIZE is in KiB and
+exact for streaming stores -> bytes = 1024 * WRITE_SIZE.  Both count Infinity-Cache hits.
+
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [images_per_launch]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+GROUP = {"k1_forward": "K1_photometric_fwd", "k0_unwarped": "K1_photometric_fwd",
+         "k2_backward": "K2_photometric_bwd", "k_smooth_bwd": "K3_smoothness_bwd"}
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    assert files, f"no counter_collection.csv under {d}"
+    acc = collections.defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"]
+            for key, grp in GROUP.items():
+                if key in name:
+                    acc[(grp, name[:80])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    imgs = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+    fetch, nf = per_kernel(fdir, "FETCH_SIZE")
+    write, _ = per_kernel(wdir, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        rd = 2 * 1024 * fetch.get(k, 0.0)
+        wr = 1024 * write.get(k, 0.0)
+        kernels[k[1]] = {"group": k[0], "read_bytes": round(rd), "write_bytes": round(wr),
+                         "dispatches_sampled": nf.get(k, 0)}
+    total = sum(v["read_bytes"] + v["write_bytes"] for v in kernels.values())
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over tools/kbench.py",
+           "correction": "read = 2*1024*FETCH_SIZE (gfx950 half-count), write = 1024*WRITE_SIZE",
+           "images_per_launch": imgs, "bytes_per_step": total, "kernels": kernels}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
