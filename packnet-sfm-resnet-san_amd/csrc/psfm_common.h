@@ -61,13 +61,26 @@ __device__ __forceinline__ void load_cam_uniform(const float* __restrict__ p, Ca
     for (int i = 0; i < 12; ++i) c.T[i] = sgpr(p[18 + i]);
 }
 
+// fp32 reciprocal / quotient from v_rcp_f32 (1 ulp) refined by one Newton step, then one
+// residual correction of the quotient: the correctly rounded IEEE result except in rare
+// double-rounding cases (then 1 ulp), for the finite, normal operands of this path (|b| in
+// [1e-8, 1e12]).  3 / +3 VALU instead of the ~10-instruction v_div_scale/fmas/fixup sequence.
+__device__ __forceinline__ float rcp_nr(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float div_nr(float a, float b, float rb /* rcp_nr(b) */) {
+    const float q = a * rb;
+    return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
+}
+
 // sigmoid -> depth (post_process_depth.py:101-106) -> inv (:369) -> warp depth (depth.py:120)
 struct DepthChain {
     float lo, rng;
     __device__ __forceinline__ float warp_depth(float s, float& d1, float& inv) const {
-        d1 = 1.0f / (lo + rng * s + 1e-8f);
-        inv = 1.0f / (d1 + 1e-8f);
-        return 1.0f / fmaxf(inv, 1e-6f);
+        d1 = rcp_nr(lo + rng * s + 1e-8f);
+        inv = rcp_nr(d1 + 1e-8f);
+        return rcp_nr(fmaxf(inv, 1e-6f));
     }
     // d(warp depth)/ds with torch's reciprocal-backward form (-out^2) at every 1/x
     __device__ __forceinline__ float dwarp_ds(float d, float d1, float inv) const {
@@ -83,30 +96,53 @@ struct Proj {
     float xn0, xn1, xn2;  // K^-1 [u v 1]
     float X0, X1, X2;     // lifted point
     float p0, p1, p2;     // K_ref (R X + t)
-    float z;              // clamp(p2, 1e-5)
+    float z, iz;          // clamp(p2, 1e-5) and its reciprocal
     float ix, iy;         // sampling position in pixels
 };
 
+// Lifted ray / point of one pixel (Camera.reconstruct): shared by every context of a target.
+struct Lift {
+    float xn0, xn1, xn2, X0, X1, X2;
+};
+__device__ __forceinline__ Lift lift(const float (&Ki)[9], float u, float v, float d) {
+    Lift l;
+    l.xn0 = Ki[0] * u + Ki[1] * v + Ki[2];
+    l.xn1 = Ki[3] * u + Ki[4] * v + Ki[5];
+    l.xn2 = Ki[6] * u + Ki[7] * v + Ki[8];
+    l.X0 = l.xn0 * d;
+    l.X1 = l.xn1 * d;
+    l.X2 = l.xn2 * d;
+    return l;
+}
+
+// Normalise to [-1,1] and back (Camera.project :172-176 then grid_sample's align_corners
+// unnormalisation): ((2 (p/z) / (S-1) - 1) + 1) / 2 * (S-1), each rounding kept.
+__device__ __forceinline__ float norm_roundtrip(float pz, float sm1, float rsm1 /* rcp_nr(sm1) */) {
+    const float n = div_nr(2.0f * pz, sm1, rsm1) - 1.0f;
+    return ((n + 1.0f) * 0.5f) * sm1;
+}
+
+// Transform + project one lifted point into one context camera (T = [R|t], Kr).
+__device__ __forceinline__ void project_lifted(const float (&T)[12], const float (&Kr)[9], const Lift& l,
+                                               float wm1, float rwm1, float hm1, float rhm1, Proj& r) {
+    r.xn0 = l.xn0; r.xn1 = l.xn1; r.xn2 = l.xn2;
+    r.X0 = l.X0; r.X1 = l.X1; r.X2 = l.X2;
+    const float c0 = T[0] * r.X0 + T[1] * r.X1 + T[2] * r.X2 + T[3];
+    const float c1 = T[4] * r.X0 + T[5] * r.X1 + T[6] * r.X2 + T[7];
+    const float c2 = T[8] * r.X0 + T[9] * r.X1 + T[10] * r.X2 + T[11];
+    r.p0 = Kr[0] * c0 + Kr[1] * c1 + Kr[2] * c2;
+    r.p1 = Kr[3] * c0 + Kr[4] * c1 + Kr[5] * c2;
+    r.p2 = Kr[6] * c0 + Kr[7] * c1 + Kr[8] * c2;
+    r.z = fmaxf(r.p2, 1e-5f);
+    r.iz = rcp_nr(r.z);
+    r.ix = norm_roundtrip(div_nr(r.p0, r.z, r.iz), wm1, rwm1);
+    r.iy = norm_roundtrip(div_nr(r.p1, r.z, r.iz), hm1, rhm1);
+}
+
 __device__ __forceinline__ void project(const CamRec& c, float u, float v, float d, int H, int W,
                                         Proj& r) {
-    r.xn0 = c.Ki[0] * u + c.Ki[1] * v + c.Ki[2];
-    r.xn1 = c.Ki[3] * u + c.Ki[4] * v + c.Ki[5];
-    r.xn2 = c.Ki[6] * u + c.Ki[7] * v + c.Ki[8];
-    r.X0 = r.xn0 * d;
-    r.X1 = r.xn1 * d;
-    r.X2 = r.xn2 * d;
-    const float c0 = c.T[0] * r.X0 + c.T[1] * r.X1 + c.T[2] * r.X2 + c.T[3];
-    const float c1 = c.T[4] * r.X0 + c.T[5] * r.X1 + c.T[6] * r.X2 + c.T[7];
-    const float c2 = c.T[8] * r.X0 + c.T[9] * r.X1 + c.T[10] * r.X2 + c.T[11];
-    r.p0 = c.Kr[0] * c0 + c.Kr[1] * c1 + c.Kr[2] * c2;
-    r.p1 = c.Kr[3] * c0 + c.Kr[4] * c1 + c.Kr[5] * c2;
-    r.p2 = c.Kr[6] * c0 + c.Kr[7] * c1 + c.Kr[8] * c2;
-    r.z = fmaxf(r.p2, 1e-5f);
     const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
-    const float xnorm = 2.0f * (r.p0 / r.z) / wm1 - 1.0f;
-    const float ynorm = 2.0f * (r.p1 / r.z) / hm1 - 1.0f;
-    r.ix = ((xnorm + 1.0f) / 2.0f) * wm1;
-    r.iy = ((ynorm + 1.0f) / 2.0f) * hm1;
+    project_lifted(c.T, c.Kr, lift(c.Ki, u, v, d), wm1, rcp_nr(wm1), hm1, rcp_nr(hm1), r);
 }
 
 // Bilinear taps of grid_sample(padding_mode='zeros'): per-tap zero when out of bounds.
@@ -128,11 +164,18 @@ __device__ __forceinline__ Taps make_taps(float ix, float iy, int H, int W) {
     return t;
 }
 
-// Branch-free tap setup: out-of-bounds taps read a clamped (valid) address and are zeroed by a
-// select, so all 12 loads of a bilinear sample issue back to back (no exec-masked branches,
-// one wait) — the per-tap zero padding of grid_sample(padding_mode='zeros') is unchanged.
+// Load at a 32-bit BYTE offset from a wave-uniform base: lets the compiler use the
+// global_load saddr form (SGPR base + VGPR offset), no per-load 64-bit address arithmetic.
+__device__ __forceinline__ float ldg(const float* __restrict__ base, uint32_t byte_off) {
+    return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+// Branch-free tap setup: out-of-bounds taps read a clamped (valid) address and get weight 0,
+// so all 12 loads of a bilinear sample issue back to back (no exec-masked branches, one wait) —
+// the per-tap zero padding of grid_sample(padding_mode='zeros') is unchanged: tap*0 == 0 for
+// the finite images of this path, and the weighted sum starts from 0 as ATen's does.
 struct TapAddr {
-    size_t nw, ne, sw, se;
+    uint32_t nw, ne, sw, se;  // BYTE offsets within one channel plane
     bool vnw, vne, vsw, vse;
     float ax, bx, ay, by;  // (x0+1-ix), (ix-x0), (y0+1-iy), (iy-y0)
 };
@@ -141,14 +184,14 @@ __device__ __forceinline__ TapAddr tap_addr(float ix, float iy, int H, int W) {
     const Taps t = make_taps(ix, iy, H, W);
     TapAddr a;
     const int x0 = t.x0, y0 = t.y0;
-    const bool xw = t.ok && x0 >= 0 && x0 < W, xe = t.ok && x0 + 1 >= 0 && x0 + 1 < W;
-    const bool yn = t.ok && y0 >= 0 && y0 < H, ys = t.ok && y0 + 1 >= 0 && y0 + 1 < H;
+    const bool xw = t.ok && (unsigned)x0 < (unsigned)W, xe = t.ok && (unsigned)(x0 + 1) < (unsigned)W;
+    const bool yn = t.ok && (unsigned)y0 < (unsigned)H, ys = t.ok && (unsigned)(y0 + 1) < (unsigned)H;
     const int cx0 = min(max(x0, 0), W - 1), cx1 = min(max(x0 + 1, 0), W - 1);
     const int cy0 = min(max(y0, 0), H - 1), cy1 = min(max(y0 + 1, 0), H - 1);
-    a.nw = (size_t)cy0 * W + cx0;
-    a.ne = (size_t)cy0 * W + cx1;
-    a.sw = (size_t)cy1 * W + cx0;
-    a.se = (size_t)cy1 * W + cx1;
+    a.nw = (uint32_t)(cy0 * W + cx0) * 4u;
+    a.ne = a.nw + (uint32_t)(cx1 - cx0) * 4u;
+    a.sw = (uint32_t)(cy1 * W + cx0) * 4u;
+    a.se = a.sw + (uint32_t)(cx1 - cx0) * 4u;
     a.vnw = yn && xw;
     a.vne = yn && xe;
     a.vsw = ys && xw;
@@ -164,24 +207,23 @@ __device__ __forceinline__ TapAddr tap_addr(float ix, float iy, int H, int W) {
 __device__ __forceinline__ void bilinear3(const float* __restrict__ img, int H, int W, float ix,
                                           float iy, float out[3]) {
     const TapAddr t = tap_addr(ix, iy, H, W);
-    const size_t plane = (size_t)H * W;
+    const uint32_t pb = (uint32_t)(H * W) * 4u;
     float v[3][4];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float* p = img + c * plane;
-        v[c][0] = p[t.nw];
-        v[c][1] = p[t.ne];
-        v[c][2] = p[t.sw];
-        v[c][3] = p[t.se];
+        v[c][0] = ldg(img, c * pb + t.nw);
+        v[c][1] = ldg(img, c * pb + t.ne);
+        v[c][2] = ldg(img, c * pb + t.sw);
+        v[c][3] = ldg(img, c * pb + t.se);
     }
-    const float wnw = t.ax * t.ay, wne = t.bx * t.ay, wsw = t.ax * t.by, wse = t.bx * t.by;
+    const float wnw = t.vnw ? t.ax * t.ay : 0.0f, wne = t.vne ? t.bx * t.ay : 0.0f;
+    const float wsw = t.vsw ? t.ax * t.by : 0.0f, wse = t.vse ? t.bx * t.by : 0.0f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        float acc = 0.0f;
-        acc += (t.vnw ? v[c][0] : 0.0f) * wnw;
-        acc += (t.vne ? v[c][1] : 0.0f) * wne;
-        acc += (t.vsw ? v[c][2] : 0.0f) * wsw;
-        acc += (t.vse ? v[c][3] : 0.0f) * wse;
+        float acc = v[c][0] * wnw;
+        acc += v[c][1] * wne;
+        acc += v[c][2] * wsw;
+        acc += v[c][3] * wse;
         out[c] = acc;
     }
 }
@@ -233,7 +275,7 @@ __device__ __forceinline__ float project_grad(const CamRec& c, const Proj& r, fl
     // ix = ((2u/(W-1) - 1 + 1)/2)(W-1) with u = p0/z  ->  d ix/du = 1 (and likewise for v)
     (void)H;
     (void)W;
-    const float iz = __builtin_amdgcn_rcpf(r.z);
+    const float iz = r.iz;
     const float gu = gix, gv = giy;
     const float gp0 = gu * iz;
     const float gp1 = gv * iz;

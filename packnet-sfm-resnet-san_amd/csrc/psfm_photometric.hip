@@ -854,7 +854,7 @@ sweep::SweepArgs sweep_args(const psfm_params* p, const psfm_inputs* in, const p
 }
 
 void launch_k0(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
-    const dim3 grid(sweep::k1_units(p->H, p->W), p->B);
+    const dim3 grid(sweep::k0_units(p->H, p->W), p->B);
     switch (p->N) {
         case 1: hipLaunchKernelGGL((sweep::k0_unwarped<1>), grid, dim3(64), 0, st, a); break;
         case 2: hipLaunchKernelGGL((sweep::k0_unwarped<2>), grid, dim3(64), 0, st, a); break;
@@ -863,15 +863,30 @@ void launch_k0(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) 
     }
 }
 
-template <bool STATS>
-void launch_k1(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
+// FAST: the reference default configuration (automask, 'min', smoothness, no clip, no mask)
+// with its flags as compile-time constants.
+bool fast_cfg(const psfm_params* p, const psfm_inputs* in) {
+    return p->automask && p->reduce_op == PSFM_REDUCE_MIN && p->smooth_w > 0.0f && !(p->clip_loss > 0.0f) &&
+           !in->mask;
+}
+
+template <bool STATS, bool FAST>
+void launch_k1_t(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
     const dim3 grid(sweep::k1_units(p->H, p->W), p->B, p->S);
     switch (p->N) {
-        case 1: hipLaunchKernelGGL((sweep::k1_forward<1, STATS>), grid, dim3(64), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((sweep::k1_forward<2, STATS>), grid, dim3(64), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((sweep::k1_forward<3, STATS>), grid, dim3(64), 0, st, a); break;
-        default: hipLaunchKernelGGL((sweep::k1_forward<4, STATS>), grid, dim3(64), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((sweep::k1_forward<1, STATS, FAST>), grid, dim3(64), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((sweep::k1_forward<2, STATS, FAST>), grid, dim3(64), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((sweep::k1_forward<3, STATS, FAST>), grid, dim3(64), 0, st, a); break;
+        default: hipLaunchKernelGGL((sweep::k1_forward<4, STATS, FAST>), grid, dim3(64), 0, st, a); break;
     }
+}
+
+template <bool STATS>
+void launch_k1(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
+    if (!STATS && fast_cfg(p, &a.in))
+        launch_k1_t<false, true>(p, a, st);
+    else
+        launch_k1_t<STATS, false>(p, a, st);
 }
 
 }  // namespace

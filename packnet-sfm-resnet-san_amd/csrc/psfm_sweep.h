@@ -27,7 +27,7 @@ namespace psfm {
 namespace sweep {
 
 #ifndef PSFM_K1_RB
-#define PSFM_K1_RB 12
+#define PSFM_K1_RB 13
 #endif
 #ifndef PSFM_K2_RB
 #define PSFM_K2_RB 24
@@ -96,15 +96,14 @@ __device__ __forceinline__ T pick4(const T (&a)[4], int i) {
 __device__ __forceinline__ void bilinear3_vd(const float* __restrict__ img, int H, int W, float ix, float iy,
                                              float v[3], float dix[3], float diy[3]) {
     const TapAddr t = tap_addr(ix, iy, H, W);
-    const size_t plane = (size_t)H * W;
+    const uint32_t pb = (uint32_t)(H * W) * 4u;
     float q[3][4];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float* im = img + c * plane;
-        q[c][0] = im[t.nw];
-        q[c][1] = im[t.ne];
-        q[c][2] = im[t.sw];
-        q[c][3] = im[t.se];
+        q[c][0] = ldg(img, c * pb + t.nw);
+        q[c][1] = ldg(img, c * pb + t.ne);
+        q[c][2] = ldg(img, c * pb + t.sw);
+        q[c][3] = ldg(img, c * pb + t.se);
     }
     const float wnw = t.ax * t.ay, wne = t.bx * t.ay, wsw = t.ax * t.by, wse = t.bx * t.by;
 #pragma unroll
@@ -178,66 +177,158 @@ __device__ __forceinline__ DepthChain depth_chain(const psfm_params& p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Packed candidate arithmetic (v3): the contexts of a target are evaluated in PAIRS, one
+// context per half of a 64-bit register pair, so every SSIM / L1 / blend operation is one
+// v_pk_{add,mul,fma}_f32 for two candidates.  Odd NC: the last pair's high half duplicates
+// the last context (computed, never read).
+// ---------------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// lane l: v[l-1] + v[l] + v[l+1] (lane 0/63 read 0 outside the wave) as two v_add_f32_dpp —
+// same association as from_prev(v) + v + from_next(v).  The s_nop covers the VALU-write ->
+// DPP-read hazard (the hazard recognizer does not look inside inline asm).  All lanes active.
+__device__ __forceinline__ float hsum3a(float v) {
+    float t, r;
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %2, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %2, %0 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(t), "=v"(r)
+        : "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 hsum3p(f2 v) { return f2{hsum3a(v.x), hsum3a(v.y)}; }
+
+// three packed pairs at once: one hazard s_nop for 12 DPP adds
+__device__ __forceinline__ void hsum3x3(f2& a, f2& b, f2& c) {
+    float t0, t1, t2, t3, t4, t5;
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %6, %6 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %7, %7 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %8, %8 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %9, %9 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %4, %10, %10 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %5, %11, %11 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %6, %0 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %7, %1 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %8, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %9, %3 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %4, %10, %4 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %5, %11, %5 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5)
+        : "v"(a.x), "v"(a.y), "v"(b.x), "v"(b.y), "v"(c.x), "v"(c.y));
+    a = f2{t0, t1};
+    b = f2{t2, t3};
+    c = f2{t4, t5};
+}
+
+// 3x3 statistics of the target (shared by every candidate): mean, mean^2, var part.
+struct TWin {
+    float my[3], my2[3], ty[3];  // ty = E[y^2] - my^2
+};
+__device__ __forceinline__ TWin target_win(const float (&ya)[3], const float (&yb)[3], const float (&yc)[3]) {
+    TWin t;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        t.my[c] = hsum3a(ya[c] + yb[c] + yc[c]) * (1.0f / 9.0f);
+        const float syy = hsum3a(ya[c] * ya[c] + yb[c] * yb[c] + yc[c] * yc[c]) * (1.0f / 9.0f);
+        t.my2[c] = t.my[c] * t.my[c];
+        t.ty[c] = syy - t.my2[c];
+    }
+    return t;
+}
+
+// Photometric candidate of a context pair at the middle row: ssim_w * mean_c clamp((1-SSIM)/2)
+// + (1-ssim_w) * mean_c |x-y| (calc_photometric_loss :218-247, SSIM :15-54).  Cross-lane.
+__device__ __forceinline__ f2 photo_pair(const f2 (&xa)[3], const f2 (&xb)[3], const f2 (&xc)[3],
+                                         const float (&ya)[3], const float (&yb)[3], const float (&yc)[3],
+                                         const TWin& tw, float C1, float C2, float ssim_w, float l1w) {
+    constexpr float k9 = 1.0f / 9.0f;
+    f2 ls = f2{0.0f, 0.0f}, l1 = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const f2 vx = xa[c] + xb[c] + xc[c];
+        const f2 vxx = xa[c] * xa[c] + xb[c] * xb[c] + xc[c] * xc[c];
+        const f2 vxy = xa[c] * ya[c] + xb[c] * yb[c] + xc[c] * yc[c];
+        f2 hx = vx, hxx = vxx, hxy = vxy;
+        hsum3x3(hx, hxx, hxy);
+        const f2 mx = hx * k9;
+        const f2 sxx = hxx * k9;
+        const f2 sxy = hxy * k9;
+        const f2 mxy = mx * tw.my[c], mx2 = mx * mx;
+        const f2 A1 = 2.0f * mxy + C1, A2 = 2.0f * (sxy - mxy) + C2;
+        const f2 B1 = mx2 + tw.my2[c] + C1, B2 = (sxx - mx2) + tw.ty[c] + C2;
+        const f2 Nn = A1 * A2, D = B1 * B2;
+        const f2 iD = f2{__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y)};
+        const f2 l = (1.0f - Nn * iD) * 0.5f;
+        ls += f2{__builtin_amdgcn_fmed3f(l.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(l.y, 0.0f, 1.0f)};
+        const f2 dd = xb[c] - yb[c];
+        l1 += f2{fabsf(dd.x), fabsf(dd.y)};
+    }
+    return ssim_w * (ls * (1.0f / 3.0f)) + l1w * (l1 * (1.0f / 3.0f));
+}
+
+// Loss configuration: FAST = the reference default (automask, 'min', smoothness on, no clip,
+// no mask) as compile-time constants; otherwise read from psfm_params.
+template <bool FAST>
+struct Cfg {
+    const psfm_params& p;
+    __device__ __forceinline__ bool automask() const { return FAST ? true : (bool)p.automask; }
+    __device__ __forceinline__ bool is_min() const { return FAST ? true : p.reduce_op == PSFM_REDUCE_MIN; }
+    __device__ __forceinline__ bool smooth() const { return FAST ? true : p.smooth_w > 0.0f; }
+    __device__ __forceinline__ bool clip() const { return FAST ? false : p.clip_loss > 0.0f; }
+};
+
+// ---------------------------------------------------------------------------------------------
 // K0: automask candidates — photometric loss of every UN-warped context against the target
 // (multiview_photometric_loss.py:394-399).  Scale independent at full resolution, so computed
-// once per call instead of once per scale; one wave per (stripe, band, batch), K1 geometry.
+// once per call instead of once per scale.  One wave per (62-col stripe, K0RB-row band,
+// batch): all K0RB+2 rows are loaded up front (independent loads, no sweep latency chain).
 // ---------------------------------------------------------------------------------------------
+constexpr int K0RB = 4;
+__host__ __device__ inline int k0_units(int H, int W) { return k1_stripes(W) * ((H + K0RB - 1) / K0RB); }
+
 template <int NC>
 __global__ __launch_bounds__(64) void k0_unwarped(SweepArgs a) {
+    constexpr int NP = (NC + 1) / 2;
     const psfm_params& p = a.p;
     const int H = p.H, W = p.W, B = p.B;
-    const size_t plane = (size_t)H * W;
+    const uint32_t plane = (uint32_t)(H * W);
     const WorkItem wi = work_item();
     const int nst = k1_stripes(W), b = wi.b;
-    const int y0 = (wi.unit / nst) * K1RB;
+    const int y0 = (wi.unit / nst) * K0RB;
     const int col = (wi.unit % nst) * K1W - 1 + (int)threadIdx.x;
     const int colr = reflect1(col, W);
     const bool pcol = threadIdx.x >= 1 && threadIdx.x <= K1W && col < W;
     const float l1w = 1.0f - p.ssim_w;
     const float* tgt = a.in.tgt + (size_t)b * 3 * plane;
-    float Y[3][3], X[3][NC][3];
-    auto load = [&](int v, float (&y)[3], float (&x)[NC][3]) {
-        const size_t pix = (size_t)reflect1(v, H) * W + colr;
+    float Y[K0RB + 2][3];
+    f2 X[K0RB + 2][NP][3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) y[c] = tgt[c * plane + pix];
+    for (int k = 0; k < K0RB + 2; ++k) {
+        const uint32_t pix = (uint32_t)(reflect1(y0 - 1 + k, H) * W + colr);
 #pragma unroll
-        for (int j = 0; j < NC; ++j)
+        for (int c = 0; c < 3; ++c) Y[k][c] = tgt[c * plane + pix];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) x[j][c] = pick4(a.in.ctx, j)[((size_t)b * 3 + c) * plane + pix];
-    };
-    auto emit = [&](int k, float (&ya)[3], float (&yb)[3], float (&yc)[3], float (&xa)[NC][3],
-                    float (&xb)[NC][3], float (&xc)[NC][3]) {
-        const int pv = y0 - 2 + k;
-        if (k < 2 || pv >= H || pv >= y0 + K1RB) return;  // wave-uniform
-        float my[3], syy[3];
-        target_window(ya, yb, yc, my, syy);
+        for (int j = 0; j < 2 * NP; ++j) {
+            const int jj = j < NC ? j : NC - 1;
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            float vx[3], vxx[3], vxy[3], l1 = 0.0f;
+            for (int c = 0; c < 3; ++c) X[k][j >> 1][c][j & 1] = pick4(a.in.ctx, jj)[(size_t)b * 3 * plane + c * plane + pix];
+        }
+    }
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                vx[c] = xa[j][c] + xb[j][c] + xc[j][c];
-                vxx[c] = xa[j][c] * xa[j][c] + xb[j][c] * xb[j][c] + xc[j][c] * xc[j][c];
-                vxy[c] = xa[j][c] * ya[c] + xb[j][c] * yb[c] + xc[j][c] * yc[c];
-                l1 += fabsf(xb[j][c] - yb[c]);
+    for (int k = 1; k <= K0RB; ++k) {
+        const int pv = y0 - 1 + k;
+        if (pv >= H) break;  // wave-uniform
+        const TWin tw = target_win(Y[k - 1], Y[k], Y[k + 1]);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const f2 v = photo_pair(X[k - 1][q], X[k][q], X[k + 1][q], Y[k - 1], Y[k], Y[k + 1], tw, p.C1, p.C2,
+                                    p.ssim_w, l1w);
+            if (pcol) {
+                float* o = a.ws.unwarp + ((size_t)(2 * q) * B + b) * plane + (uint32_t)(pv * W + col);
+                o[0] = v.x;
+                if (2 * q + 1 < NC) o[(size_t)B * plane] = v.y;
             }
-            float d0[3], d1[3], d2[3];
-            const float sm = ssim_terms<false>(vx, vxx, vxy, my, syy, p.C1, p.C2, d0, d1, d2);
-            const float val = p.ssim_w * sm + l1w * (l1 * (1.0f / 3.0f));
-            if (pcol) a.ws.unwarp[((size_t)j * B + b) * plane + (size_t)pv * W + col] = val;
-        }
-    };
-    const int nk = K1RB + 2;
-    for (int k = 0; k < nk; k += 3) {
-        load(y0 - 1 + k, Y[0], X[0]);
-        emit(k, Y[1], Y[2], Y[0], X[1], X[2], X[0]);
-        if (k + 1 < nk) {
-            load(y0 + k, Y[1], X[1]);
-            emit(k + 1, Y[2], Y[0], Y[1], X[2], X[0], X[1]);
-        }
-        if (k + 2 < nk) {
-            load(y0 + 1 + k, Y[2], X[2]);
-            emit(k + 2, Y[0], Y[1], Y[2], X[0], X[1], X[2]);
         }
     }
 }
@@ -245,20 +336,57 @@ __global__ __launch_bounds__(64) void k0_unwarped(SweepArgs a) {
 // ---------------------------------------------------------------------------------------------
 // K1: forward (+ fused smoothness forward).  NC = number of contexts (exact register arrays).
 // STATS: clip-statistics pass (sum / sumsq of every raw candidate map, :249-253).
+//
+// Software pipeline over four row slots: step k issues row v = y0-1+k (target loads, the
+// bilinear gathers of every context — using the sigmoid prefetched one step earlier — and the
+// sigmoid of row v+1), then evaluates output row v-2 from rows v-3..v-1 that landed during the
+// previous step.  The gathers of row v stay in flight under a full row of SSIM arithmetic.
 // ---------------------------------------------------------------------------------------------
-template <int NC, bool STATS>
+template <int NC>
 struct K1State {
-    float Y[3][3], XW[3][NC][3], SG[3];
+    static constexpr int NP = (NC + 1) / 2;
+    float Y[4][3], SG[4];
+    f2 X[4][NP][3];
+    float sg_next;
     float acc_photo, acc_ax, acc_ay, acc_m;
     float st[2 * NC][2];
 };
 
-template <int NC, bool STATS>
+// Wave-uniform geometry of one (scale, batch): K^-1 of the target (shared by all contexts),
+// [R|t] and K_ref per context, and the normalisation constants.
+template <int NC>
+struct SweepCams {
+    float Ki[9];
+    float T[NC][12];
+    float Kr[NC][9];
+    float wm1, rwm1, hm1, rhm1;
+    __device__ __forceinline__ void load(const float* __restrict__ rec0, int B, int H, int W) {
+        // rec0 = record of (s, context 0, b); context j is j*B records further
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Ki[i] = sgpr(rec0[i]);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const float* r = rec0 + (size_t)j * B * PSFM_CAMREC;
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Kr[j][i] = sgpr(r[9 + i]);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) T[j][i] = sgpr(r[18 + i]);
+        }
+        wm1 = (float)(W - 1);
+        hm1 = (float)(H - 1);
+        rwm1 = rcp_nr(wm1);
+        rhm1 = rcp_nr(hm1);
+    }
+};
+
+template <int NC, bool STATS, bool FAST>
 struct K1 {
+    static constexpr int NP = (NC + 1) / 2;
     const SweepArgs& a;
     const psfm_params& p;
+    Cfg<FAST> cfg;
     int H, W, b, s, unit, y0, col, colr, B;
-    size_t plane;
+    uint32_t plane;
     bool pcol;
     DepthChain dc;
     float l1w;
@@ -266,13 +394,13 @@ struct K1 {
     const float* sig;
     const float* ctx[NC];
     const float* thr;
-    CamRec cam[NC];
+    SweepCams<NC> cams;
 
-    __device__ __forceinline__ K1(const SweepArgs& a_) : a(a_), p(a_.p) {
+    __device__ __forceinline__ K1(const SweepArgs& a_) : a(a_), p(a_.p), cfg{a_.p} {
         H = p.H;
         W = p.W;
         B = p.B;
-        plane = (size_t)H * W;
+        plane = (uint32_t)(H * W);
         const int nst = k1_stripes(W);
         const WorkItem wi = work_item();
         b = wi.b;
@@ -288,92 +416,106 @@ struct K1 {
         sig = pick4(a.in.sig, s) + (size_t)b * plane;
 #pragma unroll
         for (int j = 0; j < NC; ++j) ctx[j] = pick4(a.in.ctx, j) + (size_t)b * 3 * plane;
-#pragma unroll
-        for (int j = 0; j < NC; ++j)
-            load_cam_uniform(a.in.cam + ((size_t)(s * NC + j) * B + b) * PSFM_CAMREC, cam[j]);
-        thr = (p.clip_loss > 0.0f && !STATS) ? a.ws.clip_thr + (size_t)s * (p.automask ? 2 * NC : NC) : nullptr;
+        cams.load(a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC, B, H, W);
+        thr = (cfg.clip() && !STATS) ? a.ws.clip_thr + (size_t)s * (cfg.automask() ? 2 * NC : NC) : nullptr;
     }
 
-    __device__ __forceinline__ void load_row(int v, float (&y)[3], float (&xw)[NC][3], float& sg) const {
+    __device__ __forceinline__ float load_sig(int v) const {
+        return sig[(uint32_t)(reflect1(v, H) * W + colr)];
+    }
+
+    // issue row v: target, warped contexts (from the prefetched sigmoid sg)
+    __device__ __forceinline__ void issue_row(int v, float sg, float (&y)[3], f2 (&x)[NP][3]) const {
         const int r = reflect1(v, H);
-        const size_t pix = (size_t)r * W + colr;
+        const uint32_t pix = (uint32_t)(r * W + colr);
 #pragma unroll
         for (int c = 0; c < 3; ++c) y[c] = tgt[c * plane + pix];
-        sg = sig[pix];
         float d1, inv;
         const float d = dc.warp_depth(sg, d1, inv);
+        const Lift l = lift(cams.Ki, (float)colr, (float)r, d);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             Proj pr;
-            project(cam[j], (float)colr, (float)r, d, H, W, pr);
-            bilinear3(ctx[j], H, W, pr.ix, pr.iy, xw[j]);
+            project_lifted(cams.T[j], cams.Kr[j], l, cams.wm1, cams.rwm1, cams.hm1, cams.rhm1, pr);
+            float w[3];
+            bilinear3(ctx[j], H, W, pr.ix, pr.iy, w);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[j >> 1][c][j & 1] = w[c];
+        }
+        if (NC & 1) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[NP - 1][c].y = x[NP - 1][c].x;
         }
     }
 
-    // slots: IA = row v-2, IB = row v-1 (output), IC = row v (newest)
-    template <int IA, int IB, int IC>
-    __device__ __forceinline__ void step(K1State<NC, STATS>& S, int k) const {
+    // step k with slot I: issue row v = y0-1+k into slot I (LOAD), evaluate output row v-2
+    // from slots I+1 (row v-3), I+2 (v-2), I+3 (v-1) mod 4 (EVAL)
+    template <int I, bool LOAD, bool EVAL>
+    __device__ __forceinline__ void step(K1State<NC>& S, int k) const {
+        constexpr int IA = (I + 1) & 3, IB = (I + 2) & 3, IC = (I + 3) & 3;
         const int v = y0 - 1 + k;
-        load_row(v, S.Y[IC], S.XW[IC], S.SG[IC]);
-        if (k < 2) return;
-        const int pv = v - 1;
-        if (pv >= H || pv >= y0 + K1RB) return;  // wave-uniform
+        if (LOAD) {
+            const float sg = S.sg_next;
+            S.sg_next = load_sig(v + 1);
+            S.SG[I] = sg;
+            issue_row(v, sg, S.Y[I], S.X[I]);
+        }
+        if (EVAL) eval<IA, IB, IC>(S, v - 2);
+    }
+
+    // output row pv from slots IA (pv-1), IB (pv), IC (pv+1)
+    template <int IA, int IB, int IC>
+    __device__ __forceinline__ void eval(K1State<NC>& S, int pv) const {
+        if (pv >= H) return;  // wave-uniform (partial last band)
         // ---- cross-lane phase (every lane active) ----
-        float my[3], syy[3];
-        target_window(S.Y[IA], S.Y[IB], S.Y[IC], my, syy);
+        const TWin tw = target_win(S.Y[IA], S.Y[IB], S.Y[IC]);
         float cand[2 * NC];
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            float vx[3], vxx[3], vxy[3], l1 = 0.0f;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float xa = S.XW[IA][j][c], xb = S.XW[IB][j][c], xc = S.XW[IC][j][c];
-                vx[c] = xa + xb + xc;
-                vxx[c] = xa * xa + xb * xb + xc * xc;
-                vxy[c] = xa * S.Y[IA][c] + xb * S.Y[IB][c] + xc * S.Y[IC][c];
-                l1 += fabsf(xb - S.Y[IB][c]);
-            }
-            float d0[3], d1[3], d2[3];
-            const float sm = ssim_terms<false>(vx, vxx, vxy, my, syy, p.C1, p.C2, d0, d1, d2);
-            cand[2 * j] = p.ssim_w * sm + l1w * (l1 * (1.0f / 3.0f));
+        for (int q = 0; q < NP; ++q) {
+            const f2 v = photo_pair(S.X[IA][q], S.X[IB][q], S.X[IC][q], S.Y[IA], S.Y[IB], S.Y[IC], tw, p.C1, p.C2,
+                                    p.ssim_w, l1w);
+            cand[4 * q] = v.x;
+            if (2 * q + 1 < NC) cand[4 * q + 2] = v.y;
         }
         float sgn_next = 0.0f, ynext[3] = {0.0f, 0.0f, 0.0f};
-        if (!STATS && p.smooth_w > 0.0f) {
+        if (!STATS && cfg.smooth()) {
             sgn_next = from_next(S.SG[IB]);
 #pragma unroll
             for (int c = 0; c < 3; ++c) ynext[c] = from_next(S.Y[IB][c]);
         }
         // ---- lane-local phase ----
         if (!pcol) return;
-        const size_t ppix = (size_t)pv * W + col;
-        if (p.automask) {  // un-warped candidates (K0, scale independent)
+        const uint32_t ppix = (uint32_t)(pv * W + col);
+        if (cfg.automask()) {  // un-warped candidates (K0, scale independent)
 #pragma unroll
             for (int j = 0; j < NC; ++j) cand[2 * j + 1] = a.ws.unwarp[((size_t)j * B + b) * plane + ppix];
         }
         if (STATS) {
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
-                const int sw = p.automask ? 2 * j : j;
+                const int sw = cfg.automask() ? 2 * j : j;
                 S.st[sw][0] += cand[2 * j];
                 S.st[sw][1] += cand[2 * j] * cand[2 * j];
-                if (p.automask) {
+                if (cfg.automask()) {
                     S.st[sw + 1][0] += cand[2 * j + 1];
                     S.st[sw + 1][1] += cand[2 * j + 1] * cand[2 * j + 1];
                 }
             }
             return;
         }
-        const float mval = a.in.mask ? a.in.mask[(size_t)b * plane + ppix] : 1.0f;
+        const float mval = (!FAST && a.in.mask) ? a.in.mask[(size_t)b * plane + ppix] : 1.0f;
         float best = INFINITY, sum = 0.0f;
         int arg = 0, kk = 0;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                if (u == 1 && !p.automask) break;
+                if (u == 1 && !cfg.automask()) break;
                 float val = cand[2 * j + u];
-                if (thr) val = fminf(val, thr[u ? 2 * j + 1 : (p.automask ? 2 * j : j)]);
-                val *= mval;
+                if (!FAST) {
+                    if (thr) val = fminf(val, thr[u ? 2 * j + 1 : (cfg.automask() ? 2 * j : j)]);
+                    val *= mval;
+                }
                 sum += val;
                 if (val < best) {
                     best = val;
@@ -382,13 +524,13 @@ struct K1 {
                 ++kk;
             }
         }
-        if (p.reduce_op == PSFM_REDUCE_MIN) {
+        if (cfg.is_min()) {
             S.acc_photo += best;
             a.ws.argmin[((size_t)s * B + b) * plane + ppix] = (uint8_t)arg;
         } else {
             S.acc_photo += sum;
         }
-        if (p.smooth_w > 0.0f) {  // edge-aware smoothness of the sigmoid map (utils/depth.py:165-198)
+        if (cfg.smooth()) {  // edge-aware smoothness of the sigmoid map (utils/depth.py:165-198)
             const float sc = S.SG[IB];
             S.acc_m += sc;
             if (col < W - 1) {
@@ -405,24 +547,31 @@ struct K1 {
     }
 };
 
-template <int NC, bool STATS>
-__global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
-    K1<NC, STATS> K(a);
-    K1State<NC, STATS> S;
+template <int NC, bool STATS, bool FAST>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k1_forward(SweepArgs a) {
+    static_assert((K1RB - 1) % 4 == 0, "K1 band height must be 4m+1 (4-slot pipeline)");
+    K1<NC, STATS, FAST> K(a);
+    K1State<NC> S;
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;
 #pragma unroll
     for (int k = 0; k < 2 * NC; ++k) S.st[k][0] = S.st[k][1] = 0.0f;
-    const int nk = K1RB + 2;  // rows y0-1 .. y0+K1RB
-    for (int k = 0; k < nk; k += 3) {
-        K.template step<1, 2, 0>(S, k);
-        if (k + 1 < nk) K.template step<2, 0, 1>(S, k + 1);
-        if (k + 2 < nk) K.template step<0, 1, 2>(S, k + 2);
+    // rows y0-1 .. y0+K1RB are issued at steps k = 0 .. K1RB+1; output rows at k = 3 .. K1RB+2
+    S.sg_next = K.load_sig(K.y0 - 1);
+    K.template step<0, true, false>(S, 0);
+    K.template step<1, true, false>(S, 1);
+    K.template step<2, true, false>(S, 2);
+    for (int k = 3; k < K1RB + 2; k += 4) {
+        K.template step<3, true, true>(S, k);
+        K.template step<0, true, true>(S, k + 1);
+        K.template step<1, true, true>(S, k + 2);
+        K.template step<2, true, true>(S, k + 3);
     }
+    K.template step<3, false, true>(S, K1RB + 2);
     const psfm_params& p = a.p;
     const int units = k1_units(p.H, p.W);
     const int blk = K.b * units + K.unit;
     if (STATS) {
-        const int nsrc = p.automask ? 2 * NC : NC;
+        const int nsrc = K.cfg.automask() ? 2 * NC : NC;
         for (int k = 0; k < nsrc; ++k) {
             const float s1 = wave_sum64(S.st[k][0]), s2 = wave_sum64(S.st[k][1]);
             if (threadIdx.x == 0) {
@@ -437,7 +586,7 @@ __global__ __launch_bounds__(64) void k1_forward(SweepArgs a) {
     const float ax = wave_sum64(S.acc_ax), ay = wave_sum64(S.acc_ay), m = wave_sum64(S.acc_m);
     if (threadIdx.x == 0) {
         a.ws.photo_part[(size_t)K.s * (p.B * units) + blk] = ph;
-        if (p.smooth_w > 0.0f) {
+        if (K.cfg.smooth()) {
             float* o = a.ws.smooth_part + (((size_t)K.s * p.B + K.b) * units + K.unit) * 4;
             o[0] = ax;
             o[1] = ay;

@@ -7,7 +7,7 @@ mkdir -p "$ROOT/build/variants"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -I "$ROOT/include" $flags \
-    "$ROOT/packnet-sfm-resnet-san_amd/csrc/psfm_photometric.hip" -o "$ROOT/build/variants/$name.so" &
+    "$ROOT"/packnet-sfm-resnet-san_amd/csrc/*.hip -o "$ROOT/build/variants/$name.so" &
 done
 wait
 ls "$ROOT/build/variants"

@@ -1,0 +1,63 @@
+"""Attribute the eager training step's GPU kernels to PyTorch ops (torch.profiler): which ops
+launch the casts / copies / reductions around the MIOpen convolutions.
+
+  python tools/op_profile.py [--depth-net ResNetSAN01] [--steps 3]
+Writes gpurun_out/op_profile.txt (top ops by device time, self and total, with call counts).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--depth-net", default="ResNetSAN01")
+    ap.add_argument("--pose-net", default="PoseNet")
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "op_profile.txt"))
+    a = ap.parse_args()
+    ns = argparse.Namespace(depth_net=a.depth_net, pose_net=a.pose_net, batch=a.batch, height=192, width=640,
+                            amp="bf16", nchw=False, eager=True)
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    torch.backends.cudnn.benchmark = True
+    model = bench.build_model(ns, dev).to(memory_format=torch.channels_last)
+    opt = make_optimizer(model, 1e-4, 1e-4, fused=True)
+    opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=True)
+    tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16, graph=False, flat=True, bf16_weights=True)
+    batch = bench.synthetic_batch(a.batch, 192, 640, dev, seed=0, channels_last=True)
+    for _ in range(3):
+        tr.train_step(batch)
+    torch.cuda.synchronize()
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for _ in range(a.steps):
+            tr.train_step(batch)
+        torch.cuda.synchronize()
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    ka = prof.key_averages()
+    with open(a.out, "w") as f:
+        f.write(f"{a.steps} eager steps, {a.depth_net}+{a.pose_net}, B={a.batch}\n")
+        f.write("=== by self device time ===\n")
+        f.write(ka.table(sort_by="self_device_time_total", row_limit=70, max_name_column_width=70))
+        f.write("\n=== by total device time ===\n")
+        f.write(ka.table(sort_by="device_time_total", row_limit=70, max_name_column_width=70))
+        f.write("\n=== stacks of cast/copy ops ===\n")
+        kg = prof.key_averages(group_by_input_shape=True)
+        f.write(kg.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=60))
+    print("wrote", a.out)
+
+
+if __name__ == "__main__":
+    main()
