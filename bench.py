@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     ap.add_argument("--nchw", action="store_true", help="keep the nets in NCHW (default: channels_last)")
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
+    ap.add_argument("--fused-nets", action="store_true",
+                    help="run the nets' BN/GN/bias+activation epilogues as fused HIP kernels (psfm_netops)")
     return ap.parse_args()
 
 
@@ -185,6 +187,8 @@ def main():
     from packnet_sfm_amd.losses import _hip_photometric as HP
     from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
 
+    from packnet_sfm_amd.networks.layers import fused
+    fused.ENABLED = bool(args.fused_nets)
     torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
     torch.backends.cudnn.benchmark = True
     model = build_model(args, device)
@@ -234,6 +238,7 @@ def main():
                           "step": "eager" if args.eager else "hip_graph",
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
+                          "net_epilogues": "fused HIP (psfm_netops)" if args.fused_nets else "reference op chain",
                           "weights": "random init (no network / checkpoints)"}}
         if ktimes:
             group = ("K1_photometric_fwd", "K2_photometric_bwd", "K3_smoothness_fwd", "K3_smoothness_bwd")

@@ -1,0 +1,86 @@
+/*
+ * psfm_netops.h — C-ABI of the fused normalisation / activation kernels of the depth and pose
+ * networks (gfx950).
+ *
+ * The reference runs these layers as separate ATen/MIOpen ops under autocast:
+ *   - ResNet encoder  conv -> BatchNorm2d -> ReLU (-> + identity -> ReLU)
+ *       packnet_sfm/networks/layers/resnet/resnet_encoder.py:16-98 (torchvision BasicBlock)
+ *   - DepthDecoder    Conv3x3(bias) -> ReLU / Sigmoid
+ *       packnet_sfm/networks/layers/resnet/depth_decoder.py:16-64, layers.py:12-72
+ *   - PoseNet         Conv2d(bias) -> GroupNorm(16) -> ReLU
+ *       packnet_sfm/networks/pose/PoseNet.py:15-84
+ * i.e. 3 MIOpen BN kernels + ReLU + add forward and 3 + 2 backward per BN layer, bias add +
+ * ReLU + a bias-gradient reduction per decoder conv.  Each entry point below fuses one such
+ * chain into one or two passes over the activation.
+ *
+ * Layout: an activation is a bf16 matrix [M, C] row-major — the storage order of an NHWC
+ * (torch.channels_last) tensor with M = N*H*W (GroupNorm: [N, HW, C]).  Statistics and
+ * parameters are fp32.  Reductions are deterministic: per-workgroup partials in `ws`, summed
+ * in a fixed order by the LAST workgroup to finish (an int device counter, `counter`, zeroed
+ * once by the caller and re-armed by the kernel) — no float atomics.
+ *
+ * Conventions as include/psfm.h: device pointers, caller-owned buffers, stream-ordered,
+ * graph-capturable; return 0 / <0 bad argument / >0 hipError_t, message from
+ * psfm_netops_last_error().
+ */
+#ifndef PSFM_NETOPS_H
+#define PSFM_NETOPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSFM_ACT_NONE 0
+#define PSFM_ACT_RELU 1
+#define PSFM_ACT_SIGMOID 2
+
+/* fp32 workspace floats needed by a reduction over an [M, C] activation (bias_act_bwd,
+ * bn_act_fwd / bn_act_bwd), and for groupnorm over [N, HW, C] with G groups. */
+size_t psfm_netops_ws_floats(int M, int C);
+size_t psfm_gn_ws_floats(int N, int HW, int C, int G);
+
+/* y = act(x + bias)   (Conv2d bias add + ReLU / Sigmoid, layers.py:44-51, depth_decoder.py:60).
+ * x bf16 [M,C]; bias bf16 (bias_bf16=1) or fp32 [C]; y bf16 for NONE/RELU, fp32 for SIGMOID
+ * (the sigmoid maps feed the fp32 photometric loss). */
+int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y,
+                      void* stream);
+
+/* dx = dy * act'(y) (bf16), dbias = sum_rows dx (written in the bias dtype).  dy has y's dtype. */
+int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void* dx, void* dbias,
+                      int bias_bf16, float* ws, int* counter, void* stream);
+
+/* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
+ * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
+ * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
+int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
+                    float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
+                    float* save_invstd, float* ws, int* counter, void* stream);
+
+/* Backward of psfm_bn_act_fwd: dx (bf16), dres (bf16, = ReLU-masked dy; may be NULL),
+ * dgamma / dbeta (fp32 [C], written). */
+int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
+                    const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
+                    float* dbeta, float* ws, int* counter, void* stream);
+
+/* GroupNorm(G) over (x + bias) (+ ReLU) per sample: x bf16 [N, HW, C], conv bias bf16/fp32 [C],
+ * gamma/beta fp32 [C] (PoseNet.py:15-19 conv_gn).  save_mean / save_invstd [N*G]. */
+int psfm_gn_act_fwd(const void* x, const void* bias, int bias_bf16, const float* gamma, const float* beta,
+                    float eps, int N, int HW, int C, int G, int relu, void* y, float* save_mean,
+                    float* save_invstd, float* ws, int* counter, void* stream);
+
+/* Backward of psfm_gn_act_fwd: dx (bf16), dbias (bias dtype; the column sum of the stored dx, as
+ * autograd forms a conv bias gradient), dgamma / dbeta (fp32 [C]).  Uses counter[0] and counter[1]. */
+int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bias, int bias_bf16,
+                    const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C,
+                    int G, int relu, void* dx, void* dbias, float* dgamma, float* dbeta, float* ws, int* counter,
+                    void* stream);
+
+const char* psfm_netops_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSFM_NETOPS_H */

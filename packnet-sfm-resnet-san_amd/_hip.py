@@ -79,6 +79,18 @@ def lib():
         "psfm_grad_pack": ([V, V, c_int, V, V], c_int),
         "psfm_adam_step": ([V, V, c_int, V, V, V, c_float, V, V, V, V], c_int),
         "psfm_optim_last_error": ([], ctypes.c_char_p),
+        # include/psfm_netops.h
+        "psfm_netops_ws_floats": ([c_int, c_int], c_size_t),
+        "psfm_gn_ws_floats": ([c_int, c_int, c_int, c_int], c_size_t),
+        "psfm_bias_act_fwd": ([V, V, c_int, c_int, c_int, c_int, V, V], c_int),
+        "psfm_bias_act_bwd": ([V, V, c_int, c_int, c_int, V, V, c_int, V, V, V], c_int),
+        "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
+        "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V, V], c_int),
+        "psfm_gn_act_fwd": ([V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V],
+                            c_int),
+        "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V, V],
+                            c_int),
+        "psfm_netops_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -91,13 +103,19 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_smoothness_fwd", "psfm_finalize", "psfm_photometric_bwd", "psfm_smoothness_bwd",
             "psfm_pose_grad_reduce", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
             "psfm_tiles_per_image", "psfm_last_error", "psfm_version",
-            "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error")
+            "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
+            "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
+            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error")
 
 
 def check(rc, what):
     if rc != 0:
-        err = lib().psfm_optim_last_error if what.startswith(("psfm_optim", "psfm_grad", "psfm_adam")) \
-            else lib().psfm_last_error
+        if what.startswith(("psfm_optim", "psfm_grad", "psfm_adam")):
+            err = lib().psfm_optim_last_error
+        elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops")):
+            err = lib().psfm_netops_last_error
+        else:
+            err = lib().psfm_last_error
         raise RuntimeError(f"{what} failed ({rc}): {err().decode()}")
 
 

@@ -1,0 +1,207 @@
+"""Fused normalisation / activation layers of the depth and pose networks on HIP
+(include/psfm_netops.h, csrc/psfm_netops.hip).
+
+Each helper takes the modules the reference builds (nn.BatchNorm2d, nn.GroupNorm, nn.Conv2d
+bias) — parameters, buffers and state_dict layout are unchanged — and on a ROCm device with bf16
+NHWC (channels_last) activations runs one fused kernel pair instead of the reference's op chain:
+
+  bn_act(x, bn, relu, residual)   BatchNorm2d (train) [+ identity] [+ ReLU]
+                                  (resnet_encoder.py:16-98 BasicBlock / stem / downsample)
+  bias_act(x, bias, act)          Conv2d bias add + ReLU / Sigmoid (layers.py:44-51, depth_decoder.py:60)
+  gn_act(x, bias, gn, relu)       Conv2d bias + GroupNorm(16) + ReLU (PoseNet.py:15-19)
+
+Anything else (CPU tensors, fp32 activations, eval-mode BatchNorm, momentum=None) runs the same
+math as plain torch ops — that is the reference's own path, not a fallback of a HIP kernel:
+the photometric loss (losses/_hip_photometric.py) has no such path.
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from ... import _hip
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
+ENABLED = False  # opt-in until the fused reductions beat MIOpen (bench.py --fused-nets)
+
+
+def _fusable(x):
+    return ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+
+
+def _rows(t):
+    """NHWC storage as an [M, C] matrix (copy only if not already channels_last)."""
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+def _counter(module, device):
+    c = getattr(module, "_psfm_counter", None)
+    if c is None or c.device != device:
+        c = torch.zeros(4, dtype=torch.int32, device=device)  # [fwd, bwd, bwd2, bwd2'], re-armed by the kernels
+        module._psfm_counter = c
+    return c
+
+
+def _i32p(t, i):
+    return ctypes.c_void_p(t.data_ptr() + 4 * i)
+
+
+# ----------------------------------------------------------------------------------------------
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, act, counter):
+        x = _rows(x)
+        N, C, H, W = x.shape
+        M = N * H * W
+        y = torch.empty_like(x, dtype=torch.float32 if act == ACT_SIGMOID else x.dtype,
+                             memory_format=torch.channels_last)
+        L = _hip.lib()
+        _hip.check(L.psfm_bias_act_fwd(_hip.ptr(x), _hip.ptr(bias), int(bias.dtype == torch.bfloat16), M, C, act,
+                                       _hip.ptr(y), _hip.stream(x.device)), "psfm_bias_act_fwd")
+        ctx.save_for_backward(y)
+        ctx.act, ctx.counter, ctx.bias_dtype, ctx.x_dtype = act, counter, bias.dtype, x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = _rows(dy.to(y.dtype))
+        N, C, H, W = y.shape
+        M = N * H * W
+        L = _hip.lib()
+        dx = torch.empty_like(y, dtype=ctx.x_dtype, memory_format=torch.channels_last)
+        db = torch.empty(C, device=y.device, dtype=ctx.bias_dtype)
+        ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=y.device, dtype=torch.float32)
+        _hip.check(L.psfm_bias_act_bwd(_hip.ptr(dy), _hip.ptr(y), M, C, ctx.act, _hip.ptr(dx), _hip.ptr(db),
+                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _i32p(ctx.counter, 1),
+                                       _hip.stream(y.device)), "psfm_bias_act_bwd")
+        return dx, db, None, None
+
+
+def bias_act(x, bias, act, module):
+    """act(x + bias): x = conv output WITHOUT its bias (F.conv2d(..., None)); `module` owns the
+    reduction counter.  Sigmoid outputs are fp32 (they feed the fp32 photometric loss)."""
+    if _fusable(x) and bias is not None:
+        return _BiasAct.apply(x, bias, act, _counter(module, x.device))
+    y = x if bias is None else x + bias.to(x.dtype).view(1, -1, 1, 1)
+    if act == ACT_RELU:
+        return torch.relu(y)
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(y.float()) if x.is_cuda else torch.sigmoid(y)
+    return y
+
+
+def conv_nobias(conv, x):
+    """The reference Conv2d without its bias term (the bias goes into the fused epilogue)."""
+    return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+# ----------------------------------------------------------------------------------------------
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, counter):
+        x = _rows(x)
+        N, C, H, W = x.shape
+        M = N * H * W
+        dev = x.device
+        res = _rows(residual.to(x.dtype)) if residual is not None else None
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mean = torch.empty(C, device=dev, dtype=torch.float32)
+        invstd = torch.empty(C, device=dev, dtype=torch.float32)
+        L = _hip.lib()
+        ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
+        _hip.check(L.psfm_bn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(weight), _hip.ptr(bias),
+                                     _hip.ptr(running_mean), _hip.ptr(running_var), ctypes.c_float(momentum),
+                                     ctypes.c_float(eps), M, C, int(relu), _hip.ptr(y), _hip.ptr(mean),
+                                     _hip.ptr(invstd), _hip.ptr(ws), _i32p(counter, 0), _hip.stream(dev)),
+                   "psfm_bn_act_fwd")
+        ctx.save_for_backward(x, y, weight, mean, invstd)
+        ctx.relu, ctx.has_res, ctx.counter = relu, residual is not None, counter
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        dy = _rows(dy.to(x.dtype))
+        N, C, H, W = x.shape
+        M = N * H * W
+        dev = x.device
+        L = _hip.lib()
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dw = torch.empty(C, device=dev, dtype=torch.float32)
+        db = torch.empty(C, device=dev, dtype=torch.float32)
+        ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
+        _hip.check(L.psfm_bn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(mean),
+                                     _hip.ptr(invstd), M, C, int(ctx.relu), _hip.ptr(dx), _hip.ptr(dres),
+                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _i32p(ctx.counter, 1),
+                                     _hip.stream(dev)), "psfm_bn_act_bwd")
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None, None
+
+
+def bn_act(x, bn, relu=True, residual=None):
+    """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn`."""
+    if (_fusable(x) and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
+            and bn.running_mean is not None):
+        if bn.num_batches_tracked is not None:  # the graph trainer keeps these off the step
+            bn.num_batches_tracked.add_(1)
+        return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, float(bn.momentum),
+                            float(bn.eps), bool(relu), _counter(bn, x.device))
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
+# ----------------------------------------------------------------------------------------------
+class _GNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, weight, beta, G, eps, relu, counter):
+        x = _rows(x)
+        N, C, H, W = x.shape
+        HW = H * W
+        dev = x.device
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mean = torch.empty(N * G, device=dev, dtype=torch.float32)
+        invstd = torch.empty(N * G, device=dev, dtype=torch.float32)
+        L = _hip.lib()
+        ws = torch.empty(L.psfm_gn_ws_floats(N, HW, C, G), device=dev, dtype=torch.float32)
+        bf = int(bias.dtype == torch.bfloat16)
+        _hip.check(L.psfm_gn_act_fwd(_hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight), _hip.ptr(beta),
+                                     ctypes.c_float(eps), N, HW, C, G, int(relu), _hip.ptr(y), _hip.ptr(mean),
+                                     _hip.ptr(invstd), _hip.ptr(ws), _i32p(counter, 0), _hip.stream(dev)),
+                   "psfm_gn_act_fwd")
+        ctx.save_for_backward(x, y, bias, weight, mean, invstd)
+        ctx.G, ctx.relu, ctx.counter = G, relu, counter
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, bias, weight, mean, invstd = ctx.saved_tensors
+        dy = _rows(dy.to(x.dtype))
+        N, C, H, W = x.shape
+        HW, G = H * W, ctx.G
+        dev = x.device
+        L = _hip.lib()
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dbias = torch.empty(C, device=dev, dtype=bias.dtype)
+        dw = torch.empty(C, device=dev, dtype=torch.float32)
+        db = torch.empty(C, device=dev, dtype=torch.float32)
+        ws = torch.empty(L.psfm_gn_ws_floats(N, HW, C, G), device=dev, dtype=torch.float32)
+        bf = int(bias.dtype == torch.bfloat16)
+        _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight),
+                                     _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.relu), _hip.ptr(dx),
+                                     _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws),
+                                     _i32p(ctx.counter, 2), _hip.stream(dev)), "psfm_gn_act_bwd")
+        return dx, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None
+
+
+def gn_act(x, bias, gn, relu=True):
+    """act(groupnorm(x + bias)) with the reference's nn.GroupNorm module `gn`."""
+    if _fusable(x) and bias is not None and gn.affine and x.shape[1] % gn.num_groups == 0:
+        return _GNAct.apply(x, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), bool(relu),
+                            _counter(gn, x.device))
+    if bias is not None:
+        x = x + bias.to(x.dtype).view(1, -1, 1, 1)
+    y = gn(x)
+    return torch.relu(y) if relu else y

@@ -7,6 +7,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ..fused import ACT_SIGMOID, bias_act, conv_nobias
 from .layers import Conv3x3, ConvBlock, upsample
 
 
@@ -39,6 +40,8 @@ class DepthDecoder(nn.Module):
                 x.append(input_features[i - 1])
             x = self.convs[("upconv", i, 1)](torch.cat(x, 1))
             if i in self.scales:
-                out[("disp", i)] = self.sigmoid(self.convs[("dispconv", i)](x))
+                head = self.convs[("dispconv", i)]  # Conv3x3 + sigmoid, fused epilogue (fp32 maps)
+                xin = head.pad(x) if head.pad is not None else x
+                out[("disp", i)] = bias_act(conv_nobias(head.conv, xin), head.conv.bias, ACT_SIGMOID, head)
         self.outputs = out
         return out

@@ -3,6 +3,8 @@ layers.py:12-72): Conv3x3 with zero padding inside the conv, ConvBlock = Conv3x3
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..fused import ACT_RELU, bias_act, conv_nobias
+
 
 def disp_to_depth(disp, min_depth, max_depth):
     lo, hi = 1 / max_depth, 1 / min_depth
@@ -27,7 +29,10 @@ class ConvBlock(nn.Module):
         self.nonlin = nn.ReLU(inplace=True)
 
     def forward(self, x):
-        return self.nonlin(self.conv(x))
+        # Conv3x3 without its bias + fused (bias + ReLU) epilogue with the bias-gradient reduction
+        c = self.conv
+        x = c.pad(x) if c.pad is not None else x
+        return bias_act(conv_nobias(c.conv, x), c.conv.bias, ACT_RELU, self)
 
 
 def upsample(x):

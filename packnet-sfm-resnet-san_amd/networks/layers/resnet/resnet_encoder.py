@@ -10,6 +10,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ..fused import bn_act
+
 
 def conv3x3(i, o, stride=1):
     return nn.Conv2d(i, o, kernel_size=3, stride=stride, padding=1, bias=False)
@@ -32,9 +34,10 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        return self.relu(self.bn2(self.conv2(out)) + idt)
+        # conv -> BN -> ReLU, conv -> BN -> +identity -> ReLU as fused BN epilogues (fused.py)
+        idt = x if self.downsample is None else bn_act(self.downsample[0](x), self.downsample[1], relu=False)
+        out = bn_act(self.conv1(x), self.bn1, relu=True)
+        return bn_act(self.conv2(out), self.bn2, relu=True, residual=idt)
 
 
 class Bottleneck(nn.Module):
@@ -52,10 +55,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        return self.relu(self.bn3(self.conv3(out)) + idt)
+        idt = x if self.downsample is None else bn_act(self.downsample[0](x), self.downsample[1], relu=False)
+        out = bn_act(self.conv1(x), self.bn1, relu=True)
+        out = bn_act(self.conv2(out), self.bn2, relu=True)
+        return bn_act(self.conv3(out), self.bn3, relu=True, residual=idt)
 
 
 RESNET_SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),
@@ -114,7 +117,7 @@ class ResnetEncoder(nn.Module):
 
     def forward(self, input_image):
         e = self.encoder
-        x = e.relu(e.bn1(e.conv1((input_image - 0.45) / 0.225)))
+        x = bn_act(e.conv1((input_image - 0.45) / 0.225), e.bn1, relu=True)
         feats = [x]
         feats.append(e.layer1(e.maxpool(x)))
         for layer in (e.layer2, e.layer3, e.layer4):

@@ -3,6 +3,8 @@ blocks over [target, contexts] stacked on channels, 1x1 head, spatial mean, x0.0
 import torch
 import torch.nn as nn
 
+from ..layers.fused import conv_nobias, gn_act
+
 
 def conv_gn(in_planes, out_planes, kernel_size=3):
     return nn.Sequential(
@@ -34,7 +36,8 @@ class PoseNet(nn.Module):
     def forward(self, image, context):
         assert len(context) == self.nb_ref_imgs
         x = torch.cat([image, *context], 1)
-        for i in range(7):
-            x = getattr(self, f"conv{i + 1}")(x)
+        for i in range(7):  # conv -> (bias + GroupNorm + ReLU) fused epilogue (fused.py)
+            conv, gn, _ = getattr(self, f"conv{i + 1}")
+            x = gn_act(conv_nobias(conv, x), conv.bias, gn, relu=True)
         pose = self.pose_pred(x).mean(3).mean(2)
         return 0.01 * pose.view(pose.size(0), self.nb_ref_imgs, 6)

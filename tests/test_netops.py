@@ -1,0 +1,219 @@
+"""Fused network epilogues (include/psfm_netops.h) against plain PyTorch fp32 references of the
+same ops (BatchNorm2d / GroupNorm / bias + ReLU / Sigmoid, forward and backward), and the module
+wiring on CPU (the reference op chain).  Tolerances: outputs are bf16 (relative rounding 2^-8),
+so activations / input gradients are compared at 2e-2 of the tensor's max magnitude, the fp32
+parameter gradients and running statistics at 2e-3 relative."""
+import pytest
+import torch
+import torch.nn as nn
+
+import packnet_sfm_amd  # noqa: F401
+from packnet_sfm_amd.networks.layers import fused as FU
+
+gpu = pytest.mark.gpu
+
+
+def _close(a, b, tol, where=None):
+    a, b = a.float(), b.float()
+    scale = b.abs().max().clamp(min=1e-6)
+    d = (a - b).abs()
+    if where is not None:
+        d = d[where]
+    err = d.max() / scale
+    assert err < tol, f"max err {err:.3e} (scale {scale:.3e}) > {tol}"
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    import __graft_entry__
+    __graft_entry__.build()
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def fused_on():
+    """The fused path is opt-in in the product (fused.ENABLED); these tests exercise it."""
+    prev = FU.ENABLED
+    FU.ENABLED = True
+    yield
+    FU.ENABLED = prev
+
+
+@gpu
+@pytest.mark.parametrize("shape,act,bias_bf16", [((2, 16, 24, 80), FU.ACT_RELU, True),
+                                                   ((2, 64, 12, 40), FU.ACT_RELU, False),
+                                                   ((2, 256, 6, 20), FU.ACT_RELU, True),
+                                                   ((2, 1, 48, 160), FU.ACT_SIGMOID, True),
+                                                   ((2, 16, 48, 160), FU.ACT_SIGMOID, False)])
+def test_bias_act_matches_torch(dev, shape, act, bias_bf16):
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16).requires_grad_(True)
+    b = torch.randn(shape[1], generator=g).to(dev, torch.bfloat16 if bias_bf16 else torch.float32).requires_grad_(True)
+    owner = nn.Module()
+    y = FU.bias_act(x, b, act, owner)
+    # reference in fp32 on the same (bf16) values
+    xr = x.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    u = xr + br.view(1, -1, 1, 1)
+    yr = torch.relu(u) if act == FU.ACT_RELU else torch.sigmoid(u)
+    _close(y, yr, 1e-2)
+    assert y.dtype == (torch.float32 if act == FU.ACT_SIGMOID else torch.bfloat16)
+    dy = torch.randn(shape, generator=g).to(dev, y.dtype)
+    y.backward(_cl(dy))
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 2e-2)
+    _close(b.grad, br.grad, 2e-2 if bias_bf16 else 2e-3)
+    assert b.grad.dtype == b.dtype
+
+
+@gpu
+@pytest.mark.parametrize("shape,relu,residual", [((2, 64, 48, 160), True, False),
+                                                  ((2, 64, 24, 80), True, True),
+                                                  ((4, 512, 6, 20), True, True),
+                                                  ((2, 128, 12, 40), False, False),
+                                                  ((2, 12, 10, 30), True, True)])
+def test_bn_act_matches_torch(dev, shape, relu, residual):
+    g = torch.Generator(device="cpu").manual_seed(2)
+    C = shape[1]
+    bn = nn.BatchNorm2d(C).to(dev).train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    ref = nn.BatchNorm2d(C).to(dev).train()
+    ref.load_state_dict(bn.state_dict())
+    x = _cl(torch.randn(shape, generator=g) * 2 + 0.3).to(dev, torch.bfloat16).requires_grad_(True)
+    r = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16).requires_grad_(True) if residual else None
+    y = FU.bn_act(x, bn, relu=relu, residual=r)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    yr = ref(xr)
+    if residual:  # autocast semantics: bn(x) is a bf16 tensor before the add (identity gradient)
+        yr = yr + (yr.detach().bfloat16().float() - yr.detach()) + rr
+    # elements whose pre-activation sits within bf16 noise of the ReLU kink may take either
+    # side in two correct implementations: their input gradient is excluded below
+    far = (yr.detach().abs() > 2e-2) if relu else None
+    if relu:
+        yr = torch.relu(yr)
+    _close(y, yr, 2e-2)
+    _close(bn.running_mean, ref.running_mean, 2e-3)
+    _close(bn.running_var, ref.running_var, 2e-3)
+    dy = torch.randn(shape, generator=g).to(dev, torch.bfloat16)
+    y.backward(_cl(dy))
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 2e-2, far)
+    _close(bn.weight.grad, ref.weight.grad, 2e-2)
+    _close(bn.bias.grad, ref.bias.grad, 2e-2)
+    if residual:
+        _close(r.grad, rr.grad, 2e-2, far)
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(4, 16, 96, 320), (4, 64, 24, 80), (4, 256, 3, 10), (2, 32, 5, 7)])
+def test_gn_act_matches_torch(dev, shape):
+    g = torch.Generator(device="cpu").manual_seed(3)
+    C = shape[1]
+    conv_b = torch.randn(C, generator=g).to(dev, torch.bfloat16).requires_grad_(True)
+    gn = nn.GroupNorm(16, C).to(dev)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    x = _cl(torch.randn(shape, generator=g) + 0.5).to(dev, torch.bfloat16).requires_grad_(True)
+    y = FU.gn_act(x, conv_b, gn, relu=True)
+    xr = x.detach().float().requires_grad_(True)
+    br = conv_b.detach().float().requires_grad_(True)
+    wr = gn.weight.detach().clone().requires_grad_(True)
+    betar = gn.bias.detach().clone().requires_grad_(True)
+    yr = torch.relu(torch.nn.functional.group_norm(xr + br.view(1, -1, 1, 1), 16, wr, betar, gn.eps))
+    _close(y, yr, 2e-2)
+    dy = torch.randn(shape, generator=g).to(dev, torch.bfloat16)
+    y.backward(_cl(dy))
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 2e-2)
+    # conv-bias gradient = column sum of the stored bf16 dx (what autograd sums): exact w.r.t.
+    # our dx; against the fp32 reference it carries the bf16 rounding noise of M summands
+    own = x.grad.double().sum((0, 2, 3))
+    assert torch.allclose(conv_b.grad.double(), own, rtol=1e-2, atol=1e-3 * own.abs().max().item() + 1e-6)
+    M = shape[0] * shape[2] * shape[3]
+    noise = 4 * M ** 0.5 * 2 ** -8 * xr.grad.float().pow(2).mean().sqrt()
+    assert (conv_b.grad.float() - br.grad).abs().max() <= noise + 3e-2 * br.grad.abs().max()
+    _close(gn.weight.grad, wr.grad, 2e-2)
+    _close(gn.bias.grad, betar.grad, 2e-2)
+
+
+@gpu
+def test_fused_reductions_are_deterministic_and_rearm(dev):
+    """Repeated launches reuse the device counters (re-armed by the last workgroup): results
+    stay bit-identical run to run."""
+    g = torch.Generator(device="cpu").manual_seed(4)
+    bn = nn.BatchNorm2d(64).to(dev).train()
+    x = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
+    dy = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        xi = x.clone().requires_grad_(True)
+        bn.weight.grad = None
+        y = FU.bn_act(xi, bn, relu=True)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        outs.append((y.detach().clone(), xi.grad.clone(), bn.weight.grad.clone()))
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
+
+
+@gpu
+def test_resnet_encoder_fused_matches_unfused(dev):
+    """The whole ResNet18 encoder + decoder: fused bf16 epilogues are as close to an fp32 run of
+    the reference op chain as the reference's own bf16-autocast run is (same weights)."""
+    from packnet_sfm_amd.networks.depth.ResNetSAN01 import ResNetSAN01
+    torch.manual_seed(0)
+    net = ResNetSAN01(version="18A").to(dev).train().to(memory_format=torch.channels_last)
+    x = _cl(torch.rand(2, 3, 96, 320)).to(dev)
+
+    def run(enabled, amp):
+        FU.ENABLED = enabled
+        try:
+            net.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                sig = net(x)["inv_depths"]
+            loss = sum(s.float().mean() for s in sig)
+            loss.backward()
+            return ([s.detach().float() for s in sig],
+                    [net.decoder.convs[("dispconv", 0)].conv.bias.grad.detach().float().clone(),
+                     net.encoder.encoder.conv1.weight.grad.detach().float().clone(),
+                     net.encoder.encoder.layer4[1].bn2.weight.grad.detach().float().clone()])
+        finally:
+            FU.ENABLED = True
+
+    ref = run(False, False)
+    fused, plain = run(True, True), run(False, True)
+
+    def err(a, b):
+        return float((a - b).abs().max() / b.abs().max().clamp(min=1e-12))
+
+    for k in range(4):
+        ef, ep = err(fused[0][k], ref[0][k]), err(plain[0][k], ref[0][k])
+        assert ef <= 2.0 * ep + 1e-2, (k, ef, ep)
+    for k in range(3):
+        ef, ep = err(fused[1][k], ref[1][k]), err(plain[1][k], ref[1][k])
+        assert ef <= 2.0 * ep + 2e-2, (k, ef, ep)
+
+
+def test_cpu_path_is_the_reference_op_chain():
+    """On CPU the helpers are exactly the reference's modules (BN -> +res -> ReLU etc.)."""
+    torch.manual_seed(0)
+    bn = nn.BatchNorm2d(8).train()
+    x, r = torch.randn(2, 8, 5, 6), torch.randn(2, 8, 5, 6)
+    ref = nn.BatchNorm2d(8).train()
+    ref.load_state_dict(bn.state_dict())
+    assert torch.equal(FU.bn_act(x, bn, True, r), torch.relu(ref(x) + r))
+    gn = nn.GroupNorm(4, 8)
+    b = torch.randn(8)
+    assert torch.equal(FU.gn_act(x, b, gn, True), torch.relu(gn(x + b.view(1, -1, 1, 1))))
+    assert torch.equal(FU.bias_act(x, b, FU.ACT_SIGMOID, nn.Module()), torch.sigmoid(x + b.view(1, -1, 1, 1)))

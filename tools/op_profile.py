@@ -41,7 +41,7 @@ def main():
         tr.train_step(batch)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
         for _ in range(a.steps):
             tr.train_step(batch)
         torch.cuda.synchronize()
@@ -53,9 +53,13 @@ def main():
         f.write(ka.table(sort_by="self_device_time_total", row_limit=70, max_name_column_width=70))
         f.write("\n=== by total device time ===\n")
         f.write(ka.table(sort_by="device_time_total", row_limit=70, max_name_column_width=70))
-        f.write("\n=== stacks of cast/copy ops ===\n")
+        f.write("\n=== by input shape ===\n")
         kg = prof.key_averages(group_by_input_shape=True)
-        f.write(kg.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=60))
+        f.write(kg.table(sort_by="self_device_time_total", row_limit=80, max_name_column_width=40,
+                         max_shapes_column_width=90))
+        f.write("\n=== by stack (5 frames) ===\n")
+        ks = prof.key_averages(group_by_stack_n=6)
+        f.write(ks.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=40))
     print("wrote", a.out)
 
 
