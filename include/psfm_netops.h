@@ -15,9 +15,12 @@
  *
  * Layout: an activation is a bf16 matrix [M, C] row-major — the storage order of an NHWC
  * (torch.channels_last) tensor with M = N*H*W (GroupNorm: [N, HW, C]).  Statistics and
- * parameters are fp32.  Reductions are deterministic: per-workgroup partials in `ws`, summed
- * in a fixed order by the LAST workgroup to finish (an int device counter, `counter`, zeroed
- * once by the caller and re-armed by the kernel) — no float atomics.
+ * parameters are fp32.  Reductions are deterministic and single-launch: per-workgroup partials
+ * in `ws`, summed in a fixed order (fp64) by the last workgroup of each group of 16 and then by
+ * the last group to finish — no float atomics.  Arrivals are counted in `counter`, an int array
+ * of PSFM_NETOPS_COUNTER_INTS ("one slot", psfm_gn_act_bwd: two slots) zeroed once by the
+ * caller and re-armed by the kernels, so graph replays reuse it.  Two launches that may run
+ * concurrently must not share a slot.
  *
  * Conventions as include/psfm.h: device pointers, caller-owned buffers, stream-ordered,
  * graph-capturable; return 0 / <0 bad argument / >0 hipError_t, message from
@@ -32,6 +35,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define PSFM_NETOPS_COUNTER_INTS 256
 
 #define PSFM_ACT_NONE 0
 #define PSFM_ACT_RELU 1
@@ -72,7 +77,7 @@ int psfm_gn_act_fwd(const void* x, const void* bias, int bias_bf16, const float*
                     float* save_invstd, float* ws, int* counter, void* stream);
 
 /* Backward of psfm_gn_act_fwd: dx (bf16), dbias (bias dtype; the column sum of the stored dx, as
- * autograd forms a conv bias gradient), dgamma / dbeta (fp32 [C]).  Uses counter[0] and counter[1]. */
+ * autograd forms a conv bias gradient), dgamma / dbeta (fp32 [C]).  `counter` spans two slots. */
 int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bias, int bias_bf16,
                     const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C,
                     int G, int relu, void* dx, void* dbias, float* dgamma, float* dbeta, float* ws, int* counter,

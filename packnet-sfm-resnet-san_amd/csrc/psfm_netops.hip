@@ -2,12 +2,18 @@
 // pose networks (include/psfm_netops.h), gfx950.
 //
 // An activation is a bf16 matrix [M, C] (NHWC storage).  A workgroup of 256 threads covers TR
-// rows x C channels per iteration: thread t owns the VEC consecutive channels (t % G)*VEC.. of
+// rows x C channels per row step: thread t owns the VEC consecutive channels (t % G)*VEC.. of
 // row lane t / G (G = C/VEC; VEC = 8: one 16-byte load per thread, fully coalesced rows) and
-// walks its workgroup's row range with stride TR.  Column reductions: per-thread fp32 sums ->
-// LDS tree over the TR row lanes -> per-workgroup partials in `ws` -> the last workgroup to
-// arrive (device-scope int counter) sums the partials in a fixed order (fp64) and writes the
-// per-channel results.  Deterministic; no float atomics.
+// walks its workgroup's row range in steps of U*TR rows with U independent loads in flight.
+//
+// Column reductions (batch statistics, bias gradients) are deterministic and single-launch:
+//   per-thread fp32 sums -> LDS tree over the row lanes -> one partial row per workgroup
+//   -> the last workgroup of each group of GS workgroups sums its group's rows (fp64)
+//   -> the last group sums the group rows (fp64) and finalises the per-channel results.
+// Arrival order is counted on device-scope int counters (re-armed by the last arrival, so
+// graph replays reuse them).  Partials are written with device-coherent (sc1) stores and read
+// back with coherent vector loads, all of a row block in flight at once — the tail is two
+// short dependent rounds, not a serial sweep over hundreds of partials.  No float atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,8 +38,21 @@ int fail(int code, const char* msg) {
         }                                                            \
     } while (0)
 
-constexpr int NT = 256;
-constexpr int TARGET_BLOCKS = 512;  // ~2 workgroups per CU for the streaming passes
+#ifndef NETOPS_U
+#define NETOPS_U 4
+#endif
+#ifndef NETOPS_TARGET_BLOCKS
+#define NETOPS_TARGET_BLOCKS 512
+#endif
+#ifndef NETOPS_GS
+#define NETOPS_GS 16
+#endif
+constexpr int NT = 256;           // threads per workgroup
+constexpr int U = NETOPS_U;       // row steps unrolled (independent loads in flight per thread)
+constexpr int TARGET_BLOCKS = NETOPS_TARGET_BLOCKS;
+constexpr int GS = NETOPS_GS;     // workgroups per reduction group (ngroups)
+constexpr int MAX_KC = 1024;      // widest partial row (BN: 2*C, C <= 512)
+constexpr int CTR = PSFM_NETOPS_COUNTER_INTS;
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (NaN stays NaN)
@@ -41,11 +60,20 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (N
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
+__device__ __forceinline__ float bfround(float f) { return bf2f(f2bf(f)); }
 
 template <int VEC>
 struct Vec {
     float v[VEC];
 };
+
+template <int VEC>
+__device__ __forceinline__ Vec<VEC> zero() {
+    Vec<VEC> r;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r.v[i] = 0.0f;
+    return r;
+}
 
 template <int VEC>
 __device__ __forceinline__ Vec<VEC> ld_bf(const uint16_t* __restrict__ p) {
@@ -83,9 +111,26 @@ __device__ __forceinline__ void st_bf(uint16_t* __restrict__ p, const Vec<VEC>& 
 template <int VEC>
 __device__ __forceinline__ Vec<VEC> ld_f(const float* __restrict__ p) {
     Vec<VEC> r;
+    if constexpr (VEC == 8) {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        r.v[0] = a.x, r.v[1] = a.y, r.v[2] = a.z, r.v[3] = a.w;
+        r.v[4] = b.x, r.v[5] = b.y, r.v[6] = b.z, r.v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
+        for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
+    }
     return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void st_f(float* __restrict__ p, const Vec<VEC>& a) {
+    if constexpr (VEC == 8) {
+        *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        *reinterpret_cast<float4*>(p + 4) = make_float4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) p[i] = a.v[i];
+    }
 }
 
 // per-channel parameter vector (bf16 or fp32 storage)
@@ -98,26 +143,32 @@ __device__ __forceinline__ Vec<VEC> ld_param(const void* p, int bf, int c0) {
     return r;
 }
 
-// Work geometry of an [M, C] pass: G = C / VEC vector columns, TR = row lanes per workgroup.
+// ------------------------------------------------------------------------------------------
+// Work geometry of an [M, C] pass: G = C / VEC vector columns, TR = row lanes per workgroup,
+// rpb = rows per workgroup (a multiple of U*TR), nblk workgroups (<= TARGET_BLOCKS).
+// ------------------------------------------------------------------------------------------
 struct Geo {
     int G, TR, rpb, nblk;
 };
-// Reduction passes use fewer, fuller workgroups (>= MIN_ITERS rows per row lane): the partials
-// the last workgroup sums stay few.
-constexpr int RED_BLOCKS = 256;
-constexpr int MIN_ITERS = 8;
-inline Geo geometry(int M, int C, int vec, int target = TARGET_BLOCKS, int min_iters = 1) {
+inline Geo geometry(int M, int C, int vec, int target = TARGET_BLOCKS) {
     Geo g;
     g.G = C / vec;
     g.TR = std::max(1, NT / g.G);
-    int rpb = (M + target - 1) / target;
-    rpb = std::max(g.TR * min_iters, (rpb + g.TR - 1) / g.TR * g.TR);
-    rpb = std::min(rpb, (M + g.TR - 1) / g.TR * g.TR);
-    g.rpb = rpb;
-    g.nblk = (M + rpb - 1) / rpb;
+    const int step = g.TR * U;
+    const int per = (M + target - 1) / target;
+    g.rpb = std::max(step, (per + step - 1) / step * step);
+    g.nblk = (M + g.rpb - 1) / g.rpb;
     return g;
 }
 inline int pick_vec(int C) { return (C % 8 == 0 && C / 8 <= NT) ? 8 : 1; }
+__host__ __device__ inline int ngroups(int nblk) { return (nblk + GS - 1) / GS; }
+// floats of reduction workspace for nseg segments of nblk workgroups with KC-wide rows:
+// block rows [nseg*nblk][KC] fp32, then group rows [nseg*ngroups][KC] fp64.
+__host__ __device__ inline size_t align4(size_t n) { return (n + 3) / 4 * 4; }  // 16-byte alignment
+__host__ __device__ inline size_t tree_grp_off(int nseg, int nblk, int KC) { return align4((size_t)nseg * nblk * KC); }
+__host__ __device__ inline size_t tree_ws_floats(int nseg, int nblk, int KC) {
+    return tree_grp_off(nseg, nblk, KC) + 2 * (size_t)nseg * ngroups(nblk) * KC;
+}
 
 // Block column reduction of K per-thread vectors; afterwards row lane 0 holds the block sums.
 // red: LDS [K * NT * VEC] floats (TR * G <= NT).
@@ -151,75 +202,133 @@ __device__ __forceinline__ void block_colsum(float (&acc)[K][VEC], float* red, i
     }
 }
 
-// Cross-XCD visibility without cache-wide fences: the L2 of an XCD is not coherent with the
-// others, and a device-scope release fence would write back the whole L2 (buffer_wbl2) in every
-// workgroup.  Instead the partials are written with device-scope relaxed atomic stores and read
-// back with device-scope atomic loads (both bypass the non-coherent L2 level, sc1), their
-// completion is awaited explicitly (s_waitcnt) before the counter increment, and the counter is
-// a device-scope RMW (performed at the coherent memory side).
+// ---- device-coherent partial traffic -------------------------------------------------------
+// The L2 of an XCD is not coherent with the others.  Partials are stored with agent-scope
+// relaxed atomic stores (global_store ... sc1) and read back with sc1 loads, so no cache-wide
+// writeback / invalidate fence is needed; completion is awaited (s_waitcnt) before the
+// arrival counter increment, which is a device-scope RMW.
 __device__ __forceinline__ void st_part(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_part(double* p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ float ld_part(const float* p) {
     return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ double ld_part(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int CPOL_SC1 = 16;             // gfx94x/gfx950 cache policy: agent-scope coherent
+constexpr int RSRC_WORD3 = 0x00020000;   // raw buffer resource, gfx9 data format
 
-// Last-workgroup election after this workgroup's partials are stored (st_part): true (in every
-// thread) only in the last workgroup, which then reads every other workgroup's partials with
-// ld_part.  The counter is re-armed to 0 for the next launch (graph replays included).
-__device__ __forceinline__ bool last_block(int* counter, int nblk) {
+// coherent 16-byte load of base[off_bytes/4 ..] (buffer_load_dwordx4 ... sc1; the resource is
+// wave-uniform, set up once in SGPRs)
+__device__ __forceinline__ float4 ld4_part(const float* base, int nbytes, int off_bytes) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, RSRC_WORD3);
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off_bytes, 0, CPOL_SC1));
+}
+
+// true (in every thread) only in the last of n workgroups to arrive on *ctr; re-arms *ctr.
+__device__ __forceinline__ bool arrive(int* ctr, int n) {
     __shared__ int is_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (prev == nblk - 1);
-        if (is_last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == n - 1);
+        if (is_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     return is_last;
 }
 
-// Fixed-order sum of the K partial arrays ws[b*stride + k*C + c] over b in [b0, b0+nb) for the
-// channels [cbeg, cbeg+nc) (nc <= NT): threads split channels x block ranges, combined through
-// LDS in fixed order.  out[k*nc + i] (fp64, LDS), valid after the call in every thread.
-template <int K>
-__device__ void final_colsum(const float* __restrict__ ws, size_t stride, int b0, int nb, int C, int cbeg, int nc,
-                             double* out, double* scratch /* LDS [NT*K] */) {
+// fin[c] = sum over rows r in [0, nrows) of src[r*KC + c] in fixed row order (fp64), valid in
+// every thread on return.  All NT threads take part: thread = (row lane, column vector); each
+// issues all its (<= 32) loads before summing.  scratch: LDS [NT * 4] doubles.
+template <typename T>
+__device__ void sum_rows(const T* src, int nrows, int KC, double* fin, double* scratch) {
     const int t = threadIdx.x;
-    const int tpc = NT / nc;
-    const int c = cbeg + t % nc, sub = t / nc;
-    double s[K];
+    constexpr bool F4 = sizeof(T) == 4;
+    const int W = (F4 && KC % 4 == 0) ? 4 : 1;
+    const int QW = KC / W;
+    const int LN = QW >= NT ? 1 : NT / QW;
+    const int l = t / QW, q = t % QW;
+    for (int qq = (QW >= NT ? t : q); qq < QW && l < LN; qq += (QW >= NT ? NT : QW)) {
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int r0 = (QW >= NT ? 0 : l); r0 < nrows; r0 += 8 * LN) {
+            if (W == 4) {
+                float4 v[8];
 #pragma unroll
-    for (int k = 0; k < K; ++k) s[k] = 0.0;
-    if (sub < tpc) {
-        constexpr int U = 8;  // independent loads in flight per thread, summed in order after
-        for (int b = sub; b < nb; b += U * tpc) {
-            float v[U][K];
+                for (int u = 0; u < 8; ++u) {
+                    const int rr = r0 + u * LN;
+                    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if constexpr (F4)
+                        if (rr < nrows) v[u] = ld4_part(src, nrows * KC * 4, (rr * KC + qq * 4) * 4);
+                }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int bb = b + u * tpc;
+                for (int u = 0; u < 8; ++u) {
+                    s[0] += (double)v[u].x;
+                    s[1] += (double)v[u].y;
+                    s[2] += (double)v[u].z;
+                    s[3] += (double)v[u].w;
+                }
+            } else {
+                T v[8];
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                    v[u][k] = bb < nb ? ld_part(&ws[(size_t)(b0 + bb) * stride + (size_t)k * C + c]) : 0.0f;
+                for (int u = 0; u < 8; ++u) {
+                    const int rr = r0 + u * LN;
+                    v[u] = rr < nrows ? ld_part(src + (size_t)rr * KC + qq) : (T)0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s[0] += (double)v[u];
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int k = 0; k < K; ++k) s[k] += (double)v[u][k];
+        }
+        if (QW >= NT) {  // one lane: the thread's sums are final
+            for (int i = 0; i < W; ++i) fin[qq * W + i] = s[i];
+        } else {
+            for (int i = 0; i < W; ++i) scratch[(l * QW + qq) * W + i] = s[i];
         }
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) scratch[t * K + k] = s[k];
     __syncthreads();
-    if (t < nc) {
-        for (int u = 1; u < tpc; ++u)
-#pragma unroll
-            for (int k = 0; k < K; ++k) s[k] += scratch[(u * nc + t) * K + k];
-#pragma unroll
-        for (int k = 0; k < K; ++k) out[k * nc + t] = s[k];
+    if (QW < NT) {
+        for (int c = t; c < KC; c += NT) {  // lanes combined in lane order
+            double a = 0.0;
+            for (int ll = 0; ll < LN; ++ll) a += scratch[ll * KC + c];
+            fin[c] = a;
+        }
+        __syncthreads();
     }
-    __syncthreads();
+}
+
+// Two-level deterministic reduction of one segment's block rows.  rows: [nblk][KC] fp32
+// (this workgroup's row already stored), grp: [ngroups][KC] fp64, ctr: 1 + ngroups ints.
+// Returns true in the single workgroup that finishes the segment; fin = column totals.
+__device__ bool tree_reduce(float* rows, double* grp, int* ctr, int b, int nblk, int KC, double* fin,
+                            double* scratch) {
+#ifdef NETOPS_NO_TREE  // timing experiment only: the streaming cost without the reduction tail
+    return false;
+#endif
+    const int g = b / GS, ng = ngroups(nblk);
+    const int n_in = min(GS, nblk - g * GS);
+    if (!arrive(ctr + 1 + g, n_in)) return false;
+    sum_rows<float>(rows + (size_t)g * GS * KC, n_in, KC, fin, scratch);
+    if (ng == 1) return true;
+    for (int c = threadIdx.x; c < KC; c += NT) st_part(grp + (size_t)g * KC + c, fin[c]);
+    if (!arrive(ctr, ng)) return false;
+    sum_rows<double>(grp, ng, KC, fin, scratch);
+    return true;
+}
+
+// this workgroup's K x VEC column sums (row lane 0 threads) -> its partial row
+template <int VEC, int K>
+__device__ __forceinline__ void store_row(float* row, const float (&acc)[K][VEC], int C, int c0, int r) {
+    if (r == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) st_part(row + k * C + c0 + i, acc[k][i]);
+    }
 }
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -227,6 +336,10 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
     if (act == PSFM_ACT_SIGMOID) return 1.0f / (1.0f + expf(-v));
     return v;
 }
+
+#define ROW_LOOP_BEGIN(ROW0, ROW1, R, TR)                           \
+    for (int base_ = (ROW0) + (R); base_ < (ROW1); base_ += U * (TR)) {
+#define ROW_LOOP_END }
 
 // ------------------------------------------------------------------------------------------
 // bias + activation (decoder ConvBlock / disparity head)
@@ -250,26 +363,33 @@ __global__ __launch_bounds__(NT) void k_bias_act_fwd(BiasArgs a) {
     const int c0 = cg * VEC;
     const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
     const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    for (int row = row0 + r; row < row1; row += a.TR) {
-        const size_t o = (size_t)row * a.C + c0;
-        Vec<VEC> v = ld_bf<VEC>(a.x + o);
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    Vec<VEC> v[U];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) v.v[i] = act_fwd(v.v[i] + b.v[i], a.act);
-        if (a.act == PSFM_ACT_SIGMOID) {
-            float* y = static_cast<float*>(a.out) + o;
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) y[i] = v.v[i];
-        } else {
-            st_bf<VEC>(static_cast<uint16_t*>(a.out) + o, v);
-        }
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        v[u] = row < row1 ? ld_bf<VEC>(a.x + (size_t)row * a.C + c0) : zero<VEC>();
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
+        const size_t o = (size_t)row * a.C + c0;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) v[u].v[i] = act_fwd(v[u].v[i] + b.v[i], a.act);
+        if (a.act == PSFM_ACT_SIGMOID)
+            st_f<VEC>(static_cast<float*>(a.out) + o, v[u]);
+        else
+            st_bf<VEC>(static_cast<uint16_t*>(a.out) + o, v[u]);
+    }
+    ROW_LOOP_END
 }
 
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bias_act_bwd(BiasArgs a) {
     __shared__ float red[NT * VEC];
-    __shared__ double fin[NT];
-    __shared__ double scratch[NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[1][VEC];
@@ -277,45 +397,51 @@ __global__ __launch_bounds__(NT) void k_bias_act_bwd(BiasArgs a) {
     for (int i = 0; i < VEC; ++i) acc[0][i] = 0.0f;
     if (r < a.TR) {
         const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
+        const bool sig = a.act == PSFM_ACT_SIGMOID;
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> dy[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
             const size_t o = (size_t)row * a.C + c0;
-            Vec<VEC> g;
-            if (a.act == PSFM_ACT_SIGMOID) {
-                const Vec<VEC> dy = ld_f<VEC>(static_cast<const float*>(a.dy) + o);
-                const Vec<VEC> y = ld_f<VEC>(static_cast<const float*>(a.y) + o);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) g.v[i] = dy.v[i] * ((1.0f - y.v[i]) * y.v[i]);
+            if (row < row1) {
+                dy[u] = sig ? ld_f<VEC>(static_cast<const float*>(a.dy) + o)
+                            : ld_bf<VEC>(static_cast<const uint16_t*>(a.dy) + o);
+                y[u] = sig ? ld_f<VEC>(static_cast<const float*>(a.y) + o)
+                           : ld_bf<VEC>(static_cast<const uint16_t*>(a.y) + o);
             } else {
-                const Vec<VEC> dy = ld_bf<VEC>(static_cast<const uint16_t*>(a.dy) + o);
-                const Vec<VEC> y = ld_bf<VEC>(static_cast<const uint16_t*>(a.y) + o);
-#pragma unroll
-                for (int i = 0; i < VEC; ++i)
-                    g.v[i] = (a.act == PSFM_ACT_RELU && !(y.v[i] > 0.0f)) ? 0.0f : dy.v[i];
+                dy[u] = zero<VEC>();
+                y[u] = zero<VEC>();
             }
-            Vec<VEC> gq;  // the stored (bf16) gradient is the one the bias sums, as autograd's would
-            st_bf<VEC>(static_cast<uint16_t*>(a.out) + o, g);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) gq.v[i] = bf2f(f2bf(g.v[i]));
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) acc[0][i] += gq.v[i];
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            if (row >= row1) break;
+            Vec<VEC> g;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+                if (sig)
+                    g.v[i] = dy[u].v[i] * ((1.0f - y[u].v[i]) * y[u].v[i]);
+                else
+                    g.v[i] = (a.act == PSFM_ACT_RELU && !(y[u].v[i] > 0.0f)) ? 0.0f : dy[u].v[i];
+            }
+            st_bf<VEC>(static_cast<uint16_t*>(a.out) + (size_t)row * a.C + c0, g);
+            // the stored (bf16) gradient is the one the bias sums, as autograd's would
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc[0][i] += bfround(g.v[i]);
+        }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 1>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) st_part(&a.ws[(size_t)blockIdx.x * a.C + c0 + i], acc[0][i]);
-    }
-    if (!last_block(a.counter, a.nblk)) return;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int nc = min(NT, a.C - cb);
-        final_colsum<1>(a.ws, a.C, 0, a.nblk, a.C, cb, nc, fin, scratch);
-        if (t < nc) {
-            if (a.bias_bf16)
-                static_cast<uint16_t*>(a.dbias)[cb + t] = f2bf((float)fin[t]);
-            else
-                static_cast<float*>(a.dbias)[cb + t] = (float)fin[t];
-        }
-        __syncthreads();
+    store_row<VEC, 1>(a.ws + (size_t)blockIdx.x * a.C, acc, a.C, c0, r);
+    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, a.C));
+    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, a.C, fin, scratch)) return;
+    for (int c = t; c < a.C; c += NT) {
+        if (a.bias_bf16)
+            static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)fin[c]);
+        else
+            static_cast<float*>(a.dbias)[c] = (float)fin[c];
     }
 }
 
@@ -337,19 +463,23 @@ struct BNArgs {
     uint16_t* dres;  // bwd
     float* dgamma;
     float* dbeta;
-    float* ws;       // [nblk][2][C] partials, then [2][C] coefficients
+    float* ws;       // reduction tree, then [3][C] coefficients
     int* counter;
     float momentum, eps;
     int M, C, relu, G, TR, rpb, nblk;
 };
 
-// pass 1: per-channel sum / sum of squares; last block -> mean, invstd, running stats and the
-// affine coefficients scale = gamma*invstd, shift = beta - mean*scale (ws tail).
+__device__ __forceinline__ float* bn_coef(const BNArgs& a) {
+    return a.ws + tree_ws_floats(1, a.nblk, 2 * a.C);
+}
+
+// pass 1: per-channel sum / sum of squares; the finishing workgroup -> mean, invstd, running
+// stats and the affine coefficients scale = gamma*invstd, shift = beta - mean*scale.
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bn_fwd_stats(BNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[2 * NT];
-    __shared__ double scratch[2 * NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[2][VEC];
@@ -357,46 +487,43 @@ __global__ __launch_bounds__(NT) void k_bn_fwd_stats(BNArgs a) {
     for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
     if (r < a.TR) {
         const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
-            const Vec<VEC> v = ld_bf<VEC>(a.x + (size_t)row * a.C + c0);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            v[u] = row < row1 ? ld_bf<VEC>(a.x + (size_t)row * a.C + c0) : zero<VEC>();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                acc[0][i] += v.v[i];
-                acc[1][i] += v.v[i] * v.v[i];
+                acc[0][i] += v[u].v[i];
+                acc[1][i] += v[u].v[i] * v[u].v[i];
             }
-        }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 0) * a.C + c0 + i], acc[0][i]);
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 1) * a.C + c0 + i], acc[1][i]);
-        }
-    }
-    if (!last_block(a.counter, a.nblk)) return;
-    float* coef = a.ws + (size_t)a.nblk * 2 * a.C;  // [2][C]: scale, shift
+    const int KC = 2 * a.C;
+    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * KC, acc, a.C, c0, r);
+    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, KC));
+    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, KC, fin, scratch)) return;
+    float* coef = bn_coef(a);  // [2][C]: scale, shift
     const double inv_m = 1.0 / (double)a.M;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int nc = min(NT, a.C - cb);
-        final_colsum<2>(a.ws, 2 * (size_t)a.C, 0, a.nblk, a.C, cb, nc, fin, scratch);
-        if (t < nc) {
-            const int c = cb + t;
-            const double mean = fin[t] * inv_m;
-            const double var = fmax(fin[nc + t] * inv_m - mean * mean, 0.0);
-            const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-            a.save_mean[c] = (float)mean;
-            a.save_invstd[c] = invstd;
-            if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
-                const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-                a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
-                a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-            }
-            const float scale = a.gamma[c] * invstd;
-            coef[c] = scale;
-            coef[a.C + c] = a.beta[c] - (float)mean * scale;
+    for (int c = t; c < a.C; c += NT) {
+        const double mean = fin[c] * inv_m;
+        const double var = fmax(fin[a.C + c] * inv_m - mean * mean, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        a.save_mean[c] = (float)mean;
+        a.save_invstd[c] = invstd;
+        if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
+            const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
+            a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
+            a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
         }
-        __syncthreads();
+        const float scale = a.gamma[c] * invstd;
+        coef[c] = scale;
+        coef[a.C + c] = a.beta[c] - (float)mean * scale;
     }
 }
 
@@ -406,35 +533,42 @@ __global__ __launch_bounds__(NT) void k_bn_fwd_apply(BNArgs a) {
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     if (r >= a.TR) return;
     const int c0 = cg * VEC;
-    const float* coef = a.ws + (size_t)a.nblk * 2 * a.C;
+    const float* coef = bn_coef(a);
     const Vec<VEC> sc = ld_f<VEC>(coef + c0), sh = ld_f<VEC>(coef + a.C + c0);
     const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    for (int row = row0 + r; row < row1; row += a.TR) {
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    Vec<VEC> v[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
         const size_t o = (size_t)row * a.C + c0;
-        Vec<VEC> v = ld_bf<VEC>(a.x + o);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) v.v[i] = v.v[i] * sc.v[i] + sh.v[i];
-        if (a.res) {
-            // the reference rounds bn(x) to bf16 before the residual add (both operands bf16)
-            const Vec<VEC> rv = ld_bf<VEC>(a.res + o);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) v.v[i] = bf2f(f2bf(v.v[i])) + rv.v[i];
-        }
-        if (a.relu) {
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) v.v[i] = fmaxf(v.v[i], 0.0f);
-        }
-        st_bf<VEC>(a.out + o, v);
+        v[u] = row < row1 ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+        if (a.res) rv[u] = row < row1 ? ld_bf<VEC>(a.res + o) : zero<VEC>();
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            float w = v[u].v[i] * sc.v[i] + sh.v[i];
+            // the reference rounds bn(x) to bf16 before the residual add (both operands bf16)
+            if (a.res) w = bfround(w) + rv[u].v[i];
+            if (a.relu) w = fmaxf(w, 0.0f);
+            v[u].v[i] = w;
+        }
+        st_bf<VEC>(a.out + (size_t)row * a.C + c0, v[u]);
+    }
+    ROW_LOOP_END
 }
 
-// backward pass 1: per channel sum(dyr), sum(dyr * (x - mean)); last block -> dgamma, dbeta and
-// dx coefficients k1 = gamma*invstd, k2 = sum(dyr)/M, k3 = sum(dyr*xc)*invstd^2/M.
+// backward pass 1: per channel sum(dyr), sum(dyr * (x - mean)); finishing workgroup -> dgamma,
+// dbeta and dx coefficients k1 = gamma*invstd, k2 = sum(dyr)/M, k3 = sum(dyr*xc)*invstd^2/M.
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bn_bwd_stats(BNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[2 * NT];
-    __shared__ double scratch[2 * NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[2][VEC];
@@ -443,46 +577,41 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_stats(BNArgs a) {
     if (r < a.TR) {
         const Vec<VEC> mu = ld_f<VEC>(a.save_mean + c0);
         const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
-            const size_t o = (size_t)row * a.C + c0;
-            Vec<VEC> g = ld_bf<VEC>(a.dy + o);
-            if (a.relu) {
-                const Vec<VEC> y = ld_bf<VEC>(a.y + o);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> g[U], y[U], x[U];
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) g.v[i] = y.v[i] > 0.0f ? g.v[i] : 0.0f;
-            }
-            const Vec<VEC> x = ld_bf<VEC>(a.x + o);
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            const size_t o = (size_t)row * a.C + c0;
+            const bool in = row < row1;
+            g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
+            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+            x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                acc[0][i] += g.v[i];
-                acc[1][i] += g.v[i] * (x.v[i] - mu.v[i]);
+                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
+                acc[0][i] += gg;
+                acc[1][i] += gg * (x[u].v[i] - mu.v[i]);
             }
-        }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 0) * a.C + c0 + i], acc[0][i]);
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 1) * a.C + c0 + i], acc[1][i]);
-        }
-    }
-    if (!last_block(a.counter, a.nblk)) return;
-    float* coef = a.ws + (size_t)a.nblk * 2 * a.C;  // [3][C]
+    const int KC = 2 * a.C;
+    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * KC, acc, a.C, c0, r);
+    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, KC));
+    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, KC, fin, scratch)) return;
+    float* coef = bn_coef(a);  // [3][C]
     const double inv_m = 1.0 / (double)a.M;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int nc = min(NT, a.C - cb);
-        final_colsum<2>(a.ws, 2 * (size_t)a.C, 0, a.nblk, a.C, cb, nc, fin, scratch);
-        if (t < nc) {
-            const int c = cb + t;
-            const double is = a.save_invstd[c];
-            a.dbeta[c] = (float)fin[t];
-            a.dgamma[c] = (float)(fin[nc + t] * is);
-            coef[c] = a.gamma[c] * (float)is;
-            coef[a.C + c] = (float)(fin[t] * inv_m);
-            coef[2 * a.C + c] = (float)(fin[nc + t] * is * is * inv_m);
-        }
-        __syncthreads();
+    for (int c = t; c < a.C; c += NT) {
+        const double is = a.save_invstd[c];
+        a.dbeta[c] = (float)fin[c];
+        a.dgamma[c] = (float)(fin[a.C + c] * is);
+        coef[c] = a.gamma[c] * (float)is;
+        coef[a.C + c] = (float)(fin[c] * inv_m);
+        coef[2 * a.C + c] = (float)(fin[a.C + c] * is * is * inv_m);
     }
 }
 
@@ -492,29 +621,41 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     if (r >= a.TR) return;
     const int c0 = cg * VEC;
-    const float* coef = a.ws + (size_t)a.nblk * 2 * a.C;
+    const float* coef = bn_coef(a);
     const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
     const Vec<VEC> mu = ld_f<VEC>(a.save_mean + c0);
     const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    for (int row = row0 + r; row < row1; row += a.TR) {
-        const size_t o = (size_t)row * a.C + c0;
-        Vec<VEC> g = ld_bf<VEC>(a.dy + o);
-        if (a.relu) {
-            const Vec<VEC> y = ld_bf<VEC>(a.y + o);
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    Vec<VEC> g[U], y[U], x[U];
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) g.v[i] = y.v[i] > 0.0f ? g.v[i] : 0.0f;
-        }
-        if (a.dres) st_bf<VEC>(a.dres + o, g);
-        const Vec<VEC> x = ld_bf<VEC>(a.x + o);
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        const size_t o = (size_t)row * a.C + c0;
+        const bool in = row < row1;
+        g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
+        if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+        x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
+        const size_t o = (size_t)row * a.C + c0;
         Vec<VEC> d;
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) d.v[i] = k1.v[i] * ((g.v[i] - k2.v[i]) - (x.v[i] - mu.v[i]) * k3.v[i]);
+        for (int i = 0; i < VEC; ++i) {
+            if (a.relu && !(y[u].v[i] > 0.0f)) g[u].v[i] = 0.0f;
+            d.v[i] = k1.v[i] * ((g[u].v[i] - k2.v[i]) - (x[u].v[i] - mu.v[i]) * k3.v[i]);
+        }
+        if (a.dres) st_bf<VEC>(a.dres + o, g[u]);
         st_bf<VEC>(a.out + o, d);
     }
+    ROW_LOOP_END
 }
 
 // ------------------------------------------------------------------------------------------
-// GroupNorm(G) of (x + bias) + ReLU, per sample n over rows [n*HW, (n+1)*HW)
+// GroupNorm(NG) of (x + bias) + ReLU, per sample n over rows [n*HW, (n+1)*HW).  Each sample is
+// its own reduction segment (bpn workgroups, counters at counter + n*(1+ngroups(bpn))).
 // ------------------------------------------------------------------------------------------
 struct GNArgs {
     const uint16_t* x;
@@ -523,26 +664,39 @@ struct GNArgs {
     const uint16_t* y;
     const float* gamma;
     const float* beta;
-    float* save_mean;    // [N*G]
-    float* save_invstd;  // [N*G]
+    float* save_mean;    // [N*NG]
+    float* save_invstd;  // [N*NG]
     uint16_t* out;
     void* dbias;
     float* dgamma;
     float* dbeta;
-    float* ws;  // [N][bpn][K][C] partials, then coefficients
+    float* ws;
     int* counter;
     float eps;
     int N, HW, C, NG, relu, bias_bf16, G, TR, rpb, bpn;  // bpn: workgroups per sample
 };
 
-// forward pass 1: per (n, c) sum / sumsq of x+bias; last block -> per (n, g) mean / invstd and
-// per (n, c) affine coefficients scale = gamma*invstd, shift = beta - mean*scale (bias folded:
-// y = (x + bias)*scale + shift).
+// workspace: stats tree [N segs][2C] | coef [N][3][C] | per-sample bwd rows [N][2C] fp64 |
+//            dbias tree [1 seg of N*bpn][C]
+__device__ __forceinline__ size_t gn_off_coef(const GNArgs& a) { return tree_ws_floats(a.N, a.bpn, 2 * a.C); }
+__device__ __forceinline__ size_t gn_off_nrows(const GNArgs& a) { return align4(gn_off_coef(a) + (size_t)a.N * 3 * a.C); }
+__device__ __forceinline__ size_t gn_off_dbias(const GNArgs& a) { return gn_off_nrows(a) + 2 * (size_t)a.N * 2 * a.C; }
+
+// stats segment of sample n: block rows at ws + n*bpn*KC, group rows after all block rows.
+__device__ __forceinline__ bool gn_tree(const GNArgs& a, int n, int bl, double* fin, double* scratch) {
+    const int KC = 2 * a.C;
+    float* rows = a.ws + (size_t)n * a.bpn * KC;
+    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(a.N, a.bpn, KC)) + (size_t)n * ngroups(a.bpn) * KC;
+    return tree_reduce(rows, grp, a.counter + n * (1 + ngroups(a.bpn)), bl, a.bpn, KC, fin, scratch);
+}
+
+// forward pass 1: per (n, c) sum / sumsq of x+bias; finishing workgroup of sample n -> per
+// (n, g) mean / invstd and per (n, c) affine coefficients (bias folded: y = (x+bias)*scale + shift).
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[2 * NT];
-    __shared__ double scratch[2 * NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
@@ -551,61 +705,50 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
     for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
     if (r < a.TR) {
         const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+        const uint16_t* xs = a.x + (size_t)n * a.HW * a.C;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
-            const Vec<VEC> v = ld_bf<VEC>(a.x + ((size_t)n * a.HW + row) * a.C + c0);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> v[U];
+        bool in[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            in[u] = row < row1;
+            v[u] = in[u] ? ld_bf<VEC>(xs + (size_t)row * a.C + c0) : zero<VEC>();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float u = v.v[i] + b.v[i];
-                acc[0][i] += u;
-                acc[1][i] += u * u;
+                const float w = in[u] ? v[u].v[i] + b.v[i] : 0.0f;
+                acc[0][i] += w;
+                acc[1][i] += w * w;
             }
-        }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 0) * a.C + c0 + i], acc[0][i]);
-            st_part(&a.ws[((size_t)blockIdx.x * 2 + 1) * a.C + c0 + i], acc[1][i]);
-        }
-    }
-    if (!last_block(a.counter, a.N * a.bpn)) return;
-    // per (n, c) totals, then per group (fixed channel order)
-    __shared__ double gsum[2 * NT];
-    float* coef = a.ws + (size_t)a.N * a.bpn * 2 * a.C;  // [N][2][C]
+    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * 2 * a.C, acc, a.C, c0, r);
+    if (!gn_tree(a, n, bl, fin, scratch)) return;
+    float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
     const int cpg = a.C / a.NG;
     const double inv_cnt = 1.0 / ((double)a.HW * cpg);
-    for (int nn = 0; nn < a.N; ++nn) {
-        for (int cb = 0; cb < a.C; cb += NT) {  // C <= NT for every PoseNet layer; general anyway
-            const int nc = min(NT, a.C - cb);
-            final_colsum<2>(a.ws, 2 * (size_t)a.C, nn * a.bpn, a.bpn, a.C, cb, nc, fin, scratch);
-            if (t < nc) {
-                gsum[t] = fin[t];
-                gsum[NT + t] = fin[nc + t];
-            }
-            __syncthreads();
-            if (t < nc) {
-                const int c = cb + t, g = c / cpg;
-                const int first = g * cpg - cb;  // groups never straddle a chunk: NT % cpg == 0
-                double s = 0.0, q = 0.0;
-                for (int u = 0; u < cpg; ++u) {
-                    s += gsum[first + u];
-                    q += gsum[NT + first + u];
-                }
-                const double mean = s * inv_cnt;
-                const double var = fmax(q * inv_cnt - mean * mean, 0.0);
-                const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-                if (c % cpg == 0) {
-                    a.save_mean[nn * a.NG + g] = (float)mean;
-                    a.save_invstd[nn * a.NG + g] = invstd;
-                }
-                const float scale = a.gamma[c] * invstd;
-                coef[((size_t)nn * 2 + 0) * a.C + c] = scale;
-                coef[((size_t)nn * 2 + 1) * a.C + c] = a.beta[c] - (float)mean * scale;
-            }
-            __syncthreads();
+    for (int c = t; c < a.C; c += NT) {
+        const int g = c / cpg;
+        double s = 0.0, q = 0.0;
+        for (int u = 0; u < cpg; ++u) {  // group sums in channel order
+            s += fin[g * cpg + u];
+            q += fin[a.C + g * cpg + u];
         }
+        const double mean = s * inv_cnt;
+        const double var = fmax(q * inv_cnt - mean * mean, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        if (c % cpg == 0) {
+            a.save_mean[n * a.NG + g] = (float)mean;
+            a.save_invstd[n * a.NG + g] = invstd;
+        }
+        const float scale = a.gamma[c] * invstd;
+        coef[c] = scale;
+        coef[a.C + c] = a.beta[c] - (float)mean * scale;
     }
 }
 
@@ -615,30 +758,42 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_apply(GNArgs a) {
     if (r >= a.TR) return;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
-    const float* coef = a.ws + (size_t)a.N * a.bpn * 2 * a.C + (size_t)n * 2 * a.C;
+    const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
     const Vec<VEC> sc = ld_f<VEC>(coef + c0), sh = ld_f<VEC>(coef + a.C + c0);
     const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+    const size_t so = (size_t)n * a.HW * a.C;
     const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-    for (int row = row0 + r; row < row1; row += a.TR) {
-        const size_t o = ((size_t)n * a.HW + row) * a.C + c0;
-        Vec<VEC> v = ld_bf<VEC>(a.x + o);
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    Vec<VEC> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        v[u] = row < row1 ? ld_bf<VEC>(a.x + so + (size_t)row * a.C + c0) : zero<VEC>();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
-            v.v[i] = (v.v[i] + b.v[i]) * sc.v[i] + sh.v[i];
-            if (a.relu) v.v[i] = fmaxf(v.v[i], 0.0f);
+            float w = (v[u].v[i] + b.v[i]) * sc.v[i] + sh.v[i];
+            if (a.relu) w = fmaxf(w, 0.0f);
+            v[u].v[i] = w;
         }
-        st_bf<VEC>(a.out + o, v);
+        st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, v[u]);
     }
+    ROW_LOOP_END
 }
 
-// backward pass 1: per (n, c): S1 = sum dyr, S2 = sum dyr*xhat.  Last block: dbeta[c] = sum_n
-// S1, dgamma[c] = sum_n S2, per (n, g): A = sum_{c in g} gamma S1, Bq = sum_{c in g} gamma S2;
-// dx = invstd (gamma dyr - A/cnt - xhat Bq/cnt) (coefficients for pass 2).
+// backward pass 1: per (n, c): S1 = sum dyr, S2 = sum dyr*xhat.  Finishing workgroup of sample
+// n: per (n, g) A = sum_{c in g} gamma S1, Bq = sum_{c in g} gamma S2 -> dx coefficients
+// dx = invstd (gamma dyr - A/cnt - xhat Bq/cnt); it stores (S1, S2)[n] and the last sample to
+// finish sums them over n (sample order) into dbeta / dgamma.
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[2 * NT];
-    __shared__ double scratch[2 * NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
@@ -654,67 +809,59 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
             mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
             is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
         }
+        const size_t so = (size_t)n * a.HW * a.C;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
-            const size_t o = ((size_t)n * a.HW + row) * a.C + c0;
-            Vec<VEC> g = ld_bf<VEC>(a.dy + o);
-            if (a.relu) {
-                const Vec<VEC> y = ld_bf<VEC>(a.y + o);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> g[U], y[U], x[U];
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) g.v[i] = y.v[i] > 0.0f ? g.v[i] : 0.0f;
-            }
-            const Vec<VEC> x = ld_bf<VEC>(a.x + o);
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            const size_t o = so + (size_t)row * a.C + c0;
+            const bool in = row < row1;
+            g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
+            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+            x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float xh = (x.v[i] + b.v[i] - mu[i]) * is[i];
-                acc[0][i] += g.v[i];
-                acc[1][i] += g.v[i] * xh;
+                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
+                const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
+                acc[0][i] += gg;
+                acc[1][i] += gg * xh;
             }
-        }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) st_part(&a.ws[((size_t)blockIdx.x * 2 + k) * a.C + c0 + i], acc[k][i]);
-    }
-    if (!last_block(a.counter, a.N * a.bpn)) return;
-    __shared__ double gs[2 * NT];
-    float* coef = a.ws + (size_t)a.N * a.bpn * 2 * a.C;  // [N][3][C]: k1 = gamma*invstd, k2 = A/cnt*invstd, k3 = Bq/cnt*invstd
+    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * 2 * a.C, acc, a.C, c0, r);
+    if (!gn_tree(a, n, bl, fin, scratch)) return;
+    float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;  // k1 = gamma*invstd, k2 = A/cnt*invstd, k3 = Bq/cnt*invstd
+    double* nrows = reinterpret_cast<double*>(a.ws + gn_off_nrows(a));  // [N][2C]
     const double cnt = (double)a.HW * cpg;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int nc = min(NT, a.C - cb);
+    for (int c = t; c < a.C; c += NT) {
+        const int g = c / cpg;
+        double A = 0.0, Bq = 0.0;
+        for (int u = 0; u < cpg; ++u) {
+            const int cc = g * cpg + u;
+            A += (double)a.gamma[cc] * fin[cc];
+            Bq += (double)a.gamma[cc] * fin[a.C + cc];
+        }
+        const double is = a.save_invstd[n * a.NG + g];
+        coef[c] = a.gamma[c] * (float)is;
+        coef[a.C + c] = (float)(A / cnt * is);
+        coef[2 * a.C + c] = (float)(Bq / cnt * is);
+    }
+    for (int c = t; c < 2 * a.C; c += NT) st_part(nrows + (size_t)n * 2 * a.C + c, fin[c]);
+    if (!arrive(a.counter + a.N * (1 + ngroups(a.bpn)), a.N)) return;
+    for (int c = t; c < a.C; c += NT) {
         double db = 0.0, dg = 0.0;
         for (int nn = 0; nn < a.N; ++nn) {
-            final_colsum<2>(a.ws, 2 * (size_t)a.C, nn * a.bpn, a.bpn, a.C, cb, nc, fin, scratch);
-            if (t < nc) {
-                const float gam = a.gamma[cb + t];
-                gs[t] = gam * fin[t];
-                gs[NT + t] = gam * fin[nc + t];
-            }
-            __syncthreads();
-            if (t < nc) {
-                const int c = cb + t, g = c / cpg, first = g * cpg - cb;
-                double A = 0.0, Bq = 0.0;
-                for (int u = 0; u < cpg; ++u) {
-                    A += gs[first + u];
-                    Bq += gs[NT + first + u];
-                }
-                const double is = a.save_invstd[nn * a.NG + g];
-                db += fin[t];
-                dg += fin[nc + t];
-                coef[((size_t)nn * 3 + 0) * a.C + c] = a.gamma[c] * (float)is;
-                coef[((size_t)nn * 3 + 1) * a.C + c] = (float)(A / cnt * is);
-                coef[((size_t)nn * 3 + 2) * a.C + c] = (float)(Bq / cnt * is);
-            }
-            __syncthreads();
+            db += ld_part(nrows + (size_t)nn * 2 * a.C + c);
+            dg += ld_part(nrows + (size_t)nn * 2 * a.C + a.C + c);
         }
-        if (t < nc) {
-            a.dbeta[cb + t] = (float)db;
-            a.dgamma[cb + t] = (float)dg;
-        }
-        __syncthreads();
+        a.dbeta[c] = (float)db;
+        a.dgamma[c] = (float)dg;
     }
 }
 
@@ -723,8 +870,8 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
     __shared__ float red[NT * VEC];
-    __shared__ double fin[NT];
-    __shared__ double scratch[NT];
+    __shared__ double fin[MAX_KC];
+    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
@@ -732,9 +879,8 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
     float acc[1][VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[0][i] = 0.0f;
-    float* part = a.ws + (size_t)a.N * a.bpn * 2 * a.C + (size_t)a.N * 3 * a.C;  // [N*bpn][C]
     if (r < a.TR) {
-        const float* coef = a.ws + (size_t)a.N * a.bpn * 2 * a.C + (size_t)n * 3 * a.C;
+        const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
         const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
         const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
         float mu[VEC], is[VEC];
@@ -743,43 +889,47 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
             mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
             is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
         }
+        const size_t so = (size_t)n * a.HW * a.C;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-        for (int row = row0 + r; row < row1; row += a.TR) {
-            const size_t o = ((size_t)n * a.HW + row) * a.C + c0;
-            Vec<VEC> g = ld_bf<VEC>(a.dy + o);
-            if (a.relu) {
-                const Vec<VEC> y = ld_bf<VEC>(a.y + o);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<VEC> g[U], y[U], x[U];
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) g.v[i] = y.v[i] > 0.0f ? g.v[i] : 0.0f;
-            }
-            const Vec<VEC> x = ld_bf<VEC>(a.x + o);
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            const size_t o = so + (size_t)row * a.C + c0;
+            const bool in = row < row1;
+            g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
+            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+            x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            if (row >= row1) break;
             Vec<VEC> d;
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float xh = (x.v[i] + b.v[i] - mu[i]) * is[i];
-                d.v[i] = k1.v[i] * g.v[i] - k2.v[i] - xh * k3.v[i];
+                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
+                const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
+                d.v[i] = k1.v[i] * gg - k2.v[i] - xh * k3.v[i];
             }
-            st_bf<VEC>(a.out + o, d);
+            st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, d);
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) acc[0][i] += bf2f(f2bf(d.v[i]));
+            for (int i = 0; i < VEC; ++i) acc[0][i] += bfround(d.v[i]);
         }
+        ROW_LOOP_END
     }
     block_colsum<VEC, 1>(acc, red, a.G, a.TR);
-    if (r == 0) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) st_part(&part[(size_t)blockIdx.x * a.C + c0 + i], acc[0][i]);
-    }
-    if (!last_block(a.counter + 1, a.N * a.bpn)) return;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int nc = min(NT, a.C - cb);
-        final_colsum<1>(part, a.C, 0, a.N * a.bpn, a.C, cb, nc, fin, scratch);
-        if (t < nc) {
-            if (a.bias_bf16)
-                static_cast<uint16_t*>(a.dbias)[cb + t] = f2bf((float)fin[t]);
-            else
-                static_cast<float*>(a.dbias)[cb + t] = (float)fin[t];
-        }
-        __syncthreads();
+    float* rows = a.ws + gn_off_dbias(a);
+    const int nb = a.N * a.bpn;
+    store_row<VEC, 1>(rows + (size_t)blockIdx.x * a.C, acc, a.C, c0, r);
+    double* grp = reinterpret_cast<double*>(rows + tree_grp_off(1, nb, a.C));
+    if (!tree_reduce(rows, grp, a.counter + CTR, blockIdx.x, nb, a.C, fin, scratch)) return;
+    for (int c = t; c < a.C; c += NT) {
+        if (a.bias_bf16)
+            static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)fin[c]);
+        else
+            static_cast<float*>(a.dbias)[c] = (float)fin[c];
     }
 }
 
@@ -790,26 +940,49 @@ void set_geo(A& a, const Geo& g) {
     a.rpb = g.rpb;
 }
 
+// host mirrors of the GN workspace offsets
+size_t gn_ws(int N, int bpn, int C) {
+    return align4(tree_ws_floats(N, bpn, 2 * C) + (size_t)N * 3 * C) + 2 * (size_t)N * 2 * C +
+           tree_ws_floats(1, N * bpn, C);
+}
+
+inline int check_vec(int C, const char* what) {
+    if (pick_vec(C) == 1 && C > NT) return fail(-2, (std::string(what) + ": C must be a multiple of 8 or <= 256").c_str());
+    if (2 * C > MAX_KC) return fail(-2, (std::string(what) + ": C must be <= 512").c_str());
+    return 0;
+}
+
+// GN geometry: per-sample workgroups so that all segments' counters fit one counter slot and
+// the whole grid stays <= TARGET_BLOCKS.
+inline Geo gn_geometry(int N, int HW, int C) {
+    int target = std::max(1, TARGET_BLOCKS / N);
+    Geo g = geometry(HW, C, pick_vec(C), target);
+    while (N * (1 + ngroups(g.nblk)) + 1 > CTR && target > 1) {
+        target /= 2;
+        g = geometry(HW, C, pick_vec(C), target);
+    }
+    return g;
+}
+
 }  // namespace
 
 extern "C" {
 
 size_t psfm_netops_ws_floats(int M, int C) {
-    const Geo g = geometry(M, C, pick_vec(C), RED_BLOCKS, MIN_ITERS);
-    return (size_t)g.nblk * 2 * C + 3 * (size_t)C;
+    const Geo g = geometry(M, C, pick_vec(C));
+    return tree_ws_floats(1, g.nblk, 2 * C) + 3 * (size_t)C;
 }
 
 size_t psfm_gn_ws_floats(int N, int HW, int C, int G) {
     (void)G;
-    const Geo g = geometry(HW, C, pick_vec(C), std::max(1, RED_BLOCKS / std::max(N, 1)), MIN_ITERS);
-    return (size_t)N * g.nblk * 2 * C + (size_t)N * 3 * C + (size_t)N * g.nblk * C;
+    return gn_ws(N, gn_geometry(N, HW, C).nblk, C);
 }
 
 int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y, void* stream) {
     if (!x || !bias || !y || M < 1 || C < 1) return fail(-1, "bias_act_fwd: bad arguments");
+    if (int e = check_vec(C, "bias_act_fwd")) return e;
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
-    if (vec == 1 && C > NT) return fail(-2, "bias_act_fwd: C must be a multiple of 8 or <= 256");
     BiasArgs a{};
     a.x = static_cast<const uint16_t*>(x);
     a.bias = bias;
@@ -828,9 +1001,9 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
                       float* ws, int* counter, void* stream) {
     if (!dy || !y || !dx || !dbias || !ws || !counter || M < 1 || C < 1)
         return fail(-1, "bias_act_bwd: bad arguments");
+    if (int e = check_vec(C, "bias_act_bwd")) return e;
     const int vec = pick_vec(C);
-    if (vec == 1 && C > NT) return fail(-2, "bias_act_bwd: C must be a multiple of 8 or <= 256");
-    const Geo g = geometry(M, C, vec, RED_BLOCKS, MIN_ITERS);
+    const Geo g = geometry(M, C, vec);
     BiasArgs a{};
     a.dy = dy;
     a.y = y;
@@ -854,9 +1027,9 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || !counter || M < 1 || C < 1)
         return fail(-1, "bn_act_fwd: bad arguments");
     if ((run_mean == nullptr) != (run_var == nullptr)) return fail(-1, "bn_act_fwd: running stats must pair");
+    if (int e = check_vec(C, "bn_act_fwd")) return e;
     const int vec = pick_vec(C);
-    if (vec == 1 && C > NT) return fail(-2, "bn_act_fwd: C must be a multiple of 8 or <= 256");
-    const Geo g = geometry(M, C, vec, RED_BLOCKS, MIN_ITERS);
+    const Geo g = geometry(M, C, vec);
     BNArgs a{};
     a.x = static_cast<const uint16_t*>(x);
     a.res = static_cast<const uint16_t*>(res);
@@ -884,9 +1057,9 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
     if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
         M < 1 || C < 1 || (relu && !y))
         return fail(-1, "bn_act_bwd: bad arguments");
+    if (int e = check_vec(C, "bn_act_bwd")) return e;
     const int vec = pick_vec(C);
-    if (vec == 1 && C > NT) return fail(-2, "bn_act_bwd: C must be a multiple of 8 or <= 256");
-    const Geo g = geometry(M, C, vec, RED_BLOCKS, MIN_ITERS);
+    const Geo g = geometry(M, C, vec);
     BNArgs a{};
     a.dy = static_cast<const uint16_t*>(dy);
     a.y = static_cast<const uint16_t*>(y);
@@ -911,10 +1084,11 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
 
 static int gn_setup(GNArgs& a, int N, int HW, int C, int G, Geo& g, int& vec) {
     if (N < 1 || HW < 1 || C < 1 || G < 1 || C % G != 0) return fail(-1, "groupnorm: bad shape");
+    if (int e = check_vec(C, "groupnorm")) return e;
     vec = pick_vec(C);
-    if (vec == 1 && C > NT) return fail(-2, "groupnorm: C must be a multiple of 8 or <= 256");
-    if (C > NT && NT % (C / G) != 0) return fail(-2, "groupnorm: channels per group must divide 256");
-    g = geometry(HW, C, vec, std::max(1, RED_BLOCKS / N), MIN_ITERS);
+    g = gn_geometry(N, HW, C);
+    if (N * (1 + ngroups(g.nblk)) + 1 > CTR) return fail(-2, "groupnorm: batch too large for one counter slot");
+    if (ngroups(N * g.nblk) + 1 > CTR) return fail(-2, "groupnorm: grid too large for one counter slot");
     a.N = N, a.HW = HW, a.C = C, a.NG = G, a.bpn = g.nblk;
     set_geo(a, g);
     return 0;

@@ -34,16 +34,22 @@ def _rows(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
+SLOT = 256  # PSFM_NETOPS_COUNTER_INTS (include/psfm_netops.h)
+FWD, BWD = 0, 1  # counter slots: forward kernels | backward kernels (gn_act_bwd: slots 1 and 2)
+
+
 def _counter(module, device):
+    """Arrival counters of the module's fused reductions: 3 slots, zeroed once here and re-armed
+    by the kernels after every launch (graph replays reuse them)."""
     c = getattr(module, "_psfm_counter", None)
     if c is None or c.device != device:
-        c = torch.zeros(4, dtype=torch.int32, device=device)  # [fwd, bwd, bwd2, bwd2'], re-armed by the kernels
+        c = torch.zeros(3 * SLOT, dtype=torch.int32, device=device)
         module._psfm_counter = c
     return c
 
 
-def _i32p(t, i):
-    return ctypes.c_void_p(t.data_ptr() + 4 * i)
+def _slot(t, i):
+    return ctypes.c_void_p(t.data_ptr() + 4 * SLOT * i)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -73,7 +79,7 @@ class _BiasAct(torch.autograd.Function):
         db = torch.empty(C, device=y.device, dtype=ctx.bias_dtype)
         ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=y.device, dtype=torch.float32)
         _hip.check(L.psfm_bias_act_bwd(_hip.ptr(dy), _hip.ptr(y), M, C, ctx.act, _hip.ptr(dx), _hip.ptr(db),
-                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _i32p(ctx.counter, 1),
+                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _slot(ctx.counter, BWD),
                                        _hip.stream(y.device)), "psfm_bias_act_bwd")
         return dx, db, None, None
 
@@ -113,7 +119,7 @@ class _BNAct(torch.autograd.Function):
         _hip.check(L.psfm_bn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(weight), _hip.ptr(bias),
                                      _hip.ptr(running_mean), _hip.ptr(running_var), ctypes.c_float(momentum),
                                      ctypes.c_float(eps), M, C, int(relu), _hip.ptr(y), _hip.ptr(mean),
-                                     _hip.ptr(invstd), _hip.ptr(ws), _i32p(counter, 0), _hip.stream(dev)),
+                                     _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
                    "psfm_bn_act_fwd")
         ctx.save_for_backward(x, y, weight, mean, invstd)
         ctx.relu, ctx.has_res, ctx.counter = relu, residual is not None, counter
@@ -134,7 +140,7 @@ class _BNAct(torch.autograd.Function):
         ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
         _hip.check(L.psfm_bn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(mean),
                                      _hip.ptr(invstd), M, C, int(ctx.relu), _hip.ptr(dx), _hip.ptr(dres),
-                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _i32p(ctx.counter, 1),
+                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _slot(ctx.counter, BWD),
                                      _hip.stream(dev)), "psfm_bn_act_bwd")
         return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None, None
 
@@ -169,7 +175,7 @@ class _GNAct(torch.autograd.Function):
         bf = int(bias.dtype == torch.bfloat16)
         _hip.check(L.psfm_gn_act_fwd(_hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight), _hip.ptr(beta),
                                      ctypes.c_float(eps), N, HW, C, G, int(relu), _hip.ptr(y), _hip.ptr(mean),
-                                     _hip.ptr(invstd), _hip.ptr(ws), _i32p(counter, 0), _hip.stream(dev)),
+                                     _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
                    "psfm_gn_act_fwd")
         ctx.save_for_backward(x, y, bias, weight, mean, invstd)
         ctx.G, ctx.relu, ctx.counter = G, relu, counter
@@ -192,7 +198,7 @@ class _GNAct(torch.autograd.Function):
         _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight),
                                      _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.relu), _hip.ptr(dx),
                                      _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws),
-                                     _i32p(ctx.counter, 2), _hip.stream(dev)), "psfm_gn_act_bwd")
+                                     _slot(ctx.counter, BWD), _hip.stream(dev)), "psfm_gn_act_bwd")
         return dx, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None
 
 

@@ -25,5 +25,19 @@ if len(k1) >= 3:
                  f"kernels/step {(i1 - i0) / n:.1f}")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
         lines.append(f"{v[0] / 1e3 / n:9.1f} us/step  n/step={v[1] / n:6.1f}  {k}")
+    # normalisation / epilogue kernels by launch grid (one line per layer shape)
+    pat = ("k_bn_", "k_gn_", "k_bias_act", "MIOpenBatchNorm", "RowwiseMoments", "ComputeInternalGradients")
+    bygrid = collections.defaultdict(lambda: [0, 0])
+    for r in rows[i0:i1]:
+        name = r["Kernel_Name"]
+        if any(p in name for p in pat):
+            grid = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
+            b = bygrid[(name.split("(")[0][-40:], grid)]
+            b[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            b[1] += 1
+    if bygrid:
+        lines.append("--- normalisation / epilogue kernels by grid (avg us per launch, launches/step) ---")
+        for (k, gsz), v in sorted(bygrid.items(), key=lambda kv: (kv[0][0], -kv[1][0])):
+            lines.append(f"{v[0] / 1e3 / v[1]:8.2f} us  x{v[1] / n:4.1f}  grid={gsz:>8}  {k}")
 open(out, "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:3]))
