@@ -54,6 +54,9 @@ typedef struct psfm_params {
     float min_depth, max_depth;
     float clip_loss;        /* >0: clamp each candidate map at mean+clip*std :249-253 */
     float smooth_w;         /* smooth_loss_weight                                     */
+    int grad_fused;         /* 1 when the forward of this call ran through
+                               psfm_photometric_fwd_grad (its partial sums use that kernel's
+                               unit grid: psfm_finalize / psfm_photometric_grad_finish read it) */
 } psfm_params;
 
 /* Device inputs of one call. `cam` holds one record per (scale, context, batch):
@@ -78,11 +81,14 @@ typedef struct psfm_workspace {
     uint8_t* argmin;     /* [S][B][H][W]            selected candidate per pixel ('min')   */
     float* unwarp;       /* [N][B][H][W]            automask: photometric loss of each
                                                     UN-warped context (scale independent)  */
+    float* sig_part;     /* [S][B][16]              chunk sums of each sigmoid map (the
+                                                    smoothness normaliser, fwd_grad only)  */
 } psfm_workspace;
 
 /* number of floats (and argmin bytes) the workspace of this call needs */
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
-                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp);
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp,
+                          size_t* sig_part);
 
 /* Clip statistics pass (only when clip_loss > 0): per-candidate-map sum / sum of squares
  * (calc_photometric_loss :249-253), then thresholds mean + clip*std (unbiased). */
@@ -121,6 +127,39 @@ int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float
 /* Sum the per-tile dL/dT partials of up to PSFM_MAX_SCALES calls into grad_T [N][B][12]. */
 int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
                           const psfm_workspace* const* ws, float* grad_T, void* stream);
+
+/* Pre-pass of the K12 training step: K0 (automask candidates, skipped with clip_loss > 0 where
+ * psfm_photometric_clip_stats made them) and the per-(scale, image) chunk sums of each sigmoid
+ * map into ws->sig_part (the smoothness normaliser K12 needs).  Must precede
+ * psfm_photometric_fwd_grad on the same stream. */
+int psfm_photometric_prepass(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                             void* stream);
+
+/* K12 — forward AND eager backward in one sweep (training step).  Replaces
+ * psfm_photometric_fwd + psfm_photometric_bwd + psfm_smoothness_bwd when the gradient is
+ * wanted: the gradient is linear in dL/dloss, so it is produced here for dL/dloss = 1 and
+ * scaled by psfm_photometric_grad_finish.  Writes the forward partials (ws->photo_part,
+ * ws->smooth_part; finalize as usual, with p->grad_fused = 1), ws->pose_part (dL/dT for
+ * dL/dloss = 1) and grad_sig[s] (S planes [B,1,H,W], written once: the photometric gradient
+ * plus the per-pixel smoothness gradient).  One kernel; psfm_photometric_prepass first.
+ * N <= 2 (the reference's back+forward context); clip_loss > 0 needs
+ * psfm_photometric_clip_stats first, as for psfm_photometric_fwd.  Not for l1_only calls. */
+int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                              float* const* grad_sig, void* stream);
+
+/* Completes the K12 gradient of one call after psfm_finalize:
+ *   grad_sig[s] = grad_out * (grad_k12[s] + c[s][b]),  c = d/ds of the 1/mean(s) normaliser of
+ *   the smoothness term (utils/depth.py:183-185; a per-image constant, needs finalize's sums).
+ * grad_k12 = the planes psfm_photometric_fwd_grad wrote (read only; grad_sig may alias them).
+ * smooth_stats / grad_out as for psfm_smoothness_bwd. */
+int psfm_photometric_grad_finish(const psfm_params* p, const float* smooth_stats, const float* grad_out,
+                                 const float* const* grad_k12, float* const* grad_sig, void* stream);
+
+/* Pose gradient for the K12 path: grad_T [N][B][12] = grad_out * sum of the per-unit partials
+ * of up to PSFM_MAX_SCALES calls (fixed order, fp64). */
+int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
+                                 const psfm_workspace* const* ws, const float* grad_out,
+                                 float* grad_T, void* stream);
 
 /* Standalone view_synthesis (geometry/camera_utils.py:27-59) for one context:
  * warped[B,3,H,W] = grid_sample(ref, project(reconstruct(depth))).  cam: [B][PSFM_CAMREC]. */

@@ -28,7 +28,7 @@ class Params(ctypes.Structure):
                 ("scale0", c_int), ("n_scales", c_int), ("automask", c_int), ("reduce_op", c_int),
                 ("l1_only", c_int), ("ssim_w", c_float), ("C1", c_float), ("C2", c_float),
                 ("min_depth", c_float), ("max_depth", c_float), ("clip_loss", c_float),
-                ("smooth_w", c_float)]
+                ("smooth_w", c_float), ("grad_fused", c_int)]
 
 
 class Inputs(ctypes.Structure):
@@ -41,7 +41,7 @@ class Workspace(ctypes.Structure):
     """psfm_workspace."""
     _fields_ = [("photo_part", c_void_p), ("smooth_part", c_void_p), ("clip_part", c_void_p),
                 ("clip_thr", c_void_p), ("pose_part", c_void_p), ("argmin", c_void_p),
-                ("unwarp", c_void_p)]
+                ("unwarp", c_void_p), ("sig_part", c_void_p)]
 
 
 _lib = None
@@ -60,7 +60,7 @@ def lib():
     WS, WSP, IN = ctypes.POINTER(Workspace), ctypes.POINTER(ctypes.POINTER(Workspace)), ctypes.POINTER(Inputs)
     sz = ctypes.POINTER(c_size_t)
     sig = {
-        "psfm_workspace_floats": ([P, sz, sz, sz, sz, sz, sz, sz], c_int),
+        "psfm_workspace_floats": ([P, sz, sz, sz, sz, sz, sz, sz, sz], c_int),
         "psfm_photometric_clip_stats": ([P, IN, WS, V], c_int),
         "psfm_photometric_fwd": ([P, IN, WS, V], c_int),
         "psfm_smoothness_fwd": ([P, IN, WS, V], c_int),
@@ -68,6 +68,10 @@ def lib():
         "psfm_photometric_bwd": ([P, IN, WS, V, V, V], c_int),
         "psfm_smoothness_bwd": ([P, IN, V, V, V, V], c_int),
         "psfm_pose_grad_reduce": ([c_int, PP, WSP, V, V], c_int),
+        "psfm_photometric_prepass": ([P, IN, WS, V], c_int),
+        "psfm_photometric_fwd_grad": ([P, IN, WS, V, V], c_int),
+        "psfm_photometric_grad_finish": ([P, V, V, V, V, V], c_int),
+        "psfm_pose_grad_reduce_scaled": ([c_int, PP, WSP, V, V, V], c_int),
         "psfm_view_synthesis_fwd": ([c_int, c_int, c_int, V, V, V, V, V], c_int),
         "psfm_view_synthesis_bwd": ([c_int, c_int, c_int, V, V, V, V, V, V, V, V], c_int),
         "psfm_tiles_per_image": ([c_int, c_int], c_int),
@@ -101,7 +105,8 @@ def lib():
 
 EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photometric_fwd",
             "psfm_smoothness_fwd", "psfm_finalize", "psfm_photometric_bwd", "psfm_smoothness_bwd",
-            "psfm_pose_grad_reduce", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
+            "psfm_pose_grad_reduce", "psfm_photometric_prepass", "psfm_photometric_fwd_grad", "psfm_photometric_grad_finish",
+            "psfm_pose_grad_reduce_scaled", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
             "psfm_tiles_per_image", "psfm_last_error", "psfm_version",
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",

@@ -22,6 +22,7 @@
 
 #include "psfm_common.h"
 #include "psfm_sweep.h"
+#include "psfm_fused.h"
 
 using namespace psfm;
 
@@ -738,6 +739,7 @@ struct PoseRedArgs {
     PoseRedCall c[MAXS];
     int ncalls, N, B;
     float* grad_T;
+    const float* grad_out;  // K12 path: partials are for dL/dloss = 1 (NULL: already scaled)
 };
 
 __global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
@@ -754,7 +756,64 @@ __global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
                 acc += wave_sum_d(part);
             }
         }
-        if (lane == 0) r.grad_T[item] = (float)acc;
+        if (lane == 0) r.grad_T[item] = (float)(r.grad_out ? acc * (double)*r.grad_out : acc);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K12 companions: sigmoid-sum pre-pass (smoothness normaliser) and the gradient finish.
+// ---------------------------------------------------------------------------------------------
+struct SigSumArgs {
+    const float* sig[MAXS];
+    float* part;  // [S][B][SIGCH]
+    int B;
+    uint32_t plane;
+};
+
+__global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
+    __shared__ float red[NWAVE];
+    const int ch = blockIdx.x, b = blockIdx.y, s = blockIdx.z;
+    const uint32_t per = (a.plane + fused::SIGCH - 1) / fused::SIGCH;
+    const uint32_t lo = ch * per, hi = min(a.plane, lo + per);
+    const float* x = pick4(a.sig, s) + (size_t)b * a.plane;
+    float v[1] = {0.0f};
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) v[0] += x[i];
+    block_sum<1>(v, red);
+    if (threadIdx.x == 0) a.part[((size_t)s * a.B + b) * fused::SIGCH + ch] = v[0];
+}
+
+struct GradFinishArgs {
+    const float* gin[MAXS];
+    float* g[MAXS];
+    const float* smooth_stats;  // [n][B][4] = Ax, Ay, m, max(m, 1e-6)   (finalize)
+    const float* grad_out;
+    int B, H, W, scale0, n_scales, has_smooth;
+    float smooth_w;
+};
+
+// g = gout * (g + c[s][b]); c = -(cx Ax + cy Ay) / mc^2 / (H W) where the mean is not clamped
+// (the d/ds of the 1/mean(s) normaliser; same expression as k_smooth_bwd)
+__global__ __launch_bounds__(NT) void k_grad_finish(GradFinishArgs a) {
+    const int b = blockIdx.y, s = blockIdx.z;
+    const uint32_t plane = (uint32_t)(a.H * a.W);
+    float c = 0.0f;
+    if (a.has_smooth) {
+        const int gsi = a.scale0 + s;
+        const float* st = a.smooth_stats + ((size_t)gsi * a.B + b) * 4;
+        const double base = (double)a.smooth_w / ((double)a.n_scales * (double)(1 << gsi));
+        const float cx = (float)(base / ((double)a.B * a.H * (a.W - 1)));
+        const float cy = (float)(base / ((double)a.B * (a.H - 1) * a.W));
+        const float mc = st[3];
+        if (st[2] >= 1e-6f) c = -((cx * st[0] + cy * st[1]) / (mc * mc) / (float)(a.H * a.W));
+    }
+    const float go = *a.grad_out;
+    const float* gi = pick4(a.gin, s) + (size_t)b * plane;
+    float* g = pick4(a.g, s) + (size_t)b * plane;
+    const uint32_t i0 = blockIdx.x * (NT * 4) + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * NT;
+        if (i < plane) g[i] = go * (gi[i] + c);
     }
 }
 
@@ -842,8 +901,17 @@ dim3 tile_grid(const psfm_params* p) { return dim3(tiles_img(p->H, p->W), p->B);
 // partial-sum units per image: the v2 sweep kernels handle every config except the 3-channel
 // L1-only candidates (ssim_loss_weight == 0), which keep the v1 tile kernels.
 bool use_sweep(const psfm_params* p) { return !p->l1_only; }
-int fwd_units(const psfm_params* p) { return use_sweep(p) ? sweep::k1_units(p->H, p->W) : tiles_img(p->H, p->W); }
-int bwd_units(const psfm_params* p) { return use_sweep(p) ? sweep::k2_units(p->H, p->W) : tiles_img(p->H, p->W); }
+// partial-sum units of the clip-statistics pass (always K1 / v1 tiles)
+int stats_units(const psfm_params* p) { return use_sweep(p) ? sweep::k1_units(p->H, p->W) : tiles_img(p->H, p->W); }
+bool fused_ok(const psfm_params* p) { return use_sweep(p) && p->N <= 2; }
+int fwd_units(const psfm_params* p) {
+    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W);
+    return stats_units(p);
+}
+int bwd_units(const psfm_params* p) {
+    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W);
+    return use_sweep(p) ? sweep::k2_units(p->H, p->W) : tiles_img(p->H, p->W);
+}
 
 sweep::SweepArgs sweep_args(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws) {
     sweep::SweepArgs a{};
@@ -896,10 +964,12 @@ extern "C" {
 int psfm_tiles_per_image(int H, int W) { return tiles_img(H, W); }
 
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
-                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp) {
+                          size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp,
+                          size_t* sig_part) {
     if (!p) return fail(-1, "null params");
-    const size_t t = (size_t)std::max(tiles_img(p->H, p->W), std::max(sweep::k1_units(p->H, p->W),
-                                                                         sweep::k2_units(p->H, p->W))) * p->B;
+    const int u = std::max(std::max(tiles_img(p->H, p->W), fused::units(p->H, p->W)),
+                           std::max(sweep::k1_units(p->H, p->W), sweep::k2_units(p->H, p->W)));
+    const size_t t = (size_t)u * p->B;
     const size_t ns = (size_t)n_src(*p);
     if (photo) *photo = (size_t)p->S * t;
     if (smooth) *smooth = (size_t)p->S * t * 4;
@@ -908,6 +978,7 @@ int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, s
     if (pose) *pose = (size_t)p->S * p->N * t * 12;
     if (argmin_bytes) *argmin_bytes = (size_t)p->S * p->B * p->H * p->W;
     if (unwarp) *unwarp = (p->automask && !p->l1_only) ? (size_t)p->N * p->B * p->H * p->W : 0;
+    if (sig_part) *sig_part = (size_t)p->S * p->B * fused::SIGCH;
     return 0;
 }
 
@@ -929,7 +1000,7 @@ int psfm_photometric_clip_stats(const psfm_params* p, const psfm_inputs* in,
         launch_k1<true>(p, sa, st);
     }
     PSFM_LAUNCH_CHECK();
-    ThrArgs t{ws->clip_part, ws->clip_thr, p->S, n_src(*p), p->B * fwd_units(p),
+    ThrArgs t{ws->clip_part, ws->clip_thr, p->S, n_src(*p), p->B * stats_units(p),
               (double)p->B * p->H * p->W * (p->l1_only ? 3.0 : 1.0), p->clip_loss};
     hipLaunchKernelGGL(k_clip_thr, dim3(1), dim3(1024), 0, st, t);
     PSFM_LAUNCH_CHECK();
@@ -1099,6 +1170,107 @@ int psfm_view_synthesis_bwd(int B, int H, int W, const float* ref, const float* 
     r.grad_T = grad_T;
     r.c[0] = PoseRedCall{pose_part, 1, 1, B, tiles_img(H, W)};
     hipLaunchKernelGGL(k_pose_reduce, dim3((B * 12 + 3) / 4), dim3(256), 0, st, r);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_photometric_prepass(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws, void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!fused_ok(p)) return fail(-15, "prepass/fwd_grad need ssim_loss_weight > 0 and N <= 2 (use fwd + bwd)");
+    if (!ws) return fail(-12, "null workspace");
+    if (p->smooth_w > 0.0f && !ws->sig_part) return fail(-12, "null sig_part workspace");
+    if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
+    hipStream_t st = (hipStream_t)stream;
+    if (p->automask && !(p->clip_loss > 0.0f)) launch_k0(p, sweep_args(p, in, ws), st);  // clip: clip_stats did
+    if (p->smooth_w > 0.0f) {
+        SigSumArgs sa{};
+        for (int s = 0; s < p->S; ++s) sa.sig[s] = in->sig[s];
+        sa.part = ws->sig_part;
+        sa.B = p->B;
+        sa.plane = (uint32_t)(p->H * p->W);
+        hipLaunchKernelGGL(k_sig_sum, dim3(fused::SIGCH, p->B, p->S), dim3(NT), 0, st, sa);
+    }
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
+                              float* const* grad_sig, void* stream) {
+    if (int e = validate(p, in)) return e;
+    if (!fused_ok(p)) return fail(-15, "fwd_grad needs ssim_loss_weight > 0 and N <= 2 (use fwd + bwd)");
+    if (!p->grad_fused) return fail(-15, "fwd_grad needs p->grad_fused = 1 (finalize reads its unit grid)");
+    if (!ws || !ws->photo_part || !ws->pose_part) return fail(-12, "null workspace");
+    if (p->smooth_w > 0.0f && (!ws->smooth_part || !ws->sig_part)) return fail(-12, "null smoothness workspace");
+    if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
+    if (p->clip_loss > 0.0f && !ws->clip_thr) return fail(-12, "clip needs clip_thr");
+    if (!grad_sig) return fail(-14, "null grad_sig");
+    fused::Args fa{};
+    fa.p = *p;
+    fa.in = *in;
+    fa.ws = *ws;
+    for (int s = 0; s < p->S; ++s) {
+        if (!grad_sig[s]) return fail(-14, "null grad_sig");
+        fa.grad_sig[s] = grad_sig[s];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(fused::units(p->H, p->W), p->B, p->S);
+    const size_t lds = fused::lds_bytes(p->N);
+    const bool fast = fast_cfg(p, in);
+    if (p->N == 1) {
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false>), grid, dim3(64), lds, st, fa);
+    } else {
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false>), grid, dim3(64), lds, st, fa);
+    }
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_photometric_grad_finish(const psfm_params* p, const float* smooth_stats, const float* grad_out,
+                                 const float* const* grad_k12, float* const* grad_sig, void* stream) {
+    if (!p || !grad_out || !grad_sig || !grad_k12) return fail(-14, "null grad_finish args");
+    if (p->B < 1 || p->H < 2 || p->W < 2 || p->S < 1 || p->S > MAXS) return fail(-2, "bad B/H/W/S");
+    const bool sm = p->smooth_w > 0.0f;
+    if (sm && !smooth_stats) return fail(-14, "null smooth_stats");
+    GradFinishArgs a{};
+    for (int s = 0; s < p->S; ++s) {
+        if (!grad_sig[s] || !grad_k12[s]) return fail(-14, "null grad_sig");
+        a.gin[s] = grad_k12[s];
+        a.g[s] = grad_sig[s];
+    }
+    a.smooth_stats = smooth_stats;
+    a.grad_out = grad_out;
+    a.B = p->B;
+    a.H = p->H;
+    a.W = p->W;
+    a.scale0 = p->scale0;
+    a.n_scales = p->n_scales;
+    a.has_smooth = sm;
+    a.smooth_w = p->smooth_w;
+    const int plane = p->H * p->W;
+    hipLaunchKernelGGL(k_grad_finish, dim3((plane + NT * 4 - 1) / (NT * 4), p->B, p->S), dim3(NT), 0,
+                       (hipStream_t)stream, a);
+    PSFM_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
+                                 const psfm_workspace* const* ws, const float* grad_out,
+                                 float* grad_T, void* stream) {
+    if (ncalls < 1 || ncalls > MAXS || !calls || !ws || !grad_T || !grad_out) return fail(-1, "bad pose reduce args");
+    PoseRedArgs r{};
+    r.ncalls = ncalls;
+    r.N = calls[0]->N;
+    r.B = calls[0]->B;
+    r.grad_T = grad_T;
+    r.grad_out = grad_out;
+    for (int i = 0; i < ncalls; ++i) {
+        if (calls[i]->N != r.N || calls[i]->B != r.B) return fail(-1, "calls disagree on N/B");
+        r.c[i] = PoseRedCall{ws[i]->pose_part, calls[i]->S, calls[i]->N, calls[i]->B, bwd_units(calls[i])};
+    }
+    const int items = r.N * r.B * 12;
+    hipLaunchKernelGGL(k_pose_reduce, dim3((items + 3) / 4), dim3(256), 0, (hipStream_t)stream, r);
     PSFM_LAUNCH_CHECK();
     return 0;
 }

@@ -17,10 +17,20 @@ from ..geometry.camera_utils import scale_intrinsics, pinhole_inverse
 
 # Optional live kernel timing (bench.py roofline): HIP events recorded on the stream the kernels
 # are launched on (torch's current stream, which is also what we pass to the C-ABI).
-KERNEL_TIMING = {"enabled": False, "events": []}
+KERNEL_TIMING = {"enabled": False, "events": [], "record": None}
+
+# Training steps use K12 (forward + eager backward in one sweep, psfm_photometric_fwd_grad);
+# False selects the unfused K1 forward / K2+K3 backward (tests compare the two).
+FUSED_GRAD = True
 
 
-def _run(name, fn, *args):
+def _run(name, fn, *args, keep=()):
+    """One C-ABI launch; `args` end with the stream.  With KERNEL_TIMING["record"] a list, the
+    call (minus its stream) is also recorded for graph replay timing (bench.py); `keep` holds the
+    tensors whose raw pointers the call uses alive for that replay."""
+    rec = KERNEL_TIMING.get("record")
+    if rec is not None:
+        rec.append((name, fn, args[:-1], keep))
     if KERNEL_TIMING["enabled"]:
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -30,6 +40,41 @@ def _run(name, fn, *args):
     else:
         rc = fn(*args)
     _hip.check(rc, name)
+
+
+def graph_replay_times_us(records, device, reps=10, iters=20):
+    """Per-name average duration (us) of recorded C-ABI calls, each name's calls captured `reps`
+    times into one HIP graph and replayed `iters` times between two HIP events on the replay
+    stream (no host launch gaps).  `records` from KERNEL_TIMING["record"]."""
+    names = []
+    for r in records:
+        if r[0] not in names:
+            names.append(r[0])
+    out = {}
+    for name in names:
+        sel = [r for r in records if r[0] == name]
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for _, fn, a, _k in sel:   # warm outside capture
+                _hip.check(fn(*a, _hip.stream(device)), name)
+        torch.cuda.synchronize(device)
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                for _, fn, a, _k in sel:
+                    _hip.check(fn(*a, _hip.stream(device)), name)
+        g.replay()
+        torch.cuda.synchronize(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize(device)
+        out[name] = 1000.0 * e0.elapsed_time(e1) / (iters * reps)
+        del g
+    return out
 
 
 def kernel_times_ms():
@@ -46,7 +91,7 @@ def kernel_times_ms():
 class _Call:
     """One ABI call: scales that share an image size (one call for the full-res case)."""
 
-    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask):
+    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask, fused=False):
         B, _, H, W = image.shape
         p = _hip.Params()
         p.B, p.H, p.W, p.N, p.S = B, H, W, len(contexts), S
@@ -56,6 +101,7 @@ class _Call:
         p.ssim_w, p.C1, p.C2 = cfg["ssim_w"], cfg["C1"], cfg["C2"]
         p.min_depth, p.max_depth = cfg["min_depth"], cfg["max_depth"]
         p.clip_loss, p.smooth_w = cfg["clip"], cfg["smooth_w"]
+        p.grad_fused = int(fused)
         self.params = p
         self.image, self.contexts, self.sigs, self.cam, self.mask = image, contexts, sigs, cam, mask
         inp = _hip.Inputs()
@@ -68,21 +114,26 @@ class _Call:
         inp.mask = mask.data_ptr() if mask is not None else None
         self.inputs = inp
         # workspace (caller-owned; sized by the library)
-        n = [ctypes.c_size_t() for _ in range(7)]
+        n = [ctypes.c_size_t() for _ in range(8)]
         _hip.check(_hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]),
                    "psfm_workspace_floats")
-        sizes = [x.value for x in n[:5]] + [n[6].value]
+        sizes = [x.value for x in n[:5]] + [n[6].value, n[7].value]
         total = sum(sizes)
         self.fbuf = torch.empty(total, device=image.device, dtype=torch.float32)
         self.abuf = torch.empty(max(n[5].value, 1), device=image.device, dtype=torch.uint8)
         ws = _hip.Workspace()
         off = 0
         base = self.fbuf.data_ptr()
-        for name, sz in zip(("photo_part", "smooth_part", "clip_part", "clip_thr", "pose_part", "unwarp"), sizes):
+        for name, sz in zip(("photo_part", "smooth_part", "clip_part", "clip_thr", "pose_part", "unwarp",
+                             "sig_part"), sizes):
             setattr(ws, name, base + 4 * off if sz else None)
             off += sz
         ws.argmin = self.abuf.data_ptr()
         self.ws = ws
+
+
+def _sig_array(ts):
+    return (ctypes.c_void_p * _hip.MAX_SCALES)(*([t.data_ptr() for t in ts] + [None] * (_hip.MAX_SCALES - len(ts))))
 
 
 def _to_size(t, hw, mode):
@@ -115,6 +166,9 @@ class PhotometricLossFn(torch.autograd.Function):
                 s1 += 1
             groups.append((s0, s1))
             s0 = s1
+        # training step: K12 computes the gradient during the forward
+        # (needs_input_grad is False everywhere under no_grad / for data-only inputs)
+        fused = FUSED_GRAD and any(ctx.needs_input_grad[5:]) and N <= 2 and cfg["ssim_w"] > 0.0
         calls = []
         for (a, b) in groups:
             hw = sigs[a].shape[-2:]
@@ -129,25 +183,34 @@ class PhotometricLossFn(torch.autograd.Function):
             im = _to_size(image, hw, "bilinear")
             cx = [_to_size(c, hw, "bilinear") for c in contexts]
             mk = _to_size(mask, hw, "nearest").contiguous() if mask is not None else None
-            calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk))
+            calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk, fused))
 
         L = _hip.lib()
         st = _hip.stream(dev)
         for c in calls:
             if cfg["clip"] > 0.0:
                 _run("clip_stats", L.psfm_photometric_clip_stats, ctypes.byref(c.params),
-                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st)
+                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st, keep=(c,))
+            if fused:
+                c.gsig = [torch.empty_like(t) for t in c.sigs]
+                _run("prepass", L.psfm_photometric_prepass, ctypes.byref(c.params), ctypes.byref(c.inputs),
+                     ctypes.byref(c.ws), st, keep=(c,))
+                _run("K12_photometric_fwd_grad", L.psfm_photometric_fwd_grad, ctypes.byref(c.params),
+                     ctypes.byref(c.inputs), ctypes.byref(c.ws), _sig_array(c.gsig), st, keep=(c,))
+                continue
             _run("K1_photometric_fwd", L.psfm_photometric_fwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
-                 ctypes.byref(c.ws), st)
+                 ctypes.byref(c.ws), st, keep=(c,))
             if cfg["smooth_w"] > 0.0:
                 _run("K3_smoothness_fwd", L.psfm_smoothness_fwd, ctypes.byref(c.params),
-                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st)
+                     ctypes.byref(c.inputs), ctypes.byref(c.ws), st, keep=(c,))
         smooth_stats = torch.empty(cfg["n"] * B * 4, device=dev, dtype=torch.float32)
         out = torch.empty(3, device=dev, dtype=torch.float32)
         pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
         wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
-        _run("finalize", L.psfm_finalize, len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st)
+        _run("finalize", L.psfm_finalize, len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st,
+             keep=(calls, smooth_stats, out))
         ctx.calls, ctx.smooth_stats, ctx.cfg, ctx.n_ctx, ctx.T_shape = calls, smooth_stats, cfg, N, T.shape
+        ctx.fused = fused
         ctx.sig_shapes = [s.shape for s in sigs]
         loss, photo, smooth = out[0:1], out[1].clone(), out[2].clone()
         ctx.mark_non_differentiable(photo, smooth)
@@ -160,23 +223,34 @@ class PhotometricLossFn(torch.autograd.Function):
         gout = (g_loss if g_loss is not None else torch.zeros(1, device=dev)).reshape(1).float().contiguous()
         L = _hip.lib()
         st = _hip.stream(dev)
+        N, B = ctx.n_ctx, calls[0].params.B
+        pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
+        wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
+        gT = torch.empty(N, B, 12, device=dev, dtype=torch.float32)
+        if ctx.fused:  # gradient already computed by K12 for dL/dloss = 1: scale + normaliser term
+            grads = []
+            for c in calls:
+                gsig = [torch.empty_like(g) for g in c.gsig]
+                _run("grad_finish", L.psfm_photometric_grad_finish, ctypes.byref(c.params),
+                     _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), _sig_array(c.gsig), _sig_array(gsig), st,
+                     keep=(c, ctx.smooth_stats, gout, gsig))
+                grads.extend(gsig)
+            _run("pose_grad_reduce", L.psfm_pose_grad_reduce_scaled, len(calls), pp, wp, _hip.ptr(gout),
+                 _hip.ptr(gT), st, keep=(calls, gout, gT))
+            return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
         grads = []
         for c in calls:
             gsig = [torch.empty(sh, device=dev, dtype=torch.float32) for sh in
                     ctx.sig_shapes[c.params.scale0:c.params.scale0 + c.params.S]]
-            arr = (ctypes.c_void_p * _hip.MAX_SCALES)(*([g.data_ptr() for g in gsig] +
-                                                         [None] * (_hip.MAX_SCALES - len(gsig))))
+            arr = _sig_array(gsig)
             _run("K2_photometric_bwd", L.psfm_photometric_bwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
-                 ctypes.byref(c.ws), _hip.ptr(gout), arr, st)
+                 ctypes.byref(c.ws), _hip.ptr(gout), arr, st, keep=(c, gout, gsig))
             if cfg["smooth_w"] > 0.0:
                 _run("K3_smoothness_bwd", L.psfm_smoothness_bwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
-                     _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st)
+                     _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st, keep=(c, ctx.smooth_stats, gout, gsig))
             grads.extend(gsig)
-        N, B = ctx.n_ctx, calls[0].params.B
-        gT = torch.empty(N, B, 12, device=dev, dtype=torch.float32)
-        pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
-        wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
-        _run("pose_grad_reduce", L.psfm_pose_grad_reduce, len(calls), pp, wp, _hip.ptr(gT), st)
+        _run("pose_grad_reduce", L.psfm_pose_grad_reduce, len(calls), pp, wp, _hip.ptr(gT), st,
+             keep=(calls, gT))
         return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
 
 

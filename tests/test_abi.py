@@ -37,7 +37,7 @@ def test_every_declared_symbol_is_exported(hip):
 
 def test_workspace_sizes(hip):
     p = hip.Params(B=4, H=192, W=640, N=2, S=4, scale0=0, n_scales=4, automask=1, reduce_op=0)
-    n = [ctypes.c_size_t() for _ in range(7)]
+    n = [ctypes.c_size_t() for _ in range(8)]
     assert hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]) == 0
     tiles = hip.tiles_per_image(192, 640)
     assert tiles == 10 * 48
@@ -45,6 +45,27 @@ def test_workspace_sizes(hip):
     assert n[4].value >= 4 * 2 * 4 * tiles * 12
     assert n[5].value == 4 * 4 * 192 * 640
     assert n[6].value == 2 * 4 * 192 * 640
+    assert n[7].value == 4 * 4 * 16   # sigmoid chunk sums of the K12 pre-pass
+
+
+def test_fused_path_argument_checks(hip):
+    """psfm_photometric_fwd_grad: K12 needs grad_fused=1, N <= 2 and SSIM candidates"""
+    L = hip.lib()
+    inp, ws = hip.Inputs(), hip.Workspace()
+    p = hip.Params(B=1, H=8, W=8, N=3, S=1, scale0=0, n_scales=1, automask=1, reduce_op=0, ssim_w=0.85,
+                   grad_fused=1)
+    inp.tgt = inp.cam = 1
+    for j in range(3):
+        inp.ctx[j] = 1
+    inp.sig[0] = 1
+    assert L.psfm_photometric_fwd_grad(ctypes.byref(p), ctypes.byref(inp), ctypes.byref(ws), None, None) == -15
+    p.N, p.grad_fused = 2, 0
+    assert L.psfm_photometric_fwd_grad(ctypes.byref(p), ctypes.byref(inp), ctypes.byref(ws), None, None) == -15
+    p.grad_fused = 1
+    assert L.psfm_photometric_fwd_grad(ctypes.byref(p), ctypes.byref(inp), ctypes.byref(ws), None, None) == -12
+    assert b"workspace" in L.psfm_last_error()
+    assert L.psfm_photometric_grad_finish(ctypes.byref(p), None, None, None, None, None) == -14
+    assert L.psfm_pose_grad_reduce_scaled(0, None, None, None, None, None) == -1
 
 
 @pytest.mark.parametrize("field,value,code", [("N", 0, -3), ("N", 5, -3), ("S", 0, -4), ("H", 1, -2),

@@ -1,5 +1,6 @@
-"""GPU parity of the HIP photometric path (K1/K2/K3 via the C-ABI) against the reference's
-golden fixtures and the CPU oracle.
+"""GPU parity of the HIP photometric path against the reference's golden fixtures and the CPU
+oracle — every case runs through BOTH gradient paths: K12 (forward + eager backward in one sweep,
+psfm_photometric_fwd_grad, the training default) and K1 forward / K2+K3 backward.
 
 Tolerances (BASELINE.json north_star: 1e-4 rel fp32):
   * loss / metrics: 1e-4 relative;
@@ -31,6 +32,15 @@ def dev():
     import __graft_entry__
     __graft_entry__.build()
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["k12", "k1k2"], autouse=True)
+def grad_path(request):
+    from packnet_sfm_amd.losses import _hip_photometric as HP
+    old = HP.FUSED_GRAD
+    HP.FUSED_GRAD = request.param == "k12"
+    yield request.param
+    HP.FUSED_GRAD = old
 
 
 def _T(a, dev):
@@ -201,3 +211,47 @@ def test_view_synthesis_matches_reference(dev):
     (warped * wgt.to(dev)).sum().backward()
     assert gu.rel_err(depth.grad.cpu(), d_c.grad) < GRAD_TOL
     assert gu.rel_err(vec.grad.cpu(), v_c.grad) < GRAD_TOL
+
+
+def test_grad_scales_with_upstream_gradient(dev, grad_path):
+    """K12 produces the gradient for dL/dloss = 1; the finish pass applies the real dL/dloss
+    (one rounding at the end: tight).  K2/K3 fold dL/dloss into every pixel's chain, so there
+    the check is the usual gradient tolerance."""
+    z = gu.load_golden("loss_default")
+    a, sa, va = run_hip_case(z, dev)
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    kw = _kw(z)
+    sigs = [_T(z[f"sig{i}"], dev).requires_grad_(True) for i in range(kw["num_scales"])]
+    vec = _T(z["vec"], dev).requires_grad_(True)
+    out = MultiViewPhotometricLoss(**kw)(_T(z["image"], dev), [_T(z[f"ctx{j}"], dev) for j in range(2)], sigs,
+                                         _T(z["K"], dev), _T(z["K"], dev),
+                                         [Pose.from_vec(vec[:, j], "euler") for j in range(2)], mask=_T(z["mask"], dev))
+    (2.5 * out["loss"]).sum().backward(retain_graph=True)
+    def close(a, b):
+        if grad_path == "k12":
+            return torch.allclose(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
+        return gu.grad_check(a.cpu(), b.cpu(), None, GRAD_TOL)[0]
+    for x, y in zip(sigs, sa):
+        assert close(x.grad, 2.5 * y.grad)
+    assert gu.rel_err(vec.grad.cpu(), 2.5 * va.grad.cpu()) < (1e-5 if grad_path == "k12" else GRAD_TOL)
+    g1 = [x.grad.clone() for x in sigs]
+    out["loss"].sum().backward()   # a second backward through the same graph adds 1x more
+    for x, y, g in zip(sigs, sa, g1):
+        assert close(x.grad, g + y.grad)
+
+
+def test_no_grad_forward_matches(dev):
+    """Under no_grad the forward-only K1 path runs; same loss as the training path."""
+    z = gu.load_golden("loss_default")
+    a, _, _ = run_hip_case(z, dev)
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    kw = _kw(z)
+    with torch.no_grad():
+        out = MultiViewPhotometricLoss(**kw)(
+            _T(z["image"], dev), [_T(z[f"ctx{j}"], dev) for j in range(2)],
+            [_T(z[f"sig{i}"], dev) for i in range(kw["num_scales"])], _T(z["K"], dev), _T(z["K"], dev),
+            [Pose.from_vec(_T(z["vec"], dev)[:, j], "euler") for j in range(2)], mask=_T(z["mask"], dev))
+    assert gu.rel_err(out["loss"].cpu(), z["loss"]) < LOSS_TOL
+    assert gu.rel_err(out["loss"].cpu(), a["loss"].detach().cpu()) < 1e-5

@@ -20,6 +20,7 @@ ap.add_argument("--iters", type=int, default=30)
 ap.add_argument("--B", type=int, default=4)
 ap.add_argument("--H", type=int, default=192)
 ap.add_argument("--W", type=int, default=640)
+ap.add_argument("--paths", default="k12,k1k2")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -44,18 +45,18 @@ for lib in (args.lib or [None]):
     if lib:
         _hip.LIB_PATH = lib
         _hip._lib = None
-    for _ in range(3):
-        fn(image, ctx, sigs, K, K, poses)["loss"].sum().backward()
-    torch.cuda.synchronize()
-    HP.KERNEL_TIMING["events"].clear()
-    HP.KERNEL_TIMING["enabled"] = True
-    for _ in range(args.iters):
+    for fused in [p == "k12" for p in args.paths.split(",")]:
+        HP.FUSED_GRAD = fused
+        for _ in range(2):
+            fn(image, ctx, sigs, K, K, poses)["loss"].sum().backward()
+        torch.cuda.synchronize()
+        HP.KERNEL_TIMING["record"] = rec = []
         out = fn(image, ctx, sigs, K, K, poses)
         out["loss"].sum().backward()
-    HP.KERNEL_TIMING["enabled"] = False
-    t = HP.kernel_times_ms()
-    res = {k: round(1000 * v[0] / args.iters, 2) for k, v in t.items()}
-    res["total_us"] = round(sum(res.values()), 2)
-    res["loss"] = float(out["loss"])
-    results[lib or "default"] = res
-    print(lib or "default", json.dumps(res), flush=True)
+        HP.KERNEL_TIMING["record"] = None
+        res = {k: round(v, 2) for k, v in HP.graph_replay_times_us(rec, dev, reps=10, iters=args.iters).items()}
+        res["total_us"] = round(sum(res.values()), 2)
+        res["loss"] = float(out["loss"].detach())
+        tag = (lib or "default") + (" k12" if fused else " k1k2")
+        results[tag] = res
+        print(tag, json.dumps(res), flush=True)
