@@ -37,7 +37,7 @@ for step in "$@"; do
       for ctr in FETCH_SIZE WRITE_SIZE; do
         rm -rf "$OUT/kpmc_$ctr"
         (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/kpmc_$ctr" -o run \
-           -- python3 "$ROOT/tools/kbench.py" --iters 3) > "$OUT/kpmc_$ctr.log" 2>&1; rc=$?
+           -- python3 "$ROOT/tools/kbench.py" --iters 3 --paths k12) > "$OUT/kpmc_$ctr.log" 2>&1; rc=$?
         echo "[kpmc $ctr] rc=$rc"; tail -2 "$OUT/kpmc_$ctr.log"; crash $rc && exit $rc
       done
       python3 "$ROOT/tools/pmc_traffic.py" "$OUT/kpmc_FETCH_SIZE" "$OUT/kpmc_WRITE_SIZE" "$OUT/pmc_traffic.json" 4 > /dev/null; echo "[kpmc] agg rc=$?" ;;

@@ -15,7 +15,8 @@ import json
 import os
 import sys
 
-GROUP = {"k1_forward": "K1_photometric_fwd", "k0_unwarped": "K1_photometric_fwd",
+GROUP = {"k12_fwd_grad": "K12_photometric_fwd_grad", "k0_unwarped": "prepass", "k_sig_sum": "prepass",
+         "k_grad_finish": "grad_finish", "k1_forward": "K1_photometric_fwd",
          "k2_backward": "K2_photometric_bwd", "k_smooth_bwd": "K3_smoothness_bwd"}
 
 
@@ -46,9 +47,12 @@ def main():
         kernels[k[1]] = {"group": k[0], "read_bytes": round(rd), "write_bytes": round(wr),
                          "dispatches_sampled": nf.get(k, 0)}
     total = sum(v["read_bytes"] + v["write_bytes"] for v in kernels.values())
+    dom = {k: v for k, v in kernels.items() if v["group"] == "K12_photometric_fwd_grad"}
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over tools/kbench.py",
            "correction": "read = 2*1024*FETCH_SIZE (gfx950 half-count), write = 1024*WRITE_SIZE",
-           "images_per_launch": imgs, "bytes_per_step": total, "kernels": kernels}
+           "images_per_launch": imgs, "bytes_per_step": total,
+           "dominant_kernel_bytes": sum(v["read_bytes"] + v["write_bytes"] for v in dom.values()) if dom else None,
+           "kernels": kernels}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -7,7 +7,8 @@ import sys
 trace, out = sys.argv[1], sys.argv[2]
 rows = list(csv.DictReader(open(trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-k1 = [i for i, r in enumerate(rows) if "k1_forward" in r["Kernel_Name"]]
+key = "k12_fwd_grad" if any("k12_fwd_grad" in r["Kernel_Name"] for r in rows) else "k1_forward"
+k1 = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
 lines = [f"rows {len(rows)}  k1 launches {len(k1)}"]
 if len(k1) >= 3:
     n = min(len(k1) - 1, 8)  # the last graph replays only (warm-up includes MIOpen find)
