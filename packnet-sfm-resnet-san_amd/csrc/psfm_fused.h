@@ -52,6 +52,12 @@ using sweep::work_item;
 #ifndef PSFM_K12_WAVES
 #define PSFM_K12_WAVES 2
 #endif
+#ifndef PSFM_K12_CAM_RELOAD
+#define PSFM_K12_CAM_RELOAD 1
+#endif
+#ifndef PSFM_K12_DI_B128
+#define PSFM_K12_DI_B128 0
+#endif
 #ifndef PSFM_K12_GT_REG
 #define PSFM_K12_GT_REG 0
 #endif
@@ -82,7 +88,12 @@ __host__ __device__ inline int stripes(int W) { return (W + OW - 1) / OW; }
 __host__ __device__ inline int units(int H, int W) { return stripes(W) * ((H + RB - 1) / RB); }
 // wave-private LDS (each lane touches only its own column: no barriers):
 //   [3 row slots][6 NC] d warp / d(ix, iy) | [12 NC] per-lane dL/d[R|t] accumulators
-__host__ __device__ inline size_t lds_bytes(int NC) { return (size_t)(3 * 6 + 12) * NC * 64 * sizeof(float); }
+// per-lane dL/dT row stride: 12 NC floats padded to 16 NC + ... (28 dwords at NC = 2: the 16
+// lanes of a b128 access start on distinct 4-bank groups -> no bank conflicts)
+__host__ __device__ constexpr int gt_stride(int NC) { return NC == 1 ? 12 : 28; }
+__host__ __device__ inline size_t lds_bytes(int NC) {
+    return ((size_t)3 * 6 * NC * 64 + (size_t)gt_stride(NC) * 64) * sizeof(float);
+}
 
 struct Args {
     psfm_params p;
@@ -220,6 +231,7 @@ struct State {
     float SG0, SG1, SG2, SG3;
     f2 X0[NP][3], X1[NP][3], X2[NP][3], X3[NP][3];
     float sg_next;
+    float un[NC], mv;  // K0 candidates and mask of this step's p-row (loaded before the gathers)
     template <int I> __device__ __forceinline__ float (&Y())[3] {
         if constexpr (I == 0) return Y0; else if constexpr (I == 1) return Y1; else if constexpr (I == 2) return Y2; else return Y3;
     }
@@ -267,7 +279,9 @@ struct K12 {
     __device__ __forceinline__ SweepCams<NC> load_cams() const {
         typedef __attribute__((address_space(4))) const float cfloat;
         uint64_t rp = reinterpret_cast<uint64_t>(camrec);
+#if PSFM_K12_CAM_RELOAD
         asm volatile("" : "+s"(rp));
+#endif
         cfloat* rec = reinterpret_cast<cfloat*>(rp);
         SweepCams<NC> c;
 #pragma unroll
@@ -325,7 +339,7 @@ struct K12 {
         mask = (!FAST && a.in.mask) ? a.in.mask + (size_t)b * plane : nullptr;
         gsig = pick4(a.grad_sig, s) + (size_t)b * plane;
         di = lds;
-        gt = lds + 3 * 6 * NC * 64 + lane * 12 * NC;
+        gt = lds + 3 * 6 * NC * 64 + lane * gt_stride(NC);
         camrec = a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC;
         // per-image mean of the sigmoid map (smoothness normaliser, utils/depth.py:183-185),
         // from the SIGCH chunk sums of the pre-pass, summed in chunk order in fp64 (wave-uniform
@@ -342,6 +356,43 @@ struct K12 {
         }
     }
 
+    // d warp / d(ix, iy) of a row slot: [slot][m][64] (b32, conflict-free) or, with
+    // PSFM_K12_DI_B128, [slot][lane][6 NC] (b128: a quarter of the LDS instructions)
+    __device__ __forceinline__ void di_store(int slot, const float (&dv)[NC * 6]) const {
+#if PSFM_K12_DI_B128
+        float4* d4 = reinterpret_cast<float4*>(di + (slot * 64 + lane) * (NC * 6));
+#pragma unroll
+        for (int i = 0; i < NC * 6 / 4; ++i) d4[i] = make_float4(dv[4 * i], dv[4 * i + 1], dv[4 * i + 2], dv[4 * i + 3]);
+        if ((NC * 6) % 4) {
+            float2* d2 = reinterpret_cast<float2*>(di + (slot * 64 + lane) * (NC * 6) + (NC * 6 / 4) * 4);
+            d2[0] = make_float2(dv[NC * 6 - 2], dv[NC * 6 - 1]);
+        }
+#else
+        float* ds = di + slot * (NC * 6 * 64);
+#pragma unroll
+        for (int m = 0; m < NC * 6; ++m) ds[m * 64 + lane] = dv[m];
+#endif
+    }
+    __device__ __forceinline__ void di_load(int slot, float (&dv)[NC * 6]) const {
+#if PSFM_K12_DI_B128
+        const float4* d4 = reinterpret_cast<const float4*>(di + (slot * 64 + lane) * (NC * 6));
+#pragma unroll
+        for (int i = 0; i < NC * 6 / 4; ++i) {
+            const float4 t = d4[i];
+            dv[4 * i] = t.x; dv[4 * i + 1] = t.y; dv[4 * i + 2] = t.z; dv[4 * i + 3] = t.w;
+        }
+        if ((NC * 6) % 4) {
+            const float2 t = reinterpret_cast<const float2*>(di + (slot * 64 + lane) * (NC * 6) + (NC * 6 / 4) * 4)[0];
+            dv[NC * 6 - 2] = t.x;
+            dv[NC * 6 - 1] = t.y;
+        }
+#else
+        const float* ds = di + slot * (NC * 6 * 64);
+#pragma unroll
+        for (int m = 0; m < NC * 6; ++m) dv[m] = ds[m * 64 + lane];
+#endif
+    }
+
     __device__ __forceinline__ float load_sig(int v) const { return sig[(uint32_t)(reflect1(v, H) * W + colr)]; }
 
     template <int I, bool LOAD, bool PEVAL, bool QEVAL>
@@ -349,6 +400,17 @@ struct K12 {
         constexpr int IA = (I + 1) & 3, IB = (I + 2) & 3, IC = (I + 3) & 3;
         const int v = y0 - 2 + k;
         Pend pd[NC];
+        if (PEVAL) {
+            // the p-row's K0 candidates / mask FIRST: vmcnt retires in issue order, so loads issued
+            // after the gathers would make the p-eval wait for the gathers too
+            const int pv = v - 2;
+            const bool pin = pcol && pv >= 0 && pv < H;
+            const uint32_t ppix = (uint32_t)(pv * W + col);
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+                S.un[j] = (cfg.automask() && pin) ? a.ws.unwarp[((size_t)j * B + b) * plane + ppix] : 0.0f;
+            S.mv = (mask && pin) ? mask[ppix] : 1.0f;
+        }
         if (LOAD) {
             const float sg = S.sg_next;
             S.sg_next = load_sig(v + 1);
@@ -396,7 +458,7 @@ struct K12 {
     template <int I>
     __device__ __forceinline__ void resolve_row(State<NC>& S, int k, const Pend (&pd)[NC]) const {
         {
-            float* ds = di + (k % 3) * (NC * 6 * 64);
+            float dv[NC * 6];
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
                 float x[3], dix[3], diy[3];
@@ -404,10 +466,11 @@ struct K12 {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     S.template X<I>()[j >> 1][c][j & 1] = x[c];
-                    ds[(j * 6 + c) * 64 + lane] = dix[c];
-                    ds[(j * 6 + 3 + c) * 64 + lane] = diy[c];
+                    dv[j * 6 + c] = dix[c];
+                    dv[j * 6 + 3 + c] = diy[c];
                 }
             }
+            di_store(k % 3, dv);
             if (NC & 1) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c) S.template X<I>()[NP - 1][c].y = S.template X<I>()[NP - 1][c].x;
@@ -432,7 +495,6 @@ struct K12 {
         // ---- lane-local phase ----
         const bool pin = pcol && pv >= 0 && pv < H;  // a real pixel
         const bool pout = pin && qcol && pv >= y0 && pv < y0 + RB;  // an output pixel of this wave
-        const uint32_t ppix = (uint32_t)(pv * W + col);
         float G[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) G[j] = 0.0f;
@@ -441,9 +503,9 @@ struct K12 {
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
                 raw[2 * j] = (j & 1) ? cand[j >> 1].y : cand[j >> 1].x;
-                raw[2 * j + 1] = cfg.automask() ? a.ws.unwarp[((size_t)j * B + b) * plane + ppix] : 0.0f;
+                raw[2 * j + 1] = S.un[j];
             }
-            const float mval = mask ? mask[ppix] : 1.0f;
+            const float mval = S.mv;
             float best = INFINITY, sum = 0.0f;
             int arg = 0, kk = 0;
             bool keep[NC];
@@ -545,7 +607,8 @@ struct K12 {
     __device__ __forceinline__ void qeval(State<NC>& S, int qv, int k) const {
         const float h_left = cfg.smooth() ? from_prev(S.h_p) : 0.0f;  // cross-lane
         if (qv >= H || qv >= y0 + RB || !qcol) return;
-        const float* ds = di + (k % 3) * (NC * 6 * 64);
+        float dv[NC * 6];
+        di_load(k % 3, dv);
         const SweepCams<NC> cams = load_cams();
         float d1, inv;
         const float d = dc.warp_depth(S.template SG<IQ>(), d1, inv);
@@ -559,8 +622,8 @@ struct K12 {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float dx = (j & 1) ? S.D0[q][c].y : S.D0[q][c].x;
-                gix += dx * ds[(j * 6 + c) * 64 + lane];
-                giy += dx * ds[(j * 6 + 3 + c) * 64 + lane];
+                gix += dx * dv[j * 6 + c];
+                giy += dx * dv[j * 6 + 3 + c];
             }
             Proj pr;
             project_lifted(cams.T[j], cams.Kr[j], l, cams.wm1, cams.rwm1, cams.hm1, cams.rhm1, pr);
