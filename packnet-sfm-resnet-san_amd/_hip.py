@@ -44,6 +44,12 @@ class Workspace(ctypes.Structure):
                 ("unwarp", c_void_p), ("sig_part", c_void_p)]
 
 
+class MetricsParams(ctypes.Structure):
+    """psfm_metrics_params (include/psfm_metrics.h)."""
+    _fields_ = [("B", c_int), ("H", c_int), ("W", c_int), ("min_depth", c_float), ("max_depth", c_float),
+                ("crop_garg", c_int), ("use_gt_scale", c_int)]
+
+
 _lib = None
 
 
@@ -95,6 +101,9 @@ def lib():
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V, V],
                             c_int),
         "psfm_netops_last_error": ([], ctypes.c_char_p),
+        # include/psfm_metrics.h
+        "psfm_depth_metrics": ([ctypes.POINTER(MetricsParams), V, V, V, V, V], c_int),
+        "psfm_metrics_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -110,7 +119,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_tiles_per_image", "psfm_last_error", "psfm_version",
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
-            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error")
+            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
+            "psfm_depth_metrics", "psfm_metrics_last_error")
 
 
 def check(rc, what):
@@ -119,6 +129,8 @@ def check(rc, what):
             err = lib().psfm_optim_last_error
         elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops")):
             err = lib().psfm_netops_last_error
+        elif what.startswith("psfm_depth_metrics"):
+            err = lib().psfm_metrics_last_error
         else:
             err = lib().psfm_last_error
         raise RuntimeError(f"{what} failed ({rc}): {err().decode()}")

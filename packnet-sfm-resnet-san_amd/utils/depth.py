@@ -53,27 +53,22 @@ def garg_crop_mask(H, W, device=None):
 
 
 def compute_depth_metrics(config, gt, pred, use_gt_scale=True):
-    """[abs_rel, sq_rel, rmse, rmse_log, a1, a2, a3] averaged over the batch.
+    """[abs_rel, sq_rel, rmse, rmse_log, a1, a2, a3] averaged over the batch — utils/depth.py:258-447.
 
-    Batched on the device (one masked reduction per image, medians via torch.median on the
-    valid pixels); same semantics as the reference's per-image loop.
-    """
-    B, _, H, W = gt.shape
+    `scale_depth` (ATen resample / uncrop) then ONE HIP reduction (csrc/psfm_metrics.hip,
+    include/psfm_metrics.h): per image the valid mask, exact lower medians by radix select, median
+    scaling and the seven metrics; batch average with images without valid pixels adding 0.
+    ROCm tensors only (no CPU fallback; the CPU restatement is oracle.depth_metrics)."""
+    from .. import _hip
+    import ctypes
     pred = scale_depth(pred, gt, config.scale_output)
-    crop = garg_crop_mask(H, W, gt.device) if config.crop == "garg" else None
-    acc = torch.zeros(7, dtype=torch.float64, device=gt.device)
-    for g, p in zip(gt[:, 0], pred[:, 0]):
-        valid = (g > config.min_depth) & (g < config.max_depth)
-        if crop is not None:
-            valid = valid & crop
-        if not bool(valid.any()):
-            continue
-        g, p = g[valid], p[valid]
-        if use_gt_scale:
-            p = p * (torch.median(g) / torch.median(p))
-        th = torch.max(g / p, p / g)
-        d = g - p
-        acc += torch.stack([(d.abs() / g).mean(), (d ** 2 / g).mean(), (d ** 2).mean().sqrt(),
-                            ((g.log() - p.log()) ** 2).mean().sqrt(), (th < 1.25).float().mean(),
-                            (th < 1.25 ** 2).float().mean(), (th < 1.25 ** 3).float().mean()]).double()
-    return (acc / B).to(gt.dtype)
+    gt32, pred32 = gt.float().contiguous(), pred.float().contiguous()
+    _hip.require_device(gt32, pred32)
+    B, _, H, W = gt.shape
+    p = _hip.MetricsParams(B=B, H=H, W=W, min_depth=float(config.min_depth), max_depth=float(config.max_depth),
+                           crop_garg=int(config.crop == "garg"), use_gt_scale=int(bool(use_gt_scale)))
+    per = torch.empty(B, 8, device=gt.device, dtype=torch.float32)
+    out = torch.empty(7, device=gt.device, dtype=torch.float32)
+    _hip.check(_hip.lib().psfm_depth_metrics(ctypes.byref(p), _hip.ptr(gt32), _hip.ptr(pred32), _hip.ptr(per),
+                                             _hip.ptr(out), _hip.stream(gt.device)), "psfm_depth_metrics")
+    return out.to(gt.dtype)

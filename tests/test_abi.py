@@ -19,7 +19,7 @@ def hip():
 
 def declared_functions():
     names = set()
-    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h"):
+    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src))
@@ -112,3 +112,20 @@ def test_optim_plan_chunks(hip):
     assert L.psfm_optim_last_error()
     assert L.psfm_grad_pack(None, None, 1, None, None) == -1
     assert L.psfm_adam_step(None, None, 1, None, None, None, ctypes.c_float(1.0), None, None, None, None) == -1
+
+
+def test_depth_metrics_argument_checks(hip):
+    L = hip.lib()
+    p = hip.MetricsParams(B=0, H=4, W=4, min_depth=0.0, max_depth=80.0, crop_garg=1, use_gt_scale=1)
+    assert L.psfm_depth_metrics(ctypes.byref(p), None, None, None, None, None) == -1
+    assert L.psfm_depth_metrics(ctypes.byref(p), 1, 1, 1, 1, None) == -2
+    assert b"B/H/W" in L.psfm_metrics_last_error()
+
+
+def test_depth_metrics_refuses_cpu_tensors(hip):
+    import types
+    import torch
+    from packnet_sfm_amd.utils.depth import compute_depth_metrics
+    cfg = types.SimpleNamespace(min_depth=0.0, max_depth=80.0, crop="garg", scale_output="top-center")
+    with pytest.raises(RuntimeError, match="ROCm"):
+        compute_depth_metrics(cfg, torch.ones(1, 1, 8, 8), torch.ones(1, 1, 8, 8))
