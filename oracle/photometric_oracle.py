@@ -79,9 +79,59 @@ def project_to_grid(X, K, T):
     return torch.stack([xn, yn], -1).view(B, H, W, 2)
 
 
+FLT_EPS = 2.220446049250313e-16  # sys.float_info.epsilon, as the reference clamps with it
+
+
+def fisheye_scale(cam, sw, sh):
+    """Per-scale fisheye intrinsics: centre (ux, uy) scaled as (c + 0.5) s - 0.5; k, s, div kept
+    (losses/multiview_photometric_loss.py:166-186 — the fork does not rescale s / div)."""
+    return {"k": cam["k"], "s": cam["s"], "div": cam["div"],
+            "ux": (cam["ux"] + 0.5) * sw - 0.5, "uy": (cam["uy"] + 0.5) * sh - 0.5}
+
+
+def fisheye_lift(depth, cam):
+    """FisheyeCamera.reconstruct(depth, frame='c') (geometry/camera.py:243-303): r_d from the
+    centred, scaled pixel, theta ~= r_d (the reference's approximation), ray = tan(theta)/r_d."""
+    B, _, H, W = depth.shape
+    v, u = torch.meshgrid(torch.arange(H, dtype=depth.dtype, device=depth.device),
+                          torch.arange(W, dtype=depth.dtype, device=depth.device), indexing="ij")
+    u, v = u.reshape(1, -1), v.reshape(1, -1)
+    xd = (u - cam["ux"].view(B, 1).to(depth.dtype)) / cam["s"].view(B, 1).to(depth.dtype)
+    yd = (v - cam["uy"].view(B, 1).to(depth.dtype)) / cam["div"].view(B, 1).to(depth.dtype)
+    rd = torch.sqrt(xd ** 2 + yd ** 2)
+    r = torch.tan(rd)
+    rds = torch.where(rd < FLT_EPS, torch.full_like(rd, FLT_EPS), rd)
+    d = depth.view(B, -1)
+    return torch.stack([(r / rds) * xd * d, (r / rds) * yd * d, d], 1).view(B, 3, H, W)
+
+
+def fisheye_project_to_grid(X, cam, T):
+    """c = R X + t, then FisheyeCamera.project(c, frame='c') (geometry/camera.py:305-394):
+    theta = atan(r), r_d = k0 + sum_i k_i theta^i, (u, v) = (s, div) (r_d / r) (x, y) + (ux, uy),
+    normalised to [-1, 1] (align_corners)."""
+    B, _, H, W = X.shape
+    Xc = T[:, :3, :3].bmm(X.view(B, 3, -1)) + T[:, :3, 3:]
+    Z = Xc[:, 2].clamp(min=FLT_EPS)
+    xn, yn = Xc[:, 0] / Z, Xc[:, 1] / Z
+    r = torch.sqrt(xn ** 2 + yn ** 2)
+    th = torch.atan(r)
+    k = cam["k"].to(X.dtype)
+    poly = k[:, 0].unsqueeze(1)
+    for i in range(1, 7):
+        poly = poly + k[:, i].unsqueeze(1) * torch.pow(th, i)
+    rs = torch.where(r < FLT_EPS, torch.full_like(r, FLT_EPS), r)
+    u = cam["s"].view(B, 1).to(X.dtype) * ((poly / rs) * xn) + cam["ux"].view(B, 1).to(X.dtype)
+    v = cam["div"].view(B, 1).to(X.dtype) * ((poly / rs) * yn) + cam["uy"].view(B, 1).to(X.dtype)
+    return torch.stack([2 * u / (W - 1) - 1.0, 2 * v / (H - 1) - 1.0], -1).view(B, H, W, 2)
+
+
 def synthesize(ref, depth, K_tgt, K_ref, T):
-    """Inverse warp of `ref` into the target view.  geometry/camera_utils.py:27-59."""
-    grid = project_to_grid(lift(depth, K_tgt), K_ref, T)
+    """Inverse warp of `ref` into the target view.  geometry/camera_utils.py:27-59.  K_* are
+    pinhole [B,3,3] tensors or FisheyeCamera (VADAS) intrinsics dicts."""
+    if isinstance(K_tgt, dict):
+        grid = fisheye_project_to_grid(fisheye_lift(depth, K_tgt), K_ref, T)
+    else:
+        grid = project_to_grid(lift(depth, K_tgt), K_ref, T)
     return F.grid_sample(ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
 
 
@@ -192,7 +242,11 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
         for i in range(n):
             s = inv[i].shape[-1] / float(W)
             depth = 1.0 / inv[i].clamp(min=1e-6)          # utils/depth.py:103-120
-            warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T))
+            if isinstance(K, dict):
+                sh = inv[i].shape[-2] / float(H)
+                warped.append(synthesize(refs[i], depth, fisheye_scale(K, s, sh), fisheye_scale(ref_K, s, sh), T))
+            else:
+                warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T))
         for i, p in enumerate(photo(warped, images)):
             cands[i].append(p)
         if automask_loss:
@@ -272,17 +326,18 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
     out = []
     img = image.double()
     ctx = [c.double() for c in contexts]
-    Kd = K.double()
+    fish = isinstance(K, dict)
+    Kd = {k: v.double() for k, v in K.items()} if fish else K.double()
     mats = [m.double() for m in pose_mats]
     H, W = image.shape[-2:]
     for s in sigs:
         s = s.double()
         depth = 1.0 / (1.0 / (sigmoid_to_depth(s, min_depth, max_depth) + 1e-8)).clamp(min=1e-6)
-        X = lift(depth, Kd)
+        X = fisheye_lift(depth, Kd) if fish else lift(depth, Kd)
         bad = torch.zeros_like(s, dtype=torch.bool)
         cands = []
         for c, T in zip(ctx, mats):
-            g = project_to_grid(X, Kd, T)
+            g = fisheye_project_to_grid(X, Kd, T) if fish else project_to_grid(X, Kd, T)
             ix = (g[..., 0] + 1) / 2 * (W - 1)
             iy = (g[..., 1] + 1) / 2 * (H - 1)
             kink = ((ix - ix.round()).abs() < coord_eps) | ((iy - iy.round()).abs() < coord_eps)

@@ -24,6 +24,15 @@ def kitti_K(B, H, W, dtype=torch.float32):
     return K.unsqueeze(0).repeat(B, 1, 1).contiguous()
 
 
+def vadas_intrinsics(B, H, W, dtype=torch.float32):
+    """FisheyeCamera (VADAS) intrinsics dict for an H x W image (geometry/camera.py:199-222):
+    k = theta -> r_d polynomial (7 coefficients), s / div = x / y scale, (ux, uy) = centre."""
+    k = torch.tensor([0.0, 1.0, 0.0, -0.06, 0.0, 0.004, 0.0], dtype=dtype)
+    return {"k": k.unsqueeze(0).repeat(B, 1).contiguous(),
+            "s": torch.full((B,), 0.42 * W, dtype=dtype), "div": torch.full((B,), 0.40 * W, dtype=dtype),
+            "ux": torch.full((B,), 0.5 * W - 0.3, dtype=dtype), "uy": torch.full((B,), 0.5 * H + 0.2, dtype=dtype)}
+
+
 def smooth_texture(g, B, C, H, W):
     """Smooth image in [0,1]: bilinear-upsampled coarse U[0,1] noise + fine detail."""
     h, w = max(H // 8, 2), max(W // 8, 2)

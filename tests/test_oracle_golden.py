@@ -99,3 +99,40 @@ def test_depth_metrics_match_reference():
     assert gu.rel_err(O.depth_metrics(gt, pred, 0.0, 80.0, "garg", True), z["with_scale"]) < 1e-5
     assert gu.rel_err(O.depth_metrics(gt, pred, 0.0, 80.0, "garg", False), z["no_scale"]) < 1e-5
     assert gu.rel_err(O.depth_metrics(gt, pred, 1e-3, 80.0, "", True), z["no_crop"]) < 1e-5
+
+
+def _intr(z):
+    return {k: T(z[f"intr_{k}"]) for k in ("k", "s", "div", "ux", "uy")}
+
+
+def test_fisheye_geometry_matches_reference():
+    """FisheyeCamera (VADAS) reconstruct / project (geometry/camera.py:243-394) and the fisheye
+    view synthesis, golden from the reference (tools/gen_goldens.py:gen_fisheye)."""
+    z = gu.load_golden("fisheye_small")
+    intr = _intr(z)
+    X = O.fisheye_lift(T(z["depth"]), intr)
+    assert gu.rel_err(X, z["points"]) < 1e-6
+    mat = O.pose_vec_to_mat(T(z["vec"]))
+    grid = O.fisheye_project_to_grid(T(z["points"]), intr, mat)
+    assert gu.rel_err(grid, z["coords"]) < 1e-5
+    warped = O.synthesize(T(z["ref"]), T(z["depth"]), intr, intr, mat)
+    assert gu.rel_err(warped, z["warped"]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["", "_multires"])
+def test_fisheye_loss_matches_reference(tag):
+    z = gu.load_golden("fisheye_small")
+    intr = _intr(z)
+    sigs = [T(z[f"sig{i}{tag}"]).requires_grad_(True) for i in range(4)]
+    vec = T(z[f"pvec{tag}"]).requires_grad_(True)
+    mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+    B, _, H, W = z[f"image{tag}"].shape
+    loss, photo, smooth, _ = O.photometric_loss(T(z[f"image{tag}"]), [T(z[f"ctx0{tag}"]), T(z[f"ctx1{tag}"])], sigs,
+                                                intr, intr, mats, mask=torch.ones(B, 1, H, W))
+    loss.sum().backward()
+    assert gu.rel_err(loss.detach(), z[f"loss{tag}"]) < TOL
+    assert gu.rel_err(photo.detach(), z[f"photometric_loss{tag}"]) < TOL
+    assert gu.rel_err(smooth.detach(), z[f"smoothness_loss{tag}"]) < TOL
+    for i in range(4):
+        assert gu.rel_err(sigs[i].grad, z[f"grad_sig{i}{tag}"]) < 1e-3, i
+    assert gu.rel_err(vec.grad, z[f"grad_vec{tag}"]) < 1e-3

@@ -91,6 +91,51 @@ class HarnessLoss(mpl.MultiViewPhotometricLoss):
         return super().reduce_photometric_loss(photometric_losses)
 
 
+class _FisheyeTgt:
+    """Target fisheye camera for the reference's view_synthesis: reconstruct in the camera frame
+    (identity pose).  The fork's FisheyeCamera.reconstruct/project(frame='w') apply a Pose to a
+    [B,3,N] tensor, which Pose.transform_points rejects: the harness applies the
+    reference's own Pose to the 4-D point map instead and calls the reference's frame='c' math."""
+
+    def __init__(self, cam):
+        self.cam = cam
+
+    def reconstruct(self, depth, frame="w"):
+        return self.cam.reconstruct(depth, frame="c")
+
+
+class _FisheyeRef:
+    def __init__(self, cam, pose):
+        self.cam, self.pose = cam, pose
+
+    def project(self, X, frame="w"):
+        return self.cam.project(self.pose @ X, frame="c")
+
+
+class HarnessFisheyeLoss(HarnessLoss):
+    """The fork's own fisheye warp_ref_image (:131-195: per-scale centre (c + 0.5) s - 0.5, k / s /
+    div unchanged, FisheyeCamera per scale) with the §0.3c / §0.3d workarounds above."""
+
+    def warp_ref_image(self, inv_depths, ref_image, intrinsics, ref_intrinsics, pose, image_size=None):
+        from packnet_sfm.geometry.camera import FisheyeCamera
+        B, _, H, W = ref_image.shape
+        warped = []
+        depths = [inv2depth(inv_depths[i]) for i in range(self.n)]
+        ref_images = match_scales(ref_image, inv_depths, self.n)
+        for i in range(self.n):
+            _, _, DH, DW = inv_depths[i].shape
+            sw, sh = DW / float(W), DH / float(H)
+
+            def scaled(c):
+                return {"k": c["k"].clone(), "s": c["s"].clone(), "div": c["div"].clone(),
+                        "ux": (c["ux"].clone() + 0.5) * sw - 0.5, "uy": (c["uy"].clone() + 0.5) * sh - 0.5}
+            cam = FisheyeCamera(intrinsics=scaled(intrinsics), image_size=(DH, DW))
+            ref_cam = FisheyeCamera(intrinsics=scaled(ref_intrinsics), image_size=(DH, DW))
+            warped.append(view_synthesis(ref_images[i], depths[i], _FisheyeRef(ref_cam, pose), _FisheyeTgt(cam),
+                                         padding_mode=self.padding_mode))
+        return warped
+
+
 def np32(t):
     return t.detach().cpu().numpy().astype(np.float32)
 
@@ -274,6 +319,48 @@ def gen_step_packnet():
     print(f"  step_packnet_tiny: loss={float(res['loss'][0]):.6f}")
 
 
+def gen_fisheye():
+    """FisheyeCamera (VADAS) geometry + the photometric loss on fisheye cameras (24x80, B=2)."""
+    from packnet_sfm.geometry.camera import FisheyeCamera
+    g = torch.Generator().manual_seed(41)
+    B, H, W = 2, 24, 80
+    intr = gu.vadas_intrinsics(B, H, W)
+    vec = gu.pose_vecs(g, B, 1)[:, 0] * 0.5
+    depth = 2.0 + 28.0 * torch.rand(B, 1, H, W, generator=g)
+    ref = gu.smooth_texture(g, B, 3, H, W)
+    pose = Pose.from_vec(vec, "euler")
+    cam = FisheyeCamera(intrinsics=intr, image_size=(H, W))
+    Xc = cam.reconstruct(depth, frame="c")
+    coords = FisheyeCamera(intrinsics=intr, image_size=(H, W)).project(pose @ Xc, frame="c")
+    warped = view_synthesis(ref, depth, _FisheyeRef(FisheyeCamera(intrinsics=intr, image_size=(H, W)), pose),
+                            _FisheyeTgt(cam), padding_mode="zeros")
+    res = dict(vec=np32(vec), depth=np32(depth), ref=np32(ref), points=np32(Xc), coords=np32(coords),
+               warped=np32(warped), **{f"intr_{k}": np32(v) for k, v in intr.items()})
+    # loss: full-res 4 scales and a multi-resolution case, with gradients
+    for tag, multires in (("", False), ("_multires", True)):
+        gl = torch.Generator().manual_seed(43 + int(multires))
+        image = gu.smooth_texture(gl, B, 3, H, W)
+        ctx = [gu.smooth_texture(gl, B, 3, H, W) for _ in range(2)]
+        pv = gu.pose_vecs(gl, B, 2) * 0.5
+        sig = [gu.sigmoid_maps(gl, B, H >> (i if multires else 0), W >> (i if multires else 0)) for i in range(4)]
+        sig_p = [t.clone().requires_grad_(True) for t in sig]
+        pv_p = pv.clone().requires_grad_(True)
+        fn = HarnessFisheyeLoss(**BASE_KW)
+        out = fn(image, ctx, sig_p, intr, intr, [Pose.from_vec(pv_p[:, j], "euler") for j in range(2)],
+                 progress=0.0, mask=torch.ones(B, 1, H, W))
+        out["loss"].sum().backward()
+        res.update({f"image{tag}": np32(image), f"ctx0{tag}": np32(ctx[0]), f"ctx1{tag}": np32(ctx[1]),
+                    f"pvec{tag}": np32(pv), f"loss{tag}": np32(out["loss"]),
+                    f"photometric_loss{tag}": np32(out["metrics"]["photometric_loss"]),
+                    f"smoothness_loss{tag}": np32(out["metrics"]["smoothness_loss"]),
+                    f"grad_vec{tag}": np32(pv_p.grad)})
+        for i in range(4):
+            res[f"sig{i}{tag}"] = np32(sig[i])
+            res[f"grad_sig{i}{tag}"] = np32(sig_p[i].grad)
+        print(f"  fisheye{tag}: loss={float(out['loss']):.6f}")
+    np.savez_compressed(os.path.join(OUT, "fisheye_small.npz"), **res)
+
+
 def gen_depth_metrics():
     g = torch.Generator().manual_seed(31)
     B, H, W = 2, 192, 640
@@ -301,11 +388,11 @@ if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     import contextlib
     import io
-    which = sys.argv[1:] or ["geom", "ssim", "losses", "kitti", "metrics", "step"]
+    which = sys.argv[1:] or ["geom", "ssim", "losses", "kitti", "metrics", "step", "fisheye"]
     for w in which:
         print(f"[gen] {w}")
         quiet = io.StringIO()
         with contextlib.redirect_stdout(quiet) if w == "metrics" else contextlib.nullcontext():
             {"geom": gen_geom, "ssim": gen_ssim, "losses": gen_losses, "kitti": gen_kitti_1img,
-             "metrics": gen_depth_metrics, "step": gen_step_packnet}[w]()
+             "metrics": gen_depth_metrics, "step": gen_step_packnet, "fisheye": gen_fisheye}[w]()
     print("done")
