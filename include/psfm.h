@@ -36,6 +36,9 @@ extern "C" {
 #define PSFM_CAMREC 32     /* floats per camera record: Kinv[9] | Kref[9] | T[12] | pad[2] */
 
 enum psfm_reduce_op { PSFM_REDUCE_MIN = 0, PSFM_REDUCE_MEAN = 1 };
+/* camera model of a call (psfm_params.cam_model): pinhole K (geometry/camera.py:15-190) or the
+ * fork's fisheye VADAS model (geometry/camera.py:194-394, dict intrinsics k[7], s, div, ux, uy) */
+enum psfm_cam_model { PSFM_CAM_PINHOLE = 0, PSFM_CAM_FISHEYE = 1 };
 
 /* Hyper-parameters of one photometric call: MultiViewPhotometricLoss.__init__ :92-118.
  * One call processes `S` scales that share the image size H x W (the reference's
@@ -57,12 +60,16 @@ typedef struct psfm_params {
     int grad_fused;         /* 1 when the forward of this call ran through
                                psfm_photometric_fwd_grad (its partial sums use that kernel's
                                unit grid: psfm_finalize / psfm_photometric_grad_finish read it) */
+    int cam_model;          /* psfm_cam_model; fisheye: K1 / K12 paths only, N <= 2          */
 } psfm_params;
 
 /* Device inputs of one call. `cam` holds one record per (scale, context, batch):
- *   cam[((s*N + j)*B + b)*PSFM_CAMREC + ...] = Kinv(3x3, row-major) of the target camera
- *   at that scale (camera.py:72-81), Kref(3x3) of the context camera (scaled,
- *   camera_utils.py:16-22), T = [R|t] (3x4) target->context (pose.py:39-46). */
+ *   cam[((s*N + j)*B + b)*PSFM_CAMREC + ...] =
+ *   pinhole: [0..8] Kinv(3x3, row-major) of the target camera at that scale (camera.py:72-81),
+ *            [9..17] Kref(3x3) of the context camera (scaled, camera_utils.py:16-22),
+ *   fisheye: [0..3] target s, div, ux, uy; [4..10] context k0..k6; [11..14] context s, div,
+ *            ux, uy (centres scaled per scale as (c + 0.5) s - 0.5, :166-186),
+ *   both:    [18..29] T = [R|t] (3x4) target->context (pose.py:39-46). */
 typedef struct psfm_inputs {
     const float* tgt;                     /* [B,3,H,W] target image at this size           */
     const float* ctx[PSFM_MAX_CTX];       /* N x [B,3,H,W] context images at this size     */

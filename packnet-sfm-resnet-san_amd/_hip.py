@@ -18,6 +18,7 @@ MAX_CTX = 4
 MAX_SCALES = 4
 CAMREC = 32
 REDUCE_MIN, REDUCE_MEAN = 0, 1
+CAM_PINHOLE, CAM_FISHEYE = 0, 1
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
@@ -28,7 +29,7 @@ class Params(ctypes.Structure):
                 ("scale0", c_int), ("n_scales", c_int), ("automask", c_int), ("reduce_op", c_int),
                 ("l1_only", c_int), ("ssim_w", c_float), ("C1", c_float), ("C2", c_float),
                 ("min_depth", c_float), ("max_depth", c_float), ("clip_loss", c_float),
-                ("smooth_w", c_float), ("grad_fused", c_int)]
+                ("smooth_w", c_float), ("grad_fused", c_int), ("cam_model", c_int)]
 
 
 class Inputs(ctypes.Structure):

@@ -29,6 +29,7 @@
 // Reference: losses/multiview_photometric_loss.py:15-54, :199-297, :301-327,
 // utils/depth.py:146-198, geometry/camera.py:111-190, geometry/camera_utils.py:27-59.
 #pragma once
+#include "psfm_camera.h"
 #include "psfm_sweep.h"
 
 namespace psfm {
@@ -43,7 +44,6 @@ using sweep::hsum3a;
 using sweep::hsum3x3;
 using sweep::pick4;
 using sweep::sgnf;
-using sweep::SweepCams;
 using sweep::target_win;
 using sweep::TWin;
 using sweep::wave_sum64;
@@ -149,25 +149,9 @@ __device__ __forceinline__ void resolve(const Pend& g, float v[3], float dix[3],
 
 // Adjoint of project_lifted for one context: (gix, giy) -> dL/d(warp depth), dL/dT += ...
 // (same arithmetic as psfm::project_grad)
-// Adjoint of project_lifted for one context: (gix, giy) -> dL/d(warp depth) (returned) and
-// gc = dL/dc (c = R X + t), from which dL/dT = gc (X, 1)^T (same arithmetic as psfm::project_grad)
-__device__ __forceinline__ float project_grad_j(const float (&T)[12], const float (&Kr)[9], const Proj& r,
-                                                float gix, float giy, float (&gc)[3]) {
-    const float iz = r.iz;
-    const float gp0 = gix * iz;
-    const float gp1 = giy * iz;
-    const float gp2 = (r.p2 >= 1e-5f) ? -(gix * r.p0 + giy * r.p1) * (iz * iz) : 0.0f;
-    gc[0] = Kr[0] * gp0 + Kr[3] * gp1 + Kr[6] * gp2;
-    gc[1] = Kr[1] * gp0 + Kr[4] * gp1 + Kr[7] * gp2;
-    gc[2] = Kr[2] * gp0 + Kr[5] * gp1 + Kr[8] * gp2;
-    const float gX0 = T[0] * gc[0] + T[4] * gc[1] + T[8] * gc[2];
-    const float gX1 = T[1] * gc[0] + T[5] * gc[1] + T[9] * gc[2];
-    const float gX2 = T[2] * gc[0] + T[6] * gc[1] + T[10] * gc[2];
-    return gX0 * r.xn0 + gX1 * r.xn1 + gX2 * r.xn2;
-}
-
 // dL/dT += gc (X, 1)^T into 12 accumulators (registers, or a lane-private LDS row)
-__device__ __forceinline__ void acc_gT(float* g, const float (&gc)[3], const Proj& r) {
+template <typename P>
+__device__ __forceinline__ void acc_gT(float* g, const float (&gc)[3], const P& r) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         g[4 * i + 0] += gc[i] * r.X0;
@@ -252,8 +236,9 @@ struct State {
 #endif
 };
 
-template <int NC, bool FAST>
+template <int NC, bool FAST, int MODEL>
 struct K12 {
+    using CM = Cams<NC, MODEL>;
     static constexpr int NP = (NC + 1) / 2;
     const Args& a;
     const psfm_params& p;
@@ -276,27 +261,13 @@ struct K12 {
     // The 51 camera scalars are re-loaded at each use (s_load through the constant address
     // space: scalar cache, no VGPRs) instead of being held in SGPRs for the whole sweep; the
     // laundered pointer stops the compiler from keeping them live across the SSIM phase.
-    __device__ __forceinline__ SweepCams<NC> load_cams() const {
-        typedef __attribute__((address_space(4))) const float cfloat;
+    __device__ __forceinline__ CM load_cams() const {
         uint64_t rp = reinterpret_cast<uint64_t>(camrec);
 #if PSFM_K12_CAM_RELOAD
         asm volatile("" : "+s"(rp));
 #endif
-        cfloat* rec = reinterpret_cast<cfloat*>(rp);
-        SweepCams<NC> c;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) c.Ki[i] = rec[i];
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-#pragma unroll
-            for (int i = 0; i < 9; ++i) c.Kr[j][i] = rec[(size_t)j * B * PSFM_CAMREC + 9 + i];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) c.T[j][i] = rec[(size_t)j * B * PSFM_CAMREC + 18 + i];
-        }
-        c.wm1 = (float)(W - 1);
-        c.hm1 = (float)(H - 1);
-        c.rwm1 = rcp_nr(c.wm1);
-        c.rhm1 = rcp_nr(c.hm1);
+        CM c;
+        c.load(reinterpret_cast<cfloat*>(rp), B, H, W);
         return c;
     }
 
@@ -419,14 +390,14 @@ struct K12 {
             const uint32_t pix = (uint32_t)(r * W + colr);
 #pragma unroll
             for (int c = 0; c < 3; ++c) S.template Y<I>()[c] = tgt[c * plane + pix];
-            const SweepCams<NC> cams = load_cams();
+            const CM cams = load_cams();
             float d1, inv;
             const float d = dc.warp_depth(sg, d1, inv);
-            const Lift l = lift(cams.Ki, (float)colr, (float)r, d);
+            const Lift l = cams.lift((float)colr, (float)r, d);
 #pragma unroll
             for (int j = 0; j < NC; ++j) {
-                Proj pr;
-                project_lifted(cams.T[j], cams.Kr[j], l, cams.wm1, cams.rwm1, cams.hm1, cams.rhm1, pr);
+                typename CM::P pr;
+                cams.project(j, l, pr);
                 gather(ctx[j], pb, pr.ix, pr.iy, H, W, pd[j]);
             }
         }
@@ -609,11 +580,11 @@ struct K12 {
         if (qv >= H || qv >= y0 + RB || !qcol) return;
         float dv[NC * 6];
         di_load(k % 3, dv);
-        const SweepCams<NC> cams = load_cams();
+        const CM cams = load_cams();
         float d1, inv;
         const float d = dc.warp_depth(S.template SG<IQ>(), d1, inv);
         const float dw = dc.dwarp_ds(d, d1, inv);
-        const Lift l = lift(cams.Ki, (float)col, (float)qv, d);
+        const Lift l = cams.lift((float)col, (float)qv, d);
         float gs = 0.0f;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
@@ -625,10 +596,10 @@ struct K12 {
                 gix += dx * dv[j * 6 + c];
                 giy += dx * dv[j * 6 + 3 + c];
             }
-            Proj pr;
-            project_lifted(cams.T[j], cams.Kr[j], l, cams.wm1, cams.rwm1, cams.hm1, cams.rhm1, pr);
+            typename CM::P pr;
+            cams.project(j, l, pr);
             float gc[3];
-            gs += project_grad_j(cams.T[j], cams.Kr[j], pr, gix, giy, gc) * dw;
+            gs += cams.grad(j, pr, gix, giy, gc) * dw;
 #if PSFM_K12_GT_REG
             acc_gT(S.gT[j], gc, pr);
 #else
@@ -651,10 +622,10 @@ struct K12 {
     }
 };
 
-template <int NC, bool FAST>
+template <int NC, bool FAST, int MODEL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSFM_K12_WAVES))) void k12_fwd_grad(Args a) {
     extern __shared__ __attribute__((aligned(16))) float k12_lds[];
-    const K12<NC, FAST> K(a, k12_lds);
+    const K12<NC, FAST, MODEL> K(a, k12_lds);
     constexpr int NP = (NC + 1) / 2;
     State<NC> S;
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;

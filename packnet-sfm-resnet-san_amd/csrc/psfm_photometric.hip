@@ -893,6 +893,9 @@ int validate(const psfm_params* p, const psfm_inputs* in) {
     for (int s = 0; s < p->S; ++s)
         if (!in->sig[s]) return fail(-10, "null sigmoid pointer");
     if ((long long)p->B * p->H * p->W > (1LL << 31)) return fail(-11, "image too large");
+    if (p->cam_model != PSFM_CAM_PINHOLE && p->cam_model != PSFM_CAM_FISHEYE) return fail(-16, "unknown cam_model");
+    if (p->cam_model == PSFM_CAM_FISHEYE && (p->N > 2 || p->l1_only))
+        return fail(-16, "fisheye calls: N <= 2 and SSIM candidates (ssim_loss_weight > 0)");
     return 0;
 }
 
@@ -941,11 +944,17 @@ bool fast_cfg(const psfm_params* p, const psfm_inputs* in) {
 template <bool STATS, bool FAST>
 void launch_k1_t(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) {
     const dim3 grid(sweep::k1_units(p->H, p->W), p->B, p->S);
+    constexpr int PIN = PSFM_CAM_PINHOLE, FISH = PSFM_CAM_FISHEYE;
+    if (p->cam_model == FISH) {  // N <= 2 (validated)
+        if (p->N == 1) hipLaunchKernelGGL((sweep::k1_forward<1, STATS, FAST, FISH>), grid, dim3(64), 0, st, a);
+        else hipLaunchKernelGGL((sweep::k1_forward<2, STATS, FAST, FISH>), grid, dim3(64), 0, st, a);
+        return;
+    }
     switch (p->N) {
-        case 1: hipLaunchKernelGGL((sweep::k1_forward<1, STATS, FAST>), grid, dim3(64), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((sweep::k1_forward<2, STATS, FAST>), grid, dim3(64), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((sweep::k1_forward<3, STATS, FAST>), grid, dim3(64), 0, st, a); break;
-        default: hipLaunchKernelGGL((sweep::k1_forward<4, STATS, FAST>), grid, dim3(64), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((sweep::k1_forward<1, STATS, FAST, PIN>), grid, dim3(64), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((sweep::k1_forward<2, STATS, FAST, PIN>), grid, dim3(64), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((sweep::k1_forward<3, STATS, FAST, PIN>), grid, dim3(64), 0, st, a); break;
+        default: hipLaunchKernelGGL((sweep::k1_forward<4, STATS, FAST, PIN>), grid, dim3(64), 0, st, a); break;
     }
 }
 
@@ -1083,6 +1092,7 @@ int psfm_finalize(int ncalls, const psfm_params* const* calls, const psfm_worksp
 int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm_workspace* ws,
                          const float* grad_out, float* const* grad_sig, void* stream) {
     if (int e = validate(p, in)) return e;
+    if (p->cam_model != PSFM_CAM_PINHOLE) return fail(-16, "K2 backward is pinhole-only: use psfm_photometric_fwd_grad");
     if (!ws || !ws->pose_part || (p->reduce_op == PSFM_REDUCE_MIN && !ws->argmin))
         return fail(-12, "null workspace");
     if (!grad_out || !grad_sig) return fail(-14, "null grad buffers");
@@ -1216,12 +1226,21 @@ int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const
     const dim3 grid(fused::units(p->H, p->W), p->B, p->S);
     const size_t lds = fused::lds_bytes(p->N);
     const bool fast = fast_cfg(p, in);
-    if (p->N == 1) {
-        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true>), grid, dim3(64), lds, st, fa);
-        else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false>), grid, dim3(64), lds, st, fa);
+    constexpr int PIN = PSFM_CAM_PINHOLE, FISH = PSFM_CAM_FISHEYE;
+    if (p->cam_model == FISH) {
+        if (p->N == 1) {
+            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, FISH>), grid, dim3(64), lds, st, fa);
+            else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, FISH>), grid, dim3(64), lds, st, fa);
+        } else {
+            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, FISH>), grid, dim3(64), lds, st, fa);
+            else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, FISH>), grid, dim3(64), lds, st, fa);
+        }
+    } else if (p->N == 1) {
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, PIN>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, PIN>), grid, dim3(64), lds, st, fa);
     } else {
-        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true>), grid, dim3(64), lds, st, fa);
-        else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false>), grid, dim3(64), lds, st, fa);
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, PIN>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, PIN>), grid, dim3(64), lds, st, fa);
     }
     PSFM_LAUNCH_CHECK();
     return 0;

@@ -21,6 +21,7 @@
 #pragma once
 #include <type_traits>
 
+#include "psfm_camera.h"
 #include "psfm_common.h"
 
 namespace psfm {
@@ -352,34 +353,7 @@ struct K1State {
     float st[2 * NC][2];
 };
 
-// Wave-uniform geometry of one (scale, batch): K^-1 of the target (shared by all contexts),
-// [R|t] and K_ref per context, and the normalisation constants.
-template <int NC>
-struct SweepCams {
-    float Ki[9];
-    float T[NC][12];
-    float Kr[NC][9];
-    float wm1, rwm1, hm1, rhm1;
-    __device__ __forceinline__ void load(const float* __restrict__ rec0, int B, int H, int W) {
-        // rec0 = record of (s, context 0, b); context j is j*B records further
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Ki[i] = sgpr(rec0[i]);
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const float* r = rec0 + (size_t)j * B * PSFM_CAMREC;
-#pragma unroll
-            for (int i = 0; i < 9; ++i) Kr[j][i] = sgpr(r[9 + i]);
-#pragma unroll
-            for (int i = 0; i < 12; ++i) T[j][i] = sgpr(r[18 + i]);
-        }
-        wm1 = (float)(W - 1);
-        hm1 = (float)(H - 1);
-        rwm1 = rcp_nr(wm1);
-        rhm1 = rcp_nr(hm1);
-    }
-};
-
-template <int NC, bool STATS, bool FAST>
+template <int NC, bool STATS, bool FAST, int MODEL>
 struct K1 {
     static constexpr int NP = (NC + 1) / 2;
     const SweepArgs& a;
@@ -394,7 +368,7 @@ struct K1 {
     const float* sig;
     const float* ctx[NC];
     const float* thr;
-    SweepCams<NC> cams;
+    Cams<NC, MODEL> cams;
 
     __device__ __forceinline__ K1(const SweepArgs& a_) : a(a_), p(a_.p), cfg{a_.p} {
         H = p.H;
@@ -416,7 +390,7 @@ struct K1 {
         sig = pick4(a.in.sig, s) + (size_t)b * plane;
 #pragma unroll
         for (int j = 0; j < NC; ++j) ctx[j] = pick4(a.in.ctx, j) + (size_t)b * 3 * plane;
-        cams.load(a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC, B, H, W);
+        cams.load(as_const(a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC), B, H, W);
         thr = (cfg.clip() && !STATS) ? a.ws.clip_thr + (size_t)s * (cfg.automask() ? 2 * NC : NC) : nullptr;
     }
 
@@ -432,11 +406,11 @@ struct K1 {
         for (int c = 0; c < 3; ++c) y[c] = tgt[c * plane + pix];
         float d1, inv;
         const float d = dc.warp_depth(sg, d1, inv);
-        const Lift l = lift(cams.Ki, (float)colr, (float)r, d);
+        const Lift l = cams.lift((float)colr, (float)r, d);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            Proj pr;
-            project_lifted(cams.T[j], cams.Kr[j], l, cams.wm1, cams.rwm1, cams.hm1, cams.rhm1, pr);
+            typename Cams<NC, MODEL>::P pr;
+            cams.project(j, l, pr);
             float w[3];
             bilinear3(ctx[j], H, W, pr.ix, pr.iy, w);
 #pragma unroll
@@ -547,10 +521,10 @@ struct K1 {
     }
 };
 
-template <int NC, bool STATS, bool FAST>
+template <int NC, bool STATS, bool FAST, int MODEL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k1_forward(SweepArgs a) {
     static_assert((K1RB - 1) % 4 == 0, "K1 band height must be 4m+1 (4-slot pipeline)");
-    K1<NC, STATS, FAST> K(a);
+    K1<NC, STATS, FAST, MODEL> K(a);
     K1State<NC> S;
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;
 #pragma unroll

@@ -91,7 +91,7 @@ def kernel_times_ms():
 class _Call:
     """One ABI call: scales that share an image size (one call for the full-res case)."""
 
-    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask, fused=False):
+    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask, fused=False, cam_model=0):
         B, _, H, W = image.shape
         p = _hip.Params()
         p.B, p.H, p.W, p.N, p.S = B, H, W, len(contexts), S
@@ -102,6 +102,7 @@ class _Call:
         p.min_depth, p.max_depth = cfg["min_depth"], cfg["max_depth"]
         p.clip_loss, p.smooth_w = cfg["clip"], cfg["smooth_w"]
         p.grad_fused = int(fused)
+        p.cam_model = cam_model
         self.params = p
         self.image, self.contexts, self.sigs, self.cam, self.mask = image, contexts, sigs, cam, mask
         inp = _hip.Inputs()
@@ -130,6 +131,22 @@ class _Call:
             off += sz
         ws.argmin = self.abuf.data_ptr()
         self.ws = ws
+
+
+def _fisheye_records(K, ref_K, T, sw, sh, S, N, B, dev):
+    """[S,N,B,CAMREC] fisheye records (include/psfm.h): target s, div, ux', uy' | context k0..k6,
+    s, div, ux', uy' | T, centres scaled (c + 0.5) s - 0.5 per scale, k / s / div unscaled
+    (losses/multiview_photometric_loss.py:166-186)."""
+    def cam(c):
+        return torch.stack([c["s"].float(), c["div"].float(), (c["ux"].float() + 0.5) * sw - 0.5,
+                            (c["uy"].float() + 0.5) * sh - 0.5], -1).reshape(B, 4)
+    tgt = cam(K).to(dev)
+    ref = torch.cat([ref_K["k"].float().reshape(B, 7).to(dev), cam(ref_K).to(dev)], -1)
+    rec = torch.zeros(S, N, B, _hip.CAMREC, device=dev, dtype=torch.float32)
+    rec[..., 0:4] = tgt.reshape(1, 1, B, 4)
+    rec[..., 4:15] = ref.reshape(1, 1, B, 11)
+    rec[..., 18:30] = T.reshape(1, N, B, 12)
+    return rec.contiguous()
 
 
 def _sig_array(ts):
@@ -168,22 +185,31 @@ class PhotometricLossFn(torch.autograd.Function):
             s0 = s1
         # training step: K12 computes the gradient during the forward
         # (needs_input_grad is False everywhere under no_grad / for data-only inputs)
-        fused = FUSED_GRAD and any(ctx.needs_input_grad[5:]) and N <= 2 and cfg["ssim_w"] > 0.0
+        wants_grad = any(ctx.needs_input_grad[5:])
+        fish = isinstance(K, dict)
+        fused = FUSED_GRAD and wants_grad and N <= 2 and cfg["ssim_w"] > 0.0
+        if fish and (N > 2 or cfg["ssim_w"] <= 0.0 or (wants_grad and not fused)):
+            raise NotImplementedError("fisheye (VADAS) cameras: N <= 2 contexts, SSIM candidates, and the K12 "
+                                      "gradient path (FUSED_GRAD)")
         calls = []
         for (a, b) in groups:
             hw = sigs[a].shape[-2:]
             scale = hw[1] / float(W)  # Camera.scaled(DW/W) (camera.py:84-108)
-            Kt = scale_intrinsics(K.clone(), scale, scale) if scale != 1.0 else K
-            Kr = scale_intrinsics(ref_K.clone(), scale, scale) if scale != 1.0 else ref_K
-            kinv = pinhole_inverse(Kt.float()).reshape(1, 1, B, 9).expand(b - a, N, B, 9)
-            kref = Kr.float().reshape(1, 1, B, 9).expand(b - a, N, B, 9)
-            tt = Tf.reshape(1, N, B, 12).expand(b - a, N, B, 12)
-            pad = torch.zeros(b - a, N, B, _hip.CAMREC - 30, device=dev, dtype=torch.float32)
-            cam = torch.cat([kinv, kref, tt, pad], -1).contiguous()
+            if fish:
+                cam = _fisheye_records(K, ref_K, Tf, scale, hw[0] / float(H), b - a, N, B, dev)
+            else:
+                Kt = scale_intrinsics(K.clone(), scale, scale) if scale != 1.0 else K
+                Kr = scale_intrinsics(ref_K.clone(), scale, scale) if scale != 1.0 else ref_K
+                kinv = pinhole_inverse(Kt.float()).reshape(1, 1, B, 9).expand(b - a, N, B, 9)
+                kref = Kr.float().reshape(1, 1, B, 9).expand(b - a, N, B, 9)
+                tt = Tf.reshape(1, N, B, 12).expand(b - a, N, B, 12)
+                pad = torch.zeros(b - a, N, B, _hip.CAMREC - 30, device=dev, dtype=torch.float32)
+                cam = torch.cat([kinv, kref, tt, pad], -1).contiguous()
             im = _to_size(image, hw, "bilinear")
             cx = [_to_size(c, hw, "bilinear") for c in contexts]
             mk = _to_size(mask, hw, "nearest").contiguous() if mask is not None else None
-            calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk, fused))
+            calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk, fused,
+                               _hip.CAM_FISHEYE if fish else _hip.CAM_PINHOLE))
 
         L = _hip.lib()
         st = _hip.stream(dev)

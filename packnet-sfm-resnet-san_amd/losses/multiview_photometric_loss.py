@@ -6,8 +6,9 @@ Semantics (pinned by tests/golden/, generated from the reference):
   * `inv_depths` are the depth net's SIGMOID outputs (fork semantics, :362-369): depth =
     sigmoid_to_depth_linear(s), inv = 1/(depth+1e-8), warp depth = 1/clamp(inv, 1e-6);
     smoothness acts on the sigmoid maps (:404-405);
-  * pinhole intrinsics `K [B,3,3]` (the fork's hard-wired FisheyeCamera dict path cannot
-    run, SURVEY.md §0.3b-d); `mask=None` means "no mask" (== all ones);
+  * pinhole intrinsics `K [B,3,3]` or the fork's FisheyeCamera (VADAS) dicts {k [B,7], s, div,
+    ux, uy} (:131-195; the pose is applied to the reconstructed points as R X + t, which the fork
+    cannot do on CPU / on [B,3,N], SURVEY.md §0.3c-d); `mask=None` means "no mask" (== all ones);
   * `metrics['photometric_loss']` aliases the loss value, as the reference's in-place
     `loss += smoothness` does (:296, :405).
 """
@@ -60,9 +61,8 @@ class MultiViewPhotometricLoss(LossBase):
 
     def forward(self, image, context, inv_depths, intrinsics, ref_intrinsics, poses,
                 return_logs=False, progress=0.0, mask=None):
-        if isinstance(intrinsics, dict) or isinstance(ref_intrinsics, dict):
-            raise NotImplementedError("FisheyeCamera (VADAS dict intrinsics) is a SURVEY §8f 'next' row; "
-                                      "pass pinhole K [B,3,3]")
+        if isinstance(intrinsics, dict) != isinstance(ref_intrinsics, dict):
+            raise ValueError("intrinsics and ref_intrinsics must be both pinhole K or both fisheye dicts")
         self.n = self.progressive_scaling(progress)
         sigs = [s.float() for s in inv_depths[:self.n]]  # nets may run under bf16 autocast
         T = torch.stack([p.mat[:, :3, :] for p in poses], 0)  # [N,B,3,4], differentiable
@@ -74,9 +74,10 @@ class MultiViewPhotometricLoss(LossBase):
         if mask is not None:
             mask = mask.float()
         with torch.autocast("cuda", enabled=False):   # the photometric path is fp32 end to end
+            fl = (lambda k: {n: v.float() for n, v in k.items()}) if isinstance(intrinsics, dict) else \
+                (lambda k: k.float())
             loss, photo, smooth = photometric_loss_hip(image.float(), [c.float() for c in context], sigs,
-                                                       intrinsics.float(), ref_intrinsics.float(), T.float(),
-                                                       mask, cfg)
+                                                       fl(intrinsics), fl(ref_intrinsics), T.float(), mask, cfg)
         self.add_metric("photometric_loss", photo)
         if self.smooth_loss_weight > 0.0:
             self.add_metric("smoothness_loss", smooth)

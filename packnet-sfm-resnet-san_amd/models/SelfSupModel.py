@@ -3,8 +3,8 @@
 Differences from the fork, all documented in DESIGN.md §Semantics:
   * `forward` accepts the `masks=` keyword its caller passes (model_wrapper.py:299 — the fork's
     signature rejects it, SURVEY §0.3a); the mask is `masks` if given, else batch['mask'];
-  * pinhole intrinsics: the loss gets batch['intrinsics'] ([B,3,3]); a fisheye dict in
-    batch['distortion_coeffs'] is the SURVEY §8f 'next' row (raises NotImplementedError).
+  * cameras: a fisheye (VADAS) dict in batch['distortion_coeffs'] goes to the loss for both
+    cameras, as the fork does (:108-117); otherwise the pinhole batch['intrinsics'] [B,3,3].
 """
 import torch
 
@@ -32,10 +32,8 @@ class SelfSupModel(SfmModel):
         output = super().forward(batch, return_logs=return_logs)
         if not self.training:
             return output
-        K = batch["intrinsics"]
         dc = batch.get("distortion_coeffs", None)
-        if isinstance(dc, dict):
-            raise NotImplementedError("fisheye (VADAS) intrinsics are the SURVEY §8f 'next' row")
+        K = dc if isinstance(dc, dict) else batch["intrinsics"]
         mask = masks if masks is not None else batch.get("mask", None)
         self_sup_output = self.self_supervised_loss(
             batch["rgb_original"], batch["rgb_context_original"], output["inv_depths"], output["poses"],

@@ -1,0 +1,84 @@
+"""GPU parity of the photometric path on the fork's fisheye VADAS cameras (geometry/camera.py:
+194-394, losses/multiview_photometric_loss.py:131-195) against goldens generated from the
+reference (tools/gen_goldens.py:gen_fisheye) — K12 training path and the K1 forward-only path.
+Tolerances as tests/test_hip_photometric.py."""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+LOSS_TOL, GRAD_TOL = 1e-4, 1e-3
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import __graft_entry__
+    __graft_entry__.build()
+    return torch.device("cuda:0")
+
+
+def _T(a, dev=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.to(dev) if dev is not None else t
+
+
+def _intr(z, dev=None):
+    return {k: _T(z[f"intr_{k}"], dev) for k in ("k", "s", "div", "ux", "uy")}
+
+
+def _run(z, tag, dev, grad=True):
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    sigs = [_T(z[f"sig{i}{tag}"], dev).requires_grad_(grad) for i in range(4)]
+    vec = _T(z[f"pvec{tag}"], dev).requires_grad_(grad)
+    fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
+                                  photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
+                                  min_depth=0.5, max_depth=80.0)
+    intr = _intr(z, dev)
+    with torch.set_grad_enabled(grad):
+        out = fn(_T(z[f"image{tag}"], dev), [_T(z[f"ctx0{tag}"], dev), _T(z[f"ctx1{tag}"], dev)], sigs, intr, intr,
+                 [Pose.from_vec(vec[:, j], "euler") for j in range(2)])
+    if grad:
+        out["loss"].sum().backward()
+    torch.cuda.synchronize()
+    return out, sigs, vec
+
+
+@pytest.mark.parametrize("tag", ["", "_multires"])
+def test_fisheye_loss_and_grads_match_reference(dev, tag):
+    from oracle import photometric_oracle as O
+    z = gu.load_golden("fisheye_small")
+    out, sigs, vec = _run(z, tag, dev)
+    assert gu.rel_err(out["loss"].detach().cpu(), z[f"loss{tag}"]) < LOSS_TOL
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z[f"smoothness_loss{tag}"]) < LOSS_TOL
+    sens = None
+    if not tag:
+        sens = [m.numpy() for m in O.sensitive_pixels(
+            _T(z["image"]), [_T(z["ctx0"]), _T(z["ctx1"])], [_T(z[f"sig{i}"]) for i in range(4)], _intr(z),
+            [O.pose_vec_to_mat(_T(z["pvec"])[:, j]) for j in range(2)], 0.5, 80.0)]
+    for i, s in enumerate(sigs):
+        ok, msg = gu.grad_check(s.grad.cpu(), z[f"grad_sig{i}{tag}"], None if sens is None else sens[i], GRAD_TOL)
+        assert ok, f"dL/dsig{i}: {msg}"
+    n_sens = 0 if sens is None else int(sum(m.sum() for m in sens))
+    assert gu.rel_err(vec.grad.cpu(), z[f"grad_vec{tag}"]) < (GRAD_TOL if n_sens == 0 else 2e-2)
+
+
+def test_fisheye_forward_only_path(dev):
+    z = gu.load_golden("fisheye_small")
+    out, _, _ = _run(z, "", dev, grad=False)
+    assert gu.rel_err(out["loss"].cpu(), z["loss"]) < LOSS_TOL
+
+
+def test_fisheye_needs_fused_gradient(dev):
+    from packnet_sfm_amd.losses import _hip_photometric as HP
+    z = gu.load_golden("fisheye_small")
+    HP.FUSED_GRAD = False
+    try:
+        with pytest.raises(NotImplementedError, match="fisheye"):
+            _run(z, "", dev)
+    finally:
+        HP.FUSED_GRAD = True
