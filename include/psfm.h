@@ -169,12 +169,13 @@ int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
                                  float* grad_T, void* stream);
 
 /* Standalone view_synthesis (geometry/camera_utils.py:27-59) for one context:
- * warped[B,3,H,W] = grid_sample(ref, project(reconstruct(depth))).  cam: [B][PSFM_CAMREC]. */
-int psfm_view_synthesis_fwd(int B, int H, int W, const float* ref, const float* depth,
+ * warped[B,3,H,W] = grid_sample(ref, project(reconstruct(depth))).  cam: [B][PSFM_CAMREC] records
+ * of `cam_model` (psfm_cam_model; layout as psfm_inputs.cam with N = 1). */
+int psfm_view_synthesis_fwd(int cam_model, int B, int H, int W, const float* ref, const float* depth,
                             const float* cam, float* warped, void* stream);
 /* its backward: dL/ddepth [B,1,H,W] (written) and dL/dT partials [B][tiles][12], reduced into
  * grad_T [B][12] */
-int psfm_view_synthesis_bwd(int B, int H, int W, const float* ref, const float* depth,
+int psfm_view_synthesis_bwd(int cam_model, int B, int H, int W, const float* ref, const float* depth,
                             const float* cam, const float* grad_warped, float* grad_depth,
                             float* pose_part, float* grad_T, void* stream);
 

@@ -79,8 +79,8 @@ def lib():
         "psfm_photometric_fwd_grad": ([P, IN, WS, V, V], c_int),
         "psfm_photometric_grad_finish": ([P, V, V, V, V, V], c_int),
         "psfm_pose_grad_reduce_scaled": ([c_int, PP, WSP, V, V, V], c_int),
-        "psfm_view_synthesis_fwd": ([c_int, c_int, c_int, V, V, V, V, V], c_int),
-        "psfm_view_synthesis_bwd": ([c_int, c_int, c_int, V, V, V, V, V, V, V, V], c_int),
+        "psfm_view_synthesis_fwd": ([c_int, c_int, c_int, c_int, V, V, V, V, V], c_int),
+        "psfm_view_synthesis_bwd": ([c_int, c_int, c_int, c_int, V, V, V, V, V, V, V, V], c_int),
         "psfm_tiles_per_image": ([c_int, c_int], c_int),
         "psfm_last_error": ([], ctypes.c_char_p),
         "psfm_version": ([], ctypes.c_char_p),

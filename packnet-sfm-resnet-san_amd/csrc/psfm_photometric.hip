@@ -831,39 +831,48 @@ struct VSArgs {
     float* pose_part;
 };
 
+template <int MODEL>
 __global__ __launch_bounds__(NT) void k_vs_fwd(VSArgs v) {
     const TileGeom g = tile_geom(v.H, v.W);
     if (!g.inside) return;
     const size_t plane = (size_t)v.H * v.W, pix = (size_t)g.gy * v.W + g.gx;
-    CamRec cam;
-    load_cam(v.cam + (size_t)g.b * PSFM_CAMREC, cam);
-    Proj r;
-    project(cam, (float)g.gx, (float)g.gy, v.depth[(size_t)g.b * plane + pix], v.H, v.W, r);
+    Cams<1, MODEL> cam;
+    cam.load(as_const(v.cam + (size_t)g.b * PSFM_CAMREC), v.B, v.H, v.W);
+    typename Cams<1, MODEL>::P r;
+    cam.project(0, cam.lift((float)g.gx, (float)g.gy, v.depth[(size_t)g.b * plane + pix]), r);
     float w[3];
     bilinear3(v.ref + (size_t)g.b * 3 * plane, v.H, v.W, r.ix, r.iy, w);
 #pragma unroll
     for (int c = 0; c < 3; ++c) v.warped[((size_t)g.b * 3 + c) * plane + pix] = w[c];
 }
 
+template <int MODEL>
 __global__ __launch_bounds__(NT) void k_vs_bwd(VSArgs v) {
     const TileGeom g = tile_geom(v.H, v.W);
     __shared__ float red[NWAVE * 12];
     const size_t plane = (size_t)v.H * v.W, pix = (size_t)g.gy * v.W + g.gx;
-    CamRec cam;
-    load_cam(v.cam + (size_t)g.b * PSFM_CAMREC, cam);
+    Cams<1, MODEL> cam;
+    cam.load(as_const(v.cam + (size_t)g.b * PSFM_CAMREC), v.B, v.H, v.W);
     float gT[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) gT[k] = 0.0f;
     if (g.inside) {
         const float d = v.depth[(size_t)g.b * plane + pix];
-        Proj r;
-        project(cam, (float)g.gx, (float)g.gy, d, v.H, v.W, r);
+        typename Cams<1, MODEL>::P r;
+        cam.project(0, cam.lift((float)g.gx, (float)g.gy, d), r);
         float gw[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) gw[c] = v.grad_warped[((size_t)g.b * 3 + c) * plane + pix];
-        float gix, giy;
+        float gix, giy, gc[3];
         bilinear3_grad_pos(v.ref + (size_t)g.b * 3 * plane, v.H, v.W, r.ix, r.iy, gw, gix, giy);
-        v.grad_depth[(size_t)g.b * plane + pix] = project_grad(cam, r, d, gix, giy, v.H, v.W, gT);
+        v.grad_depth[(size_t)g.b * plane + pix] = cam.grad(0, r, gix, giy, gc);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {  // dL/dT = gc (X, 1)^T
+            gT[4 * i + 0] += gc[i] * r.X0;
+            gT[4 * i + 1] += gc[i] * r.X1;
+            gT[4 * i + 2] += gc[i] * r.X2;
+            gT[4 * i + 3] += gc[i];
+        }
     }
     block_sum<12>(gT, red);
     if (threadIdx.x == 0) {
@@ -1155,23 +1164,31 @@ int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
     return 0;
 }
 
-int psfm_view_synthesis_fwd(int B, int H, int W, const float* ref, const float* depth,
+int psfm_view_synthesis_fwd(int cam_model, int B, int H, int W, const float* ref, const float* depth,
                             const float* cam, float* warped, void* stream) {
     if (B < 1 || H < 2 || W < 2 || !ref || !depth || !cam || !warped) return fail(-1, "bad view_synthesis args");
+    if (cam_model != PSFM_CAM_PINHOLE && cam_model != PSFM_CAM_FISHEYE) return fail(-16, "unknown cam_model");
     VSArgs v{B, H, W, ref, depth, cam, nullptr, warped, nullptr, nullptr};
-    hipLaunchKernelGGL(k_vs_fwd, dim3(tiles_img(H, W), B), dim3(NT), 0, (hipStream_t)stream, v);
+    if (cam_model == PSFM_CAM_FISHEYE)
+        hipLaunchKernelGGL(k_vs_fwd<PSFM_CAM_FISHEYE>, dim3(tiles_img(H, W), B), dim3(NT), 0, (hipStream_t)stream, v);
+    else
+        hipLaunchKernelGGL(k_vs_fwd<PSFM_CAM_PINHOLE>, dim3(tiles_img(H, W), B), dim3(NT), 0, (hipStream_t)stream, v);
     PSFM_LAUNCH_CHECK();
     return 0;
 }
 
-int psfm_view_synthesis_bwd(int B, int H, int W, const float* ref, const float* depth,
+int psfm_view_synthesis_bwd(int cam_model, int B, int H, int W, const float* ref, const float* depth,
                             const float* cam, const float* grad_warped, float* grad_depth,
                             float* pose_part, float* grad_T, void* stream) {
     if (B < 1 || H < 2 || W < 2 || !ref || !depth || !cam || !grad_warped || !grad_depth || !pose_part || !grad_T)
         return fail(-1, "bad view_synthesis_bwd args");
+    if (cam_model != PSFM_CAM_PINHOLE && cam_model != PSFM_CAM_FISHEYE) return fail(-16, "unknown cam_model");
     VSArgs v{B, H, W, ref, depth, cam, grad_warped, nullptr, grad_depth, pose_part};
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_vs_bwd, dim3(tiles_img(H, W), B), dim3(NT), 0, st, v);
+    if (cam_model == PSFM_CAM_FISHEYE)
+        hipLaunchKernelGGL(k_vs_bwd<PSFM_CAM_FISHEYE>, dim3(tiles_img(H, W), B), dim3(NT), 0, st, v);
+    else
+        hipLaunchKernelGGL(k_vs_bwd<PSFM_CAM_PINHOLE>, dim3(tiles_img(H, W), B), dim3(NT), 0, st, v);
     PSFM_LAUNCH_CHECK();
     PoseRedArgs r{};
     r.ncalls = 1;

@@ -33,11 +33,23 @@ def pinhole_inverse(K):
 
 def view_synthesis(ref_image, depth, ref_cam, cam, mode="bilinear", padding_mode="zeros"):
     """Warp `ref_image` [B,3,H,W] into `cam`'s view using `depth` [B,1,H,W]
-    (bilinear, zero padding, align_corners=True).  Differentiable w.r.t. depth and the poses."""
+    (bilinear, zero padding, align_corners=True).  Differentiable w.r.t. depth and the poses.
+    `Camera` (pinhole) or `FisheyeCamera` (VADAS) pairs."""
     if mode != "bilinear" or padding_mode != "zeros":
         raise NotImplementedError("HIP view_synthesis implements bilinear / zeros (reference default)")
     assert depth.size(1) == 1
+    from .. import _hip
     from ..losses._hip_photometric import ViewSynthesisFn
+    from .camera import FisheyeCamera
     # world->ref composite: ref_cam.Tcw @ cam.Twc (camera.py:144 then :165)
     T = ref_cam.Tcw.mat.bmm(cam.Twc.mat)[:, :3, :]
-    return ViewSynthesisFn.apply(ref_image, depth, pinhole_inverse(cam.K.float()), ref_cam.K.float(), T)
+    B = depth.shape[0]
+    if isinstance(cam, FisheyeCamera) != isinstance(ref_cam, FisheyeCamera):
+        raise ValueError("view_synthesis: both cameras pinhole or both fisheye")
+    if isinstance(cam, FisheyeCamera):
+        f = lambda t: t.float().reshape(B, -1)  # noqa: E731
+        rec = torch.cat([f(cam.s), f(cam.div), f(cam.ux), f(cam.uy), f(ref_cam.k), f(ref_cam.s), f(ref_cam.div),
+                         f(ref_cam.ux), f(ref_cam.uy), torch.zeros(B, 3, device=depth.device)], -1)
+        return ViewSynthesisFn.apply(ref_image, depth, rec, T, _hip.CAM_FISHEYE)
+    rec = torch.cat([pinhole_inverse(cam.K.float()).reshape(B, 9), ref_cam.K.float().reshape(B, 9)], -1)
+    return ViewSynthesisFn.apply(ref_image, depth, rec, T, _hip.CAM_PINHOLE)

@@ -287,22 +287,23 @@ def photometric_loss_hip(image, contexts, sigs, K, ref_K, T, mask, cfg):
 
 # -------------------------------------------------------------------------------------------------
 class ViewSynthesisFn(torch.autograd.Function):
-    """view_synthesis (geometry/camera_utils.py:27-59) on HIP: grads to depth and [R|t]."""
+    """view_synthesis (geometry/camera_utils.py:27-59) on HIP: grads to depth and [R|t].
+    `rec` [B, CAMREC-18] = the camera fields of the record (pinhole K^-1 | K, or the fisheye
+    target | context parameters); T [B,3,4] target -> context."""
 
     @staticmethod
-    def forward(ctx, ref_image, depth, Kinv, Kref, T):
+    def forward(ctx, ref_image, depth, rec, T, cam_model):
         ref_image, depth = ref_image.contiguous(), depth.contiguous()
         _hip.require_device(ref_image, depth)
         B, _, H, W = ref_image.shape
         pad = torch.zeros(B, _hip.CAMREC - 30, device=depth.device)
-        cam = torch.cat([Kinv.reshape(B, 9).float(), Kref.reshape(B, 9).float(),
-                         T.detach().reshape(B, 12).float(), pad], -1).contiguous()
+        cam = torch.cat([rec.reshape(B, 18).float(), T.detach().reshape(B, 12).float(), pad], -1).contiguous()
         warped = torch.empty_like(ref_image)
-        _hip.check(_hip.lib().psfm_view_synthesis_fwd(B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
+        _hip.check(_hip.lib().psfm_view_synthesis_fwd(cam_model, B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
                                                       _hip.ptr(cam), _hip.ptr(warped),
                                                       _hip.stream(depth.device)), "view_synthesis_fwd")
         ctx.save_for_backward(ref_image, depth, cam)
-        ctx.T_shape = T.shape
+        ctx.T_shape, ctx.cam_model = T.shape, cam_model
         return warped
 
     @staticmethod
@@ -314,8 +315,8 @@ class ViewSynthesisFn(torch.autograd.Function):
         tiles = _hip.tiles_per_image(H, W)
         part = torch.empty(B * tiles * 12, device=depth.device)
         gT = torch.empty(B, 12, device=depth.device)
-        _hip.check(_hip.lib().psfm_view_synthesis_bwd(B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
+        _hip.check(_hip.lib().psfm_view_synthesis_bwd(ctx.cam_model, B, H, W, _hip.ptr(ref_image), _hip.ptr(depth),
                                                       _hip.ptr(cam), _hip.ptr(g), _hip.ptr(gd),
                                                       _hip.ptr(part), _hip.ptr(gT),
                                                       _hip.stream(depth.device)), "view_synthesis_bwd")
-        return None, gd, None, None, gT.reshape(ctx.T_shape)
+        return None, gd, None, gT.reshape(ctx.T_shape), None

@@ -82,3 +82,28 @@ def test_fisheye_needs_fused_gradient(dev):
             _run(z, "", dev)
     finally:
         HP.FUSED_GRAD = True
+
+
+def test_fisheye_view_synthesis(dev):
+    """view_synthesis with FisheyeCameras (HIP standalone warp) vs the reference's warp (golden)
+    and its gradient vs the oracle's autograd"""
+    from oracle import photometric_oracle as O
+    from packnet_sfm_amd.geometry.camera import FisheyeCamera
+    from packnet_sfm_amd.geometry.camera_utils import view_synthesis
+    from packnet_sfm_amd.geometry.pose import Pose
+    z = gu.load_golden("fisheye_small")
+    B, _, H, W = z["depth"].shape
+    depth = _T(z["depth"], dev).requires_grad_(True)
+    vec = _T(z["vec"], dev).requires_grad_(True)
+    warped = view_synthesis(_T(z["ref"], dev), depth,
+                            FisheyeCamera(_intr(z, dev), Tcw=Pose.from_vec(vec, "euler"), image_size=(H, W)),
+                            FisheyeCamera(_intr(z, dev), image_size=(H, W)))
+    assert gu.rel_err(warped.detach().cpu(), z["warped"]) < 1e-4
+    d_c = _T(z["depth"]).requires_grad_(True)
+    v_c = _T(z["vec"]).requires_grad_(True)
+    ref = O.synthesize(_T(z["ref"]), d_c, _intr(z), _intr(z), O.pose_vec_to_mat(v_c))
+    wgt = torch.linspace(0.5, 1.5, ref.numel()).reshape(ref.shape)
+    (ref * wgt).sum().backward()
+    (warped * wgt.to(dev)).sum().backward()
+    assert gu.rel_err(depth.grad.cpu(), d_c.grad) < GRAD_TOL
+    assert gu.rel_err(vec.grad.cpu(), v_c.grad) < 5e-3
