@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     ap.add_argument("--nchw", action="store_true", help="keep the nets in NCHW (default: channels_last)")
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
+    ap.add_argument("--no-miopen-find", action="store_true",
+                    help="torch.backends.cudnn.benchmark = False (MIOpen heuristics instead of find)")
     ap.add_argument("--fused-nets", action="store_true",
                     help="run the nets' BN/GN/bias+activation epilogues as fused HIP kernels (psfm_netops)")
     return ap.parse_args()
@@ -80,6 +82,16 @@ def synthetic_batch(B, H, W, device, seed, channels_last=False):
         cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
         batch["rgb"], batch["rgb_context"] = cl(rgb), [cl(c) for c in ctx]
     return batch
+
+
+def to_channels_last(model):
+    """NHWC for every 4-D parameter (the MIOpen NHWC conv kernels); PackNet01's Conv3d weights
+    (5-D) stay as they are (Module.to(memory_format=...) refuses a model that has them)."""
+    with torch.no_grad():
+        for p in model.parameters():
+            if p.dim() == 4:
+                p.data = p.data.contiguous(memory_format=torch.channels_last)
+    return model
 
 
 def build_model(args, device):
@@ -195,17 +207,21 @@ def main():
     from packnet_sfm_amd.networks.layers import fused
     fused.ENABLED = bool(args.fused_nets)
     torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = not args.no_miopen_find
     model = build_model(args, device)
     if not args.nchw:
-        model = model.to(memory_format=torch.channels_last)
+        to_channels_last(model)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
                          graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager))
     batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank, channels_last=not args.nchw)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):   # the first steps include MIOpen find and the HIP-graph capture
+        t_w = time.perf_counter()
         trainer.train_step(batch)
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup step {i}: {time.perf_counter() - t_w:.2f} s", file=sys.stderr, flush=True)
     trainer.check_finite()
 
     if world > 1:

@@ -102,6 +102,11 @@ def lib():
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V, V],
                             c_int),
         "psfm_netops_last_error": ([], ctypes.c_char_p),
+        # include/psfm_pack3d.h
+        "psfm_p3d_fwd": ([V, V, V, V, V, V], c_int),
+        "psfm_p3d_ws_floats": ([V], ctypes.c_int64),
+        "psfm_p3d_bwd": ([V, V, V, V, V, V, V, V, V], c_int),
+        "psfm_p3d_last_error": ([], ctypes.c_char_p),
         # include/psfm_metrics.h
         "psfm_depth_metrics": ([ctypes.POINTER(MetricsParams), V, V, V, V, V], c_int),
         "psfm_metrics_last_error": ([], ctypes.c_char_p),
@@ -121,7 +126,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
-            "psfm_depth_metrics", "psfm_metrics_last_error")
+            "psfm_depth_metrics", "psfm_metrics_last_error",
+            "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error")
 
 
 def check(rc, what):
@@ -132,6 +138,8 @@ def check(rc, what):
             err = lib().psfm_netops_last_error
         elif what.startswith("psfm_depth_metrics"):
             err = lib().psfm_metrics_last_error
+        elif what.startswith("psfm_p3d"):
+            err = lib().psfm_p3d_last_error
         else:
             err = lib().psfm_last_error
         raise RuntimeError(f"{what} failed ({rc}): {err().decode()}")

@@ -1,0 +1,371 @@
+// psfm_pack3d.hip — fused PackNet packing / unpacking 3-D convolution for MI355X (gfx950), behind
+// include/psfm_pack3d.h.
+//
+// Reference: packnet_sfm/networks/layers/packnet/layers01.py:126-146 (packing), :189-223
+// (PackLayerConv3d), :226-282 (UnpackLayerConv3d).  The Conv3d(1 -> d=8, 3x3x3, pad 1) is a small
+// stencil (216 FMAs per voxel) whose output is 8x its input: it is HBM-bound on the write, so
+// the kernels stream the volume through LDS tiles (with a 1-voxel halo in k, y, x), keep the 216
+// weights in LDS ([tap][o]: two b128 broadcast reads per tap), and write every folded /
+// pixel-shuffled output element exactly once, straight into the caller's layout (strides).
+//   k_p3d_fwd      y  = conv3d(V)            4 x 16 pixels x 32 k per chunk
+//   k_p3d_bwd_x    dV = conv3d^T(dy)         4 x 8 pixels x 16 k, dy tile with halo in LDS
+//   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (tap, o)), fixed-order fp64 reduce
+// V is the virtual volume: pack = space-to-depth view of x (channel k = c r^2 + i r + j),
+// unpack = x itself; the output channel o K + k is folded (pack) or pixel-shuffled (unpack).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/psfm_pack3d.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+constexpr int NTH = 256;
+constexpr int ND = 8;  // Conv3d output features (PackNet d = 8)
+
+struct P3 {
+    int B, C, Hv, Wv, r, K, KG;  // K volume channels, KG chunks of channels per workgroup
+    int64_t xs[4], ys[4];
+    const void* x;
+    const void* dy;
+    void* y;
+    void* dx;
+    const float* w;
+    const float* bias;
+    float* ws;
+};
+
+// storage types: fp32, or bf16 as raw 16-bit words (round to nearest even, as torch does)
+template <typename T>
+__device__ __forceinline__ float ld(const void* p, int64_t i);
+template <>
+__device__ __forceinline__ float ld<float>(const void* p, int64_t i) {
+    return static_cast<const float*>(p)[i];
+}
+template <>
+__device__ __forceinline__ float ld<uint16_t>(const void* p, int64_t i) {
+    return __uint_as_float((uint32_t)static_cast<const uint16_t*>(p)[i] << 16);
+}
+template <typename T>
+__device__ __forceinline__ void st(void* p, int64_t i, float v);
+template <>
+__device__ __forceinline__ void st<float>(void* p, int64_t i, float v) {
+    static_cast<float*>(p)[i] = v;
+}
+template <>
+__device__ __forceinline__ void st<uint16_t>(void* p, int64_t i, float v) {
+    uint32_t u = __float_as_uint(v);
+    u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite values)
+    static_cast<uint16_t*>(p)[i] = (uint16_t)(u >> 16);
+}
+
+// element offset of volume voxel (b, k, y, x) in x
+template <int MODE>
+__device__ __forceinline__ int64_t vaddr(const P3& a, int b, int k, int y, int x) {
+    if (MODE == PSFM_P3D_PACK) {
+        const int rr = a.r * a.r, c = k / rr, q = k - c * rr, i = q / a.r, j = q - i * a.r;
+        return b * a.xs[0] + c * a.xs[1] + (int64_t)(y * a.r + i) * a.xs[2] + (int64_t)(x * a.r + j) * a.xs[3];
+    }
+    return b * a.xs[0] + k * a.xs[1] + (int64_t)y * a.xs[2] + (int64_t)x * a.xs[3];
+}
+// element offset of output feature (b, o, k, y, x) in y (folded channel o K + k)
+template <int MODE>
+__device__ __forceinline__ int64_t yaddr(const P3& a, int b, int o, int k, int y, int x) {
+    const int q = o * a.K + k;
+    if (MODE == PSFM_P3D_PACK)
+        return b * a.ys[0] + q * a.ys[1] + (int64_t)y * a.ys[2] + (int64_t)x * a.ys[3];
+    const int rr = a.r * a.r, c = q / rr, s = q - c * rr, i = s / a.r, j = s - i * a.r;
+    return b * a.ys[0] + c * a.ys[1] + (int64_t)(y * a.r + i) * a.ys[2] + (int64_t)(x * a.r + j) * a.ys[3];
+}
+
+__device__ __forceinline__ void load_weights(const P3& a, float* sw) {
+    // sw[tap * 8 + o] = w[o][tap]; sw[216 + o] = bias[o]
+    for (int i = threadIdx.x; i < 27 * ND; i += NTH) sw[i] = a.w[(i % ND) * 27 + i / ND];
+    if (threadIdx.x < ND) sw[27 * ND + threadIdx.x] = a.bias ? a.bias[threadIdx.x] : 0.0f;
+}
+
+// --------------------------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(NTH) void k_p3d_fwd(P3 a) {
+    constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 2;
+    __shared__ float sv[LY * LX * LK];
+    __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
+    load_weights(a, sw);
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int dl = threadIdx.x % DC, pg = threadIdx.x / DC;
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC;
+        __syncthreads();
+        for (int e = threadIdx.x; e < LY * LX * LK; e += NTH) {
+            const int kk = e % LK, rest = e / LK, xx = rest % LX, yy = rest / LX;
+            const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+            const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
+            sv[e] = in ? ld<T>(a.x, vaddr<MODE>(a, b, gk, gy, gx)) : 0.0f;
+        }
+        __syncthreads();
+        const int k = k0 + dl;
+        if (k >= a.K) continue;
+#pragma unroll 1
+        for (int pp = 0; pp < (TY * TX) / (NTH / DC); ++pp) {
+            const int p = pg + pp * (NTH / DC), py = p / TX, px = p % TX;
+            const int gy = y0 + py, gx = x0 + px;
+            if (gy >= a.Hv || gx >= a.Wv) continue;
+            float acc[ND];
+#pragma unroll
+            for (int o = 0; o < ND; ++o) acc[o] = sw[27 * ND + o];
+#pragma unroll
+            for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const float v = sv[((py + dy) * LX + (px + dx)) * LK + dl + dz];
+                        const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
+                        const float4 wa = w4[0], wb = w4[1];
+                        acc[0] += wa.x * v; acc[1] += wa.y * v; acc[2] += wa.z * v; acc[3] += wa.w * v;
+                        acc[4] += wb.x * v; acc[5] += wb.y * v; acc[6] += wb.z * v; acc[7] += wb.w * v;
+                    }
+#pragma unroll
+            for (int o = 0; o < ND; ++o) st<T>(a.y, yaddr<MODE>(a, b, o, k, gy, gx), acc[o]);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// dV[k, y, x] = sum_o sum_taps w[o, dz, dy, dx] dy[o, k - dz + 1, y - dy + 1, x - dx + 1]
+template <typename T, int MODE>
+__global__ __launch_bounds__(NTH) void k_p3d_bwd_x(P3 a) {
+    constexpr int TY = 4, TX = 8, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
+    __shared__ float sg[LY * LX * ND * LK];  // [yy][xx][o][kk]
+    __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
+    load_weights(a, sw);
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int dl = threadIdx.x % DC, pg = threadIdx.x / DC;
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC;
+        __syncthreads();
+        for (int e = threadIdx.x; e < LY * LX * ND * LK; e += NTH) {
+            const int kk = e % LK, r1 = e / LK, o = r1 % ND, r2 = r1 / ND, xx = r2 % LX, yy = r2 / LX;
+            const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+            const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
+            sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, o, gk, gy, gx)) : 0.0f;
+        }
+        __syncthreads();
+        const int k = k0 + dl;
+        if (k >= a.K) continue;
+#pragma unroll 1
+        for (int pp = 0; pp < (TY * TX) / (NTH / DC); ++pp) {
+            const int p = pg + pp * (NTH / DC), py = p / TX, px = p % TX;
+            const int gy = y0 + py, gx = x0 + px;
+            if (gy >= a.Hv || gx >= a.Wv) continue;
+            float acc = 0.0f;
+#pragma unroll
+            for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const float* g = sg + (((py + 2 - dy) * LX + (px + 2 - dx)) * ND) * LK + dl + 2 - dz;
+                        const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
+                        const float4 wa = w4[0], wb = w4[1];
+                        acc += wa.x * g[0 * LK] + wa.y * g[1 * LK] + wa.z * g[2 * LK] + wa.w * g[3 * LK] +
+                               wb.x * g[4 * LK] + wb.y * g[5 * LK] + wb.z * g[6 * LK] + wb.w * g[7 * LK];
+                    }
+            st<T>(a.dx, vaddr<MODE>(a, b, k, gy, gx), acc);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// per-workgroup partials: thread t < 216 -> (tap = t / 8, o = t % 8) of dw; 216..223 -> dbias[o]
+template <typename T, int MODE>
+__global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) {
+    constexpr int TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
+    __shared__ float sv[LY * LX * LK];         // [yy][xx][kk] with halo
+    __shared__ float sg[TY * TX * ND * DC];    // [p][o][dl], zero where out of range
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int t = threadIdx.x;
+    const int o = t % ND, tap = t / ND, dz = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
+    float acc = 0.0f;
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC;
+        __syncthreads();
+        for (int e = t; e < LY * LX * LK; e += NTH) {
+            const int kk = e % LK, rest = e / LK, xx = rest % LX, yy = rest / LX;
+            const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+            const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
+            sv[e] = in ? ld<T>(a.x, vaddr<MODE>(a, b, gk, gy, gx)) : 0.0f;
+        }
+        for (int e = t; e < TY * TX * ND * DC; e += NTH) {
+            const int kl = e % DC, r1 = e / DC, oo = r1 % ND, p = r1 / ND, py = p / TX, px = p % TX;
+            const int gk = k0 + kl, gy = y0 + py, gx = x0 + px;
+            const bool in = gk < a.K && gy < a.Hv && gx < a.Wv;
+            sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, oo, gk, gy, gx)) : 0.0f;
+        }
+        __syncthreads();
+        if (t < 27 * ND) {
+#pragma unroll 4
+            for (int p = 0; p < TY * TX; ++p) {
+                const int py = p / TX, px = p % TX;
+                const float* g = sg + (p * ND + o) * DC;
+                const float* v = sv + ((py + dy) * LX + (px + dx)) * LK + dz;
+#pragma unroll
+                for (int kl = 0; kl < DC; ++kl) acc += g[kl] * v[kl];
+            }
+        } else if (t < 27 * ND + ND) {
+            const int ob = t - 27 * ND;
+            for (int p = 0; p < TY * TX; ++p) {
+                const float* g = sg + (p * ND + ob) * DC;
+#pragma unroll
+                for (int kl = 0; kl < DC; ++kl) acc += g[kl];
+            }
+        }
+    }
+    const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (t < 27 * ND + ND) a.ws[blk * (27 * ND + ND) + t] = acc;
+}
+
+// fixed-order fp64 reduction of the partials -> dw [o][tap], dbias [o]: one workgroup per output
+// (strided fp64 partial sums per thread, then the wave butterflies and the 4 waves in order)
+__global__ __launch_bounds__(NTH) void k_p3d_reduce_w(const float* ws, int64_t nblk, float* dw, float* db) {
+    __shared__ double red[NTH / 64];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    double s = 0.0;
+    for (int64_t i = tid; i < nblk; i += NTH) s += (double)ws[i * (27 * ND + ND) + t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = s;
+    __syncthreads();
+    if (tid != 0) return;
+    const double v = ((red[0] + red[1]) + red[2]) + red[3];
+    if (t < 27 * ND) {
+        if (dw) dw[(t % ND) * 27 + t / ND] = (float)v;
+    } else if (db) {
+        db[t - 27 * ND] = (float)v;
+    }
+}
+
+// workgroups along the channel axis: enough to fill the chip when the image is small
+int k_groups(int K, int DC, int tiles) {
+    const int nch = (K + DC - 1) / DC;
+    return std::max(1, std::min(nch, (2048 + tiles - 1) / std::max(tiles, 1)));
+}
+
+int check_desc(const psfm_p3d_desc* t) {
+    if (!t) return fail(-1, "null descriptor");
+    if (t->mode != PSFM_P3D_PACK && t->mode != PSFM_P3D_UNPACK) return fail(-2, "bad mode");
+    if (t->dtype != PSFM_P3D_F32 && t->dtype != PSFM_P3D_BF16) return fail(-2, "bad dtype");
+    if (t->B < 1 || t->C < 1 || t->Hv < 1 || t->Wv < 1 || t->r < 1) return fail(-3, "bad shape");
+    if (t->d != ND) return fail(-4, "d (3-D features) must be 8");
+    if (t->mode == PSFM_P3D_UNPACK && (ND * t->C) % (t->r * t->r)) return fail(-3, "d*C not divisible by r^2");
+    return 0;
+}
+
+P3 make(const psfm_p3d_desc* t) {
+    P3 a{};
+    a.B = t->B;
+    a.C = t->C;
+    a.Hv = t->Hv;
+    a.Wv = t->Wv;
+    a.r = t->r;
+    a.K = t->mode == PSFM_P3D_PACK ? t->C * t->r * t->r : t->C;
+    for (int i = 0; i < 4; ++i) {
+        a.xs[i] = t->xs[i];
+        a.ys[i] = t->ys[i];
+    }
+    return a;
+}
+
+#define P3D_LAUNCH(KERNEL, grid, st, a, t)                                                              \
+    do {                                                                                                \
+        if ((t)->dtype == PSFM_P3D_BF16) {                                                              \
+            if ((t)->mode == PSFM_P3D_PACK)                                                             \
+                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);       \
+            else                                                                                        \
+                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);     \
+        } else {                                                                                        \
+            if ((t)->mode == PSFM_P3D_PACK)                                                             \
+                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);          \
+            else                                                                                        \
+                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);        \
+        }                                                                                               \
+    } while (0)
+
+dim3 grid_of(P3& a, int TY, int TX, int DC) {
+    const int gx = (a.Wv + TX - 1) / TX, gy = (a.Hv + TY - 1) / TY;
+    a.KG = k_groups(a.K, DC, gx * gy * a.B);
+    return dim3(gx, gy, a.B * a.KG);
+}
+
+}  // namespace
+
+extern "C" {
+
+int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const float* bias, void* y, void* stream) {
+    if (int e = check_desc(t)) return e;
+    if (!x || !w || !y) return fail(-1, "null pointer");
+    P3 a = make(t);
+    a.x = x;
+    a.y = y;
+    a.w = w;
+    a.bias = bias;
+    const dim3 grid = grid_of(a, 4, 16, 32);
+    P3D_LAUNCH(k_p3d_fwd, grid, (hipStream_t)stream, a, t);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail((int)e, std::string("launch: ") + hipGetErrorString(e));
+}
+
+int64_t psfm_p3d_ws_floats(const psfm_p3d_desc* t) {
+    if (check_desc(t)) return -1;
+    P3 a = make(t);
+    const dim3 g = grid_of(a, 4, 16, 16);
+    return (int64_t)g.x * g.y * g.z * (27 * ND + ND);
+}
+
+int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const void* dy, void* dx, float* dw,
+                 float* dbias, float* ws, void* stream) {
+    if (int e = check_desc(t)) return e;
+    if (!x || !w || !dy) return fail(-1, "null pointer");
+    if ((dw || dbias) && !ws) return fail(-1, "weight gradient needs the workspace");
+    hipStream_t st = (hipStream_t)stream;
+    P3 a = make(t);
+    a.x = x;
+    a.dy = dy;
+    a.dx = dx;
+    a.w = w;
+    if (dx) {
+        const dim3 grid = grid_of(a, 4, 8, 16);
+        P3D_LAUNCH(k_p3d_bwd_x, grid, st, a, t);
+    }
+    if (dw || dbias) {
+        P3 aw = make(t);
+        aw.x = x;
+        aw.dy = dy;
+        aw.ws = ws;
+        const dim3 grid = grid_of(aw, 4, 16, 16);
+        P3D_LAUNCH(k_p3d_bwd_w, grid, st, aw, t);
+        hipLaunchKernelGGL(k_p3d_reduce_w, dim3(27 * ND + ND), dim3(NTH), 0, st, (const float*)ws,
+                           (int64_t)grid.x * grid.y * grid.z, dw, dbias);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail((int)e, std::string("launch: ") + hipGetErrorString(e));
+}
+
+const char* psfm_p3d_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

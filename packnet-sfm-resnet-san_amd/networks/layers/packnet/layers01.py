@@ -1,13 +1,15 @@
 """PackNet building blocks (packnet_sfm/networks/layers/packnet/layers01.py:10-286), PyTorch-ROCm
 (MIOpen convolutions).  Parameter names match the reference so its checkpoints load as-is.
 
-`packing` (space-to-depth) is a pure index permutation; the fused pack+Conv3d HIP op is the
-SURVEY §8f "next" row 1.
+`packing` (space-to-depth) is a pure index permutation; on a ROCm device the pack / unpack
+3-D convolutions run as one fused HIP kernel per direction (pack3d.py, include/psfm_pack3d.h).
 """
 from functools import partial
 
 import torch
 import torch.nn as nn
+
+from .pack3d import conv3d_unpack, pack_conv3d
 
 
 class Conv2D(nn.Module):
@@ -100,11 +102,10 @@ class PackLayerConv3d(nn.Module):
         self.conv = Conv2D(in_channels * (r ** 2) * d, in_channels, kernel_size, 1)
         self.pack = partial(packing, r=r)
         self.conv3d = _conv3d_d(d)
+        self.r = r
 
     def forward(self, x):
-        x = self.conv3d(self.pack(x).unsqueeze(1))
-        b, c, d, h, w = x.shape
-        return self.conv(x.reshape(b, c * d, h, w))
+        return self.conv(pack_conv3d(x, self.conv3d, self.r, self.pack))
 
 
 class UnpackLayerConv3d(nn.Module):
@@ -115,8 +116,7 @@ class UnpackLayerConv3d(nn.Module):
         self.conv = Conv2D(in_channels, out_channels * (r ** 2) // d, kernel_size, 1)
         self.unpack = nn.PixelShuffle(r)
         self.conv3d = _conv3d_d(d)
+        self.r = r
 
     def forward(self, x):
-        x = self.conv3d(self.conv(x).unsqueeze(1))
-        b, c, d, h, w = x.shape
-        return self.unpack(x.reshape(b, c * d, h, w))
+        return conv3d_unpack(self.conv(x), self.conv3d, self.r, self.unpack)

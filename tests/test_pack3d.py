@@ -1,0 +1,92 @@
+"""GPU parity of the fused PackNet pack / unpack 3-D convolution (include/psfm_pack3d.h;
+reference packnet_sfm/networks/layers/packnet/layers01.py:126-146, :189-282) against the
+reference op chain (packing / Conv3d / view / PixelShuffle) evaluated in float64 on the CPU, for
+the forward and all three gradients (input, weight, bias).
+
+Tolerances: fp32 storage 1e-5 * max|ref| per element; bf16 storage (inputs rounded to bf16 for
+both sides, fp32 accumulation) 1e-2 * max|ref| on the bf16 outputs and input gradient, 2e-3
+relative on the fp32-accumulated weight / bias gradients."""
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import __graft_entry__
+    __graft_entry__.build()
+    return torch.device("cuda:0")
+
+
+def _ref(mode, x, w, b, r):
+    from packnet_sfm_amd.networks.layers.packnet.layers01 import packing
+    conv = nn.Conv3d(1, 8, 3, 1, 1).double()
+    with torch.no_grad():
+        conv.weight.copy_(w.double())
+        conv.bias.copy_(b.double())
+    xd = x.detach().double().requires_grad_(True)
+    v = packing(xd, r) if mode == 0 else xd
+    y = conv(v.unsqueeze(1))
+    B, c, d, h, ww = y.shape
+    y = y.reshape(B, c * d, h, ww)
+    if mode == 1:
+        y = nn.PixelShuffle(r)(y)
+    return xd, conv, y
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,cl", [((2, 5, 14, 38), True), ((1, 16, 24, 40), False), ((2, 3, 6, 70), True)])
+def test_matches_reference_chain(dev, mode, dtype, shape, cl):
+    from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
+    g = torch.Generator().manual_seed(sum(shape) + mode)
+    B, C, H, W = shape
+    if mode == 1:
+        C = C * 4 // 4 * 2  # d*C divisible by r^2 = 4 (d = 8: always)
+    x = torch.randn(B, C, H, W, generator=g).to(dtype)
+    w = (torch.randn(8, 1, 3, 3, 3, generator=g) * 0.2)
+    b = torch.randn(8, generator=g) * 0.1
+    xd, conv, yref = _ref(mode, x.float(), w, b, 2)
+    gy = torch.randn(yref.shape, generator=g).to(dtype).float()   # the upstream gradient in storage dtype
+    (yref * gy.double()).sum().backward()
+    xg = x.to(dev)
+    if cl:
+        xg = xg.contiguous(memory_format=torch.channels_last)
+    xg.requires_grad_(True)
+    wg = w.to(dev).requires_grad_(True)
+    bg = b.to(dev).requires_grad_(True)
+    y = Pack3dFn.apply(xg, wg, bg, mode, 2)
+    (y.float() * gy.to(dev)).sum().backward()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    for got, ref in ((y, yref), (xg.grad, xd.grad)):
+        err = (got.double().cpu() - ref).abs().max().item()
+        assert err <= tol * ref.abs().max().item(), (err, ref.abs().max().item())
+    wtol = 1e-5 if dtype == torch.float32 else 2e-3
+    for got, ref in ((wg.grad, conv.weight.grad), (bg.grad, conv.bias.grad)):
+        assert (got.double().cpu() - ref).abs().max().item() <= wtol * ref.abs().max().item()
+
+
+def test_pack_layers_use_fused_op_and_match_torch(dev):
+    """PackLayerConv3d / UnpackLayerConv3d on the device (fused) == the same modules' torch chain"""
+    from packnet_sfm_amd.networks.layers.packnet import pack3d
+    from packnet_sfm_amd.networks.layers.packnet.layers01 import PackLayerConv3d, UnpackLayerConv3d
+    torch.manual_seed(0)
+    for mod, shape in ((PackLayerConv3d(16, 3), (2, 16, 16, 32)), (UnpackLayerConv3d(32, 32, 3), (2, 32, 8, 16))):
+        mod = mod.to(dev)
+        x = torch.randn(shape, device=dev)
+        pack3d.ENABLED = False
+        ref = mod(x)
+        pack3d.ENABLED = True
+        got = mod(x)
+        assert (got - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            pack3d.ENABLED = False
+            ref16 = mod(x)
+            pack3d.ENABLED = True
+            got16 = mod(x)
+        assert got16.dtype == ref16.dtype
+        assert (got16.float() - ref16.float()).abs().max().item() <= 3e-2 * ref16.float().abs().max().item()
