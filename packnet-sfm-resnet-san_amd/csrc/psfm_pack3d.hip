@@ -30,6 +30,9 @@ int fail(int code, const std::string& msg) {
 }
 
 constexpr int NTH = 256;
+#ifndef PSFM_P3D_WAVES
+#define PSFM_P3D_WAVES 2
+#endif
 constexpr int ND = 8;  // Conv3d output features (PackNet d = 8)
 
 struct P3 {
@@ -95,7 +98,7 @@ __device__ __forceinline__ void load_weights(const P3& a, float* sw) {
 
 // --------------------------------------------------------------------------------------------
 template <typename T, int MODE>
-__global__ __launch_bounds__(NTH) void k_p3d_fwd(P3 a) {
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WAVES))) void k_p3d_fwd(P3 a) {
     constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sv[LY * LX * LK];
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_fwd(P3 a) {
 // --------------------------------------------------------------------------------------------
 // dV[k, y, x] = sum_o sum_taps w[o, dz, dy, dx] dy[o, k - dz + 1, y - dy + 1, x - dx + 1]
 template <typename T, int MODE>
-__global__ __launch_bounds__(NTH) void k_p3d_bwd_x(P3 a) {
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WAVES))) void k_p3d_bwd_x(P3 a) {
     constexpr int TY = 4, TX = 8, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sg[LY * LX * ND * LK];  // [yy][xx][o][kk]
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];

@@ -8,12 +8,15 @@ from functools import partial
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .pack3d import conv3d_unpack, pack_conv3d
 
 
 class Conv2D(nn.Module):
-    """zero-pad(k//2) -> Conv2d -> GroupNorm(16) -> ELU."""
+    """zero-pad(k//2) -> Conv2d -> GroupNorm(16) -> ELU.  The zero padding is the convolution's
+    own (`padding=k//2`, identical arithmetic to ConstantPad2d + unpadded conv, layers01.py:34-39)
+    instead of a padded copy of the input; `pad` is kept as the (parameter-free) module."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride):
         super().__init__()
@@ -24,7 +27,8 @@ class Conv2D(nn.Module):
         self.activ = nn.ELU(inplace=True)
 
     def forward(self, x):
-        return self.activ(self.normalize(self.conv_base(self.pad(x))))
+        c = self.conv_base
+        return self.activ(self.normalize(F.conv2d(x, c.weight, c.bias, c.stride, self.kernel_size // 2)))
 
 
 class ResidualConv(nn.Module):
