@@ -89,8 +89,8 @@ def to_channels_last(model):
     (5-D) stay as they are (Module.to(memory_format=...) refuses a model that has them)."""
     with torch.no_grad():
         for p in model.parameters():
-            if p.dim() == 4:
-                p.data = p.data.contiguous(memory_format=torch.channels_last)
+            if p.dim() == 4:   # explicit NHWC strides (also for 1x1 kernels, as Module.to does)
+                p.data = torch.empty_like(p.data, memory_format=torch.channels_last).copy_(p.data)
     return model
 
 
