@@ -51,6 +51,19 @@ class MetricsParams(ctypes.Structure):
                 ("crop_garg", c_int), ("use_gt_scale", c_int)]
 
 
+class Jitter(ctypes.Structure):
+    """psfm_jitter (include/psfm_augment.h)."""
+    _fields_ = [("apply", c_int), ("order", c_int * 4), ("factor", c_float * 3), ("hue_shift", c_int),
+                ("use_matrix", c_int), ("matrix", c_float * 3)]
+
+
+class AugmentParams(ctypes.Structure):
+    """psfm_augment_params (include/psfm_augment.h)."""
+    _fields_ = [("n_samples", c_int), ("n_img", c_int), ("src_h", c_int), ("src_w", c_int),
+                ("src_stride", ctypes.c_longlong), ("crop_l", c_int), ("crop_t", c_int), ("crop_r", c_int),
+                ("crop_b", c_int), ("out_h", c_int), ("out_w", c_int)]
+
+
 _lib = None
 
 
@@ -110,6 +123,11 @@ def lib():
         # include/psfm_metrics.h
         "psfm_depth_metrics": ([ctypes.POINTER(MetricsParams), V, V, V, V, V], c_int),
         "psfm_metrics_last_error": ([], ctypes.c_char_p),
+        # include/psfm_augment.h
+        "psfm_augment_plan": ([ctypes.POINTER(AugmentParams), V], ctypes.c_longlong),
+        "psfm_augment_ws_bytes": ([ctypes.POINTER(AugmentParams)], c_size_t),
+        "psfm_train_augment": ([ctypes.POINTER(AugmentParams), V, V, V, V, V, V, V], c_int),
+        "psfm_augment_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -127,7 +145,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
             "psfm_depth_metrics", "psfm_metrics_last_error",
-            "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error")
+            "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
+            "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error")
 
 
 def check(rc, what):
@@ -138,6 +157,8 @@ def check(rc, what):
             err = lib().psfm_netops_last_error
         elif what.startswith("psfm_depth_metrics"):
             err = lib().psfm_metrics_last_error
+        elif what.startswith(("psfm_augment", "psfm_train_augment")):
+            err = lib().psfm_augment_last_error
         elif what.startswith("psfm_p3d"):
             err = lib().psfm_p3d_last_error
         else:

@@ -19,7 +19,7 @@ def hip():
 
 def declared_functions():
     names = set()
-    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h", "psfm_pack3d.h"):
+    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h", "psfm_pack3d.h", "psfm_augment.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src))
