@@ -18,6 +18,7 @@
 // precision HSV conversion, IEEE division for ToTensor.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -28,6 +29,7 @@ namespace {
 
 constexpr int PREC = 22;  // Resample.c PRECISION_BITS (8-bit images)
 constexpr int NT = 256;
+constexpr int KM = 16;  // fixed-trip (predicated) tap loops up to KM taps
 constexpr int PLAN_HDR = 8;  // kh, kv, rows_tmp, off_bh, off_ch, off_bv, off_cv, y0
 constexpr int MAX_CROP_W = 16384;
 
@@ -56,8 +58,9 @@ int plan_ksize(int in, int out) {
     return (int)std::ceil(3.0 * fs) * 2 + 1;
 }
 
-// bounds [out][2] (first tap, count), coeffs [out][ksize]; either may be null
-void plan_dir(int in, int out, int32_t* bounds, int32_t* coeffs) {
+// bounds [out][2] (first tap, count), coeffs [out][ksize] (or [ksize][out] when tap_major: the
+// horizontal pass reads one tap of 64 consecutive outputs per wave instruction); either may be null
+void plan_dir(int in, int out, int32_t* bounds, int32_t* coeffs, bool tap_major = false) {
     const int ks = plan_ksize(in, out);
     if (in == out) {
         for (int i = 0; i < out; ++i) {
@@ -87,7 +90,7 @@ void plan_dir(int in, int out, int32_t* bounds, int32_t* coeffs) {
         for (; x < ks; ++x) k[x] = 0;
         if (coeffs)
             for (x = 0; x < ks; ++x)
-                coeffs[xx * ks + x] = k[x] < 0 ? (int32_t)(-0.5 + k[x] * (1 << PREC))
+                coeffs[tap_major ? (size_t)x * out + xx : (size_t)xx * ks + x] = k[x] < 0 ? (int32_t)(-0.5 + k[x] * (1 << PREC))
                                                 : (int32_t)(0.5 + k[x] * (1 << PREC));
         if (bounds) { bounds[2 * xx] = xmin; bounds[2 * xx + 1] = xmax; }
     }
@@ -144,6 +147,7 @@ WsLayout ws_layout(const psfm_augment_params* p, const Dims& d) {
     return w;
 }
 
+
 // ---------------------------------------------------------------------------------------------
 // device: Pillow's 8-bit pixel arithmetic
 // ---------------------------------------------------------------------------------------------
@@ -164,8 +168,26 @@ __device__ __forceinline__ int rgb2l(int r, int g, int b) {
 }
 __device__ __forceinline__ int clip8i(int v) { return v <= 0 ? 0 : v >= 255 ? 255 : v; }
 
+// hsv2rgb's per-byte quantities (Convert.c), computed once per workgroup with the reference's
+// double expressions: i(h) = floor(h * 6.0 / 255.0), f(h) = (float)(h * 6.0 / 255.0 - i),
+// fs(s) = (float)(s / 255.0).
+struct HueTables {
+    float f[256], fs[256];
+    int i[256];
+};
+__device__ __forceinline__ void fill_hue_tables(HueTables& t) {
+#pragma clang fp contract(off)
+    for (int v = threadIdx.x; v < 256; v += blockDim.x) {
+        const double x = (double)(float)v * 6.0 / 255.0;
+        const int i = (int)floor(x);
+        t.i[v] = i;
+        t.f[v] = (float)(x - (double)(float)i);
+        t.fs[v] = (float)((double)(float)v / 255.0);
+    }
+}
+
 // Convert.c rgb2hsv_row -> h += shift (uint8) -> hsv2rgb
-__device__ __noinline__ void hue_shift(int& R, int& G, int& B, int shift) {
+__device__ __forceinline__ void hue_shift(int& R, int& G, int& B, int shift, const HueTables& T) {
 #pragma clang fp contract(off)
     const int r = R, g = G, b = B;
     const int maxc = max(r, max(g, b)), minc = min(r, min(g, b));
@@ -174,12 +196,15 @@ __device__ __noinline__ void hue_shift(int& R, int& G, int& B, int shift) {
     if (minc != maxc) {
         const float cr = (float)(maxc - minc);
         const float s = cr / (float)maxc;
-        const float rc = ((float)(maxc - r)) / cr, gc = ((float)(maxc - g)) / cr, bc = ((float)(maxc - b)) / cr;
         float h;
-        if (r == maxc) h = bc - gc;
-        else if (g == maxc) h = (float)(2.0 + rc - bc);
-        else h = (float)(4.0 + gc - rc);
-        h = (float)fmod(((double)h / 6.0 + 1.0), 1.0);
+        if (r == maxc) h = ((float)(maxc - b)) / cr - ((float)(maxc - g)) / cr;
+        else if (g == maxc) h = (float)(2.0 + (double)(((float)(maxc - r)) / cr) - (double)(((float)(maxc - b)) / cr));
+        else h = (float)(4.0 + (double)(((float)(maxc - g)) / cr) - (double)(((float)(maxc - r)) / cr));
+        // fmod(h / 6.0 + 1.0, 1.0) with h in [-1, 5]: the argument lies in [5/6, 11/6), where
+        // fmod is the exact subtraction of 1 (Sterbenz) — no libm loop
+        double y = (double)h / 6.0 + 1.0;
+        if (y >= 1.0) y -= 1.0;
+        h = (float)y;
         uh = clip8i((int)((double)h * 255.0));
         us = clip8i((int)((double)s * 255.0));
     }
@@ -188,12 +213,12 @@ __device__ __noinline__ void hue_shift(int& R, int& G, int& B, int shift) {
         R = G = B = v;
         return;
     }
-    const int i = (int)floor((double)(float)h * 6.0 / 255.0);
-    const float f = (float)((double)(float)h * 6.0 / 255.0 - (double)(float)i);
-    const float fs = (float)((double)(float)s / 255.0);
-    const int p = clip8i((int)round((double)(float)v * (1.0 - (double)fs)));
-    const int q = clip8i((int)round((double)(float)v * (1.0 - (double)(fs * f))));
-    const int t = clip8i((int)round((double)(float)v * (1.0 - (double)fs * (1.0 - (double)f))));
+    const int i = T.i[h];
+    const float f = T.f[h], fs = T.fs[s];
+    const double dv = (double)(float)v;
+    const int p = clip8i((int)round(dv * (1.0 - (double)fs)));
+    const int q = clip8i((int)round(dv * (1.0 - (double)(fs * f))));
+    const int t = clip8i((int)round(dv * (1.0 - (double)fs * (1.0 - (double)f))));
     switch (i % 6) {
         case 0: R = v; G = t; B = p; break;
         case 1: R = q; G = v; B = p; break;
@@ -204,16 +229,25 @@ __device__ __noinline__ void hue_shift(int& R, int& G, int& B, int shift) {
     }
 }
 
-__device__ __forceinline__ void apply_op(int op, int& r, int& g, int& b, const psfm_jitter& j, int mean) {
-    if (op == PSFM_JIT_BRIGHTNESS) {  // ImageEnhance.Brightness: blend(black, img, f)
-        r = blend(0, r, j.factor[0]); g = blend(0, g, j.factor[0]); b = blend(0, b, j.factor[0]);
-    } else if (op == PSFM_JIT_CONTRAST) {  // ImageEnhance.Contrast: blend(mean L, img, f)
-        r = blend(mean, r, j.factor[1]); g = blend(mean, g, j.factor[1]); b = blend(mean, b, j.factor[1]);
-    } else if (op == PSFM_JIT_SATURATION) {  // ImageEnhance.Color: blend(L, img, f)
-        const int l = rgb2l(r, g, b);
-        r = blend(l, r, j.factor[2]); g = blend(l, g, j.factor[2]); b = blend(l, b, j.factor[2]);
+template <int V>
+__device__ __forceinline__ void apply_op_v(int op, int (&c)[3][V], const psfm_jitter& j, int mean, const HueTables& T) {
+    if (op == PSFM_JIT_HUE) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) hue_shift(c[0][e], c[1][e], c[2][e], j.hue_shift, T);
+    } else if (op == PSFM_JIT_SATURATION) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const int l = rgb2l(c[0][e], c[1][e], c[2][e]);
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) c[ch][e] = blend(l, c[ch][e], j.factor[2]);
+        }
     } else {
-        hue_shift(r, g, b, j.hue_shift);
+        const int a = op == PSFM_JIT_CONTRAST ? mean : 0;
+        const float f = op == PSFM_JIT_CONTRAST ? j.factor[1] : j.factor[0];
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) c[ch][e] = blend(a, c[ch][e], f);
     }
 }
 
@@ -236,10 +270,12 @@ struct Geo {
 // ---------------------------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(NT) k_resize_h(Geo g, const uint8_t* __restrict__ src,
-                                                 const int32_t* __restrict__ plan, uint8_t* __restrict__ tmp) {
+// One workgroup (a multiple of 64 threads, up to 1024: one output column per thread at KITTI
+// width) per intermediate row.
+__global__ void __launch_bounds__(1024) k_resize_h(Geo g, const uint8_t* __restrict__ src,
+                                                   const int32_t* __restrict__ plan, uint8_t* __restrict__ tmp) {
     extern __shared__ uint8_t seg[];  // [seg_len * 3] bytes of the source row segment
-    const int r = blockIdx.x, img = blockIdx.y, tid = threadIdx.x;
+    const int r = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
     const int sy = g.crop_t + g.y0 + r;  // source row
     const int nbytes = 3 * g.seg_len;
     const int sx0 = g.crop_l + g.seg0;  // source column of seg[0]
@@ -255,26 +291,36 @@ __global__ void __launch_bounds__(NT) k_resize_h(Geo g, const uint8_t* __restric
     const uintptr_t base = (uintptr_t)row;
     const long long w0 = (long long)((base + lo) >> 2);
     const long long w1 = hi > lo ? (long long)((base + hi - 1) >> 2) + 1 : w0;
-    for (long long w = w0 + tid; w < w1; w += NT) {
+    const long long wb = (long long)(base >> 2);  // word holding seg[0] (seg is 4-byte aligned)
+    const int shift = (int)(base & 3);
+    for (long long w = w0 + tid; w < w1; w += nt) {
         const uint32_t v = *(const uint32_t*)(uintptr_t)(w << 2);
+        const long long o0 = ((w - wb) << 2) - shift;  // segment offset of the word's byte 0
+        if (o0 >= lo && o0 + 3 < hi) {
+            // whole word inside [lo, hi): four byte writes at consecutive LDS addresses
+            seg[o0] = (uint8_t)v; seg[o0 + 1] = (uint8_t)(v >> 8);
+            seg[o0 + 2] = (uint8_t)(v >> 16); seg[o0 + 3] = (uint8_t)(v >> 24);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const long long o = (w << 2) + k - (long long)base;
-            if (o >= lo && o < hi) seg[o] = (uint8_t)(v >> (8 * k));
+            for (int k = 0; k < 4; ++k) {
+                const long long o = o0 + k;
+                if (o >= lo && o < hi) seg[o] = (uint8_t)(v >> (8 * k));
+            }
         }
     }
-    for (int o = tid; o < nbytes; o += NT)
-        if (o < lo || o >= hi) seg[o] = 0;
+    for (int o = tid; o < lo; o += nt) seg[o] = 0;
+    for (int o = hi + tid; o < nbytes; o += nt) seg[o] = 0;
     __syncthreads();
     const int32_t* bh = plan + g.off_bh;
-    const int32_t* ch = plan + g.off_ch;
+    const int32_t* ch = plan + g.off_ch;  // [out_w][kh]
     const size_t plane = (size_t)g.rows_tmp * g.out_w;
     uint8_t* out = tmp + (size_t)img * 3 * plane + (size_t)r * g.out_w;
-    for (int x = tid; x < g.out_w; x += NT) {
+    for (int x = tid; x < g.out_w; x += nt) {
         const int xmin = bh[2 * x] - g.seg0, xn = bh[2 * x + 1];
-        const int32_t* k = ch + (size_t)x * g.kh;
         int32_t s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
-        const uint8_t* px = seg + 3 * xmin;
+        const uint8_t* px = seg + 3 * xmin;  // byte reads: no unpacking VALU
+        const int32_t* k = ch + (size_t)x * g.kh;
+#pragma unroll 4
         for (int t = 0; t < xn; ++t) {
             const int32_t c = k[t];
             s0 += px[3 * t] * c;
@@ -287,104 +333,201 @@ __global__ void __launch_bounds__(NT) k_resize_h(Geo g, const uint8_t* __restric
     }
 }
 
-__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red) {
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) red[wv] = v;
     __syncthreads();
-    uint32_t s = 0;
+    T s = 0;
     if (threadIdx.x == 0)
         for (int i = 0; i < NT / 64; ++i) s += red[i];
     return s;
 }
 
+template <int V> struct Vec;
+template <> struct Vec<1> { typedef uint8_t u8; typedef float f32; };
+template <> struct Vec<4> { typedef uint32_t u8; typedef float4 f32; };
+
+__device__ __forceinline__ void unpack(uint8_t v, int* o) { o[0] = v; }
+__device__ __forceinline__ void unpack(uint32_t v, int* o) {
+    o[0] = v & 255; o[1] = (v >> 8) & 255; o[2] = (v >> 16) & 255; o[3] = v >> 24;
+}
+__device__ __forceinline__ void pack(const int* o, uint8_t& v) { v = (uint8_t)o[0]; }
+__device__ __forceinline__ void pack(const int* o, uint32_t& v) {
+    v = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+}
+// ToTensor through a 256-entry LDS table of the IEEE quotients u / 255.0f (u * (1/255) is not
+// exact for 126 of the 256 bytes)
+__device__ __forceinline__ void fill_u2f(float* t) {
+    for (int v = threadIdx.x; v < 256; v += blockDim.x) t[v] = to_float(v);
+}
+__device__ __forceinline__ void tofloat(const int* o, float& v, const float* t) { v = t[o[0]]; }
+__device__ __forceinline__ void tofloat(const int* o, float4& v, const float* t) {
+    v = make_float4(t[o[0]], t[o[1]], t[o[2]], t[o[3]]);
+}
+
+// V consecutive output pixels of one row per thread (V = 4 when out_w % 4 == 0: dword byte
+// loads, float4 stores).  Vertical pass, rgb_original, and (jittering) the resized bytes + the
+// contrast prefix's L sums.
+template <int V>
 __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restrict__ plan,
                                                  const uint8_t* __restrict__ tmp, const psfm_jitter* __restrict__ jit,
                                                  float* __restrict__ orig, uint8_t* __restrict__ resized,
                                                  uint32_t* __restrict__ part) {
+    typedef typename Vec<V>::u8 U8;
+    typedef typename Vec<V>::f32 F32;
     __shared__ uint32_t red[NT / 64];
+    __shared__ HueTables T;
+    __shared__ float u2f[256];
     const int img = blockIdx.y, tid = threadIdx.x;
     const int hw = g.out_h * g.out_w;
-    const int pidx = blockIdx.x * NT + tid;
+    const int pidx = (blockIdx.x * NT + tid) * V;
+    fill_u2f(u2f);
+    __syncthreads();
     const bool live = pidx < hw;
-    int v[3] = {0, 0, 0};
+    int v[3][V];
     if (live) {
         const int y = pidx / g.out_w, x = pidx - y * g.out_w;
         const int ymin = plan[g.off_bv + 2 * y], yn = plan[g.off_bv + 2 * y + 1];
         const int32_t* k = plan + g.off_cv + (size_t)y * g.kv;
         const size_t plane = (size_t)g.rows_tmp * g.out_w;
         const uint8_t* col = tmp + (size_t)img * 3 * plane + (size_t)ymin * g.out_w + x;
-        int32_t s0 = 1 << (PREC - 1), s1 = s0, s2 = s0;
-        for (int t = 0; t < yn; ++t) {
-            const int32_t c = k[t];
-            const uint8_t* q = col + (size_t)t * g.out_w;
-            s0 += q[0] * c;
-            s1 += q[plane] * c;
-            s2 += q[2 * plane] * c;
+        int32_t s[3][V];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int e = 0; e < V; ++e) s[c][e] = 1 << (PREC - 1);
+        if (g.kv <= KM) {
+            // every tap's loads issued at once (predicated, fixed trip count)
+            U8 raw[KM][3];
+#pragma unroll
+            for (int t = 0; t < KM; ++t)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    raw[t][c] = t < yn ? *(const U8*)(col + (size_t)t * g.out_w + c * plane) : (U8)0;
+#pragma unroll
+            for (int t = 0; t < KM; ++t) {
+                const int32_t cf = t < yn ? k[t] : 0;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    int u[V];
+                    unpack(raw[t][c], u);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) s[c][e] += u[e] * cf;
+                }
+            }
+        } else {
+            for (int t = 0; t < yn; ++t) {
+                const int32_t cf = k[t];
+                const uint8_t* q = col + (size_t)t * g.out_w;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    int u[V];
+                    unpack(*(const U8*)(q + c * plane), u);
+#pragma unroll
+                    for (int e = 0; e < V; ++e) s[c][e] += u[e] * cf;
+                }
+            }
         }
-        v[0] = clip8_fixed(s0); v[1] = clip8_fixed(s1); v[2] = clip8_fixed(s2);
         float* o = orig + (size_t)img * 3 * hw + pidx;
-        o[0] = to_float(v[0]);
-        o[hw] = to_float(v[1]);
-        o[2 * (size_t)hw] = to_float(v[2]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) v[c][e] = clip8_fixed(s[c][e]);
+            F32 f;
+            tofloat(v[c], f, u2f);
+            *(F32*)(o + (size_t)c * hw) = f;
+        }
     }
     if (!resized) return;  // no jitter requested (uniform)
-    if (live) {
-        uint8_t* q = resized + (size_t)img * 3 * hw + pidx;
-        q[0] = (uint8_t)v[0]; q[hw] = (uint8_t)v[1]; q[2 * (size_t)hw] = (uint8_t)v[2];
-    }
-    // L of the image as ImageEnhance.Contrast sees it: the ops before contrast applied first
+    // the ops before contrast (in the sample's shuffled order) run here, once: `resized` holds
+    // the image as ImageEnhance.Contrast receives it, and the workgroup's sum of its L values
     const psfm_jitter j = jit[img % g.n_samples];
-    if (!j.apply) return;  // uniform per workgroup
+    bool hue_first = false;
+    if (j.apply)
+        for (int k = 0; k < 4 && j.order[k] != PSFM_JIT_CONTRAST; ++k) hue_first |= j.order[k] == PSFM_JIT_HUE;
+    if (hue_first) {  // uniform
+        fill_hue_tables(T);
+        __syncthreads();
+    }
     uint32_t l = 0;
     if (live) {
-        int r = v[0], gg = v[1], b = v[2];
-        for (int k = 0; k < 4 && j.order[k] != PSFM_JIT_CONTRAST; ++k) apply_op(j.order[k], r, gg, b, j, 0);
-        l = (uint32_t)rgb2l(r, gg, b);
+        if (j.apply)
+            for (int k = 0; k < 4 && j.order[k] != PSFM_JIT_CONTRAST; ++k) apply_op_v<V>(j.order[k], v, j, 0, T);
+        uint8_t* q = resized + (size_t)img * 3 * hw + pidx;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            U8 w;
+            pack(v[c], w);
+            *(U8*)(q + (size_t)c * hw) = w;
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) l += (uint32_t)rgb2l(v[0][e], v[1][e], v[2][e]);
     }
+    if (!j.apply) return;  // uniform per workgroup
     const uint32_t s = block_sum(l, red);
     if (tid == 0) part[(size_t)img * gridDim.x + blockIdx.x] = s;
 }
 
+template <int V>
 __global__ void __launch_bounds__(NT) k_jitter(Geo g, const psfm_jitter* __restrict__ jit,
                                                const uint8_t* __restrict__ resized, const uint32_t* __restrict__ part,
                                                float* __restrict__ rgb) {
-    __shared__ uint32_t red[NT / 64];
+    typedef typename Vec<V>::u8 U8;
+    typedef typename Vec<V>::f32 F32;
+    __shared__ unsigned long long red[NT / 64];
     __shared__ int s_mean;
+    __shared__ HueTables T;
+    __shared__ float u2f[256];
     const int img = blockIdx.y, tid = threadIdx.x;
     const int hw = g.out_h * g.out_w;
     const int nblk = gridDim.x;
     const psfm_jitter j = jit[img % g.n_samples];
+    fill_u2f(u2f);
     int mean = 0;
     if (j.apply) {
-        // the whole image's L sum (exact integers; each partial <= 256 * 255)
-        uint32_t s = 0;
+        fill_hue_tables(T);
+        // the whole image's L sum (exact integers; each partial <= NT * V * 255)
+        unsigned long long s = 0;
         for (int i = tid; i < nblk; i += NT) s += part[(size_t)img * nblk + i];
-        const uint32_t tot = block_sum(s, red);
+        const unsigned long long tot = block_sum(s, red);
         if (tid == 0) {
             // int(sum / n + 0.5) == floor((2 sum + n) / 2n) exactly (ImageStat mean, Contrast)
             const unsigned long long n = (unsigned long long)hw;
             s_mean = (int)((2ULL * tot + n) / (2ULL * n));
         }
-        __syncthreads();
-        mean = s_mean;
     }
-    const int pidx = blockIdx.x * NT + tid;
+    __syncthreads();  // u2f, hue tables, s_mean
+    if (j.apply) mean = s_mean;
+    const int pidx = (blockIdx.x * NT + tid) * V;
     if (pidx >= hw) return;
     const uint8_t* q = resized + (size_t)img * 3 * hw + pidx;
-    int r = q[0], gg = q[hw], b = q[2 * (size_t)hw];
+    int c3[3][V];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) unpack(*(const U8*)(q + (size_t)c * hw), c3[c]);
     if (j.apply) {
-        for (int k = 0; k < 4; ++k) apply_op(j.order[k], r, gg, b, j, mean);
-        if (j.use_matrix) {
-            r = matrix_ch(j.matrix[0], r);
-            gg = matrix_ch(j.matrix[1], gg);
-            b = matrix_ch(j.matrix[2], b);
+        // from contrast on: the ops before it already ran in k_resize_v (constant indices only:
+        // a dynamically indexed record would live in scratch)
+        bool after = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            after |= j.order[k] == PSFM_JIT_CONTRAST;
+            if (after) apply_op_v<V>(j.order[k], c3, j, mean, T);
         }
+        if (j.use_matrix)
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) c3[ch][e] = matrix_ch(j.matrix[ch], c3[ch][e]);
     }
     float* o = rgb + (size_t)img * 3 * hw + pidx;
-    o[0] = to_float(r);
-    o[hw] = to_float(gg);
-    o[2 * (size_t)hw] = to_float(b);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        F32 f;
+        tofloat(c3[c], f, u2f);
+        *(F32*)(o + (size_t)c * hw) = f;
+    }
 }
 
 }  // namespace
@@ -430,14 +573,10 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     g.off_bh = (int)d.off_bh; g.off_ch = (int)d.off_ch; g.off_bv = (int)d.off_bv; g.off_cv = (int)d.off_cv;
     // the source columns the horizontal pass reads (host copy of the first / last bounds)
     {
-        int32_t b0[2], bl[2];
         std::vector<int32_t> bh(2 * (size_t)p->out_w);
         plan_dir(d.crop_w, p->out_w, bh.data(), nullptr);
-        b0[0] = bh[0];
-        bl[0] = bh[2 * (p->out_w - 1)];
-        bl[1] = bh[2 * (p->out_w - 1) + 1];
-        g.seg0 = b0[0];
-        g.seg_len = bl[0] + bl[1] - b0[0];
+        g.seg0 = bh[0];
+        g.seg_len = bh[2 * (p->out_w - 1)] + bh[2 * (p->out_w - 1) + 1] - bh[0];
     }
     hipStream_t st = (hipStream_t)stream;
     uint8_t* base = (uint8_t*)ws;
@@ -445,14 +584,24 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     uint8_t* resized = rgb ? base + wl.resized : nullptr;
     uint32_t* part = (uint32_t*)(base + wl.part);
     const int hw = p->out_h * p->out_w;
-    const int nblk = (hw + NT - 1) / NT;
+    const int vec = p->out_w % 4 == 0 ? 4 : 1;  // 4-pixel groups never straddle a row
+    const int nblk = (hw / vec + NT - 1) / NT;
     const size_t lds = (size_t)((3 * g.seg_len + 3) & ~3);
-    hipLaunchKernelGGL(k_resize_h, dim3(d.rows_tmp, p->n_img), dim3(NT), lds, st, g, src, plan, tmp);
-    hipLaunchKernelGGL(k_resize_v, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,
-                       rgb_original, resized, part);
-    if (rgb)
-        hipLaunchKernelGGL(k_jitter, dim3(nblk, p->n_img), dim3(NT), 0, st, g, jitter, (const uint8_t*)resized,
-                           (const uint32_t*)part, rgb);
+    const int nth = NT;
+    hipLaunchKernelGGL(k_resize_h, dim3(d.rows_tmp, p->n_img), dim3(nth), lds, st, g, src, plan, tmp);
+    if (vec == 4) {
+        hipLaunchKernelGGL(k_resize_v<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,
+                           rgb_original, resized, part);
+        if (rgb)
+            hipLaunchKernelGGL(k_jitter<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, jitter, (const uint8_t*)resized,
+                               (const uint32_t*)part, rgb);
+    } else {
+        hipLaunchKernelGGL(k_resize_v<1>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,
+                           rgb_original, resized, part);
+        if (rgb)
+            hipLaunchKernelGGL(k_jitter<1>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, jitter, (const uint8_t*)resized,
+                               (const uint32_t*)part, rgb);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail((int)e, std::string("launch: ") + hipGetErrorString(e));
     return 0;

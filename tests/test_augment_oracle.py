@@ -114,7 +114,8 @@ def test_plan_matches_oracle(hip, src, box, out):
     assert L.psfm_augment_plan(ctypes.byref(p), plan.ctypes.data_as(ctypes.c_void_p)) == n
     kh, kv, rows, obh, och, obv, ocv, y0 = (int(v) for v in plan[:8])
     cw, ch = box[2] - box[0], box[3] - box[1]
-    for (ins, outs, k, ob, oc, shift) in ((cw, out[1], kh, obh, och, 0), (ch, out[0], kv, obv, ocv, y0)):
+    for (ins, outs, k, ob, oc, shift, tap_major) in ((cw, out[1], kh, obh, och, 0, False),
+                                                     (ch, out[0], kv, obv, ocv, y0, False)):
         if ins == outs:
             assert k == 1
             continue
@@ -123,7 +124,8 @@ def test_plan_matches_oracle(hip, src, box, out):
         bb = plan[ob:ob + 2 * outs].reshape(outs, 2).copy()
         bb[:, 0] += shift
         np.testing.assert_array_equal(bb, b)
-        np.testing.assert_array_equal(plan[oc:oc + k * outs].reshape(outs, k), c)
+        cc = plan[oc:oc + k * outs].reshape(k, outs).T if tap_major else plan[oc:oc + k * outs].reshape(outs, k)
+        np.testing.assert_array_equal(cc, c)
     assert hip.lib().psfm_augment_ws_bytes(ctypes.byref(p)) > 0
 
 

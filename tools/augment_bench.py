@@ -26,6 +26,7 @@ ap.add_argument("--src", default="375x1242")
 ap.add_argument("--shape", default="192x640")
 ap.add_argument("--cpu-seconds", type=float, default=10.0)
 ap.add_argument("--no-cpu-baseline", action="store_true")
+ap.add_argument("--jitter", default="0.2,0.2,0.2,0.05", help="'none' = no colour jitter (rgb = copy)")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -39,7 +40,8 @@ g = np.random.default_rng(0)
 imgs_np = g.integers(0, 256, (n_img, h, w, 3), dtype=np.uint8)
 imgs = torch.from_numpy(imgs_np).to(dev)
 rng = random.Random(0)
-jit = [AUG.random_color_jitter_params((0.2, 0.2, 0.2, 0.05), 1.0, rng) for _ in range(B)]
+jpar = None if args.jitter == "none" else tuple(float(v) for v in args.jitter.split(","))
+jit = [AUG.random_color_jitter_params(jpar, 1.0 if jpar else 0.0, rng) for _ in range(B)]
 box = (0, 0, w, h)
 
 # warm-up / plan upload through the public API, then the raw C-ABI call on resident buffers
