@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -96,9 +97,36 @@ void plan_dir(int in, int out, int32_t* bounds, int32_t* coeffs, bool tap_major 
     }
 }
 
+// Per-byte tables, computed on the host with the reference's expressions (IEEE double / float:
+// bit-identical to evaluating them on the device):
+//   u2f[u] = u / 255.0f                                   ToTensor
+//   i[h] = floor(h * 6.0 / 255.0), f[h] = (float)(h * 6.0 / 255.0 - i), fs[s] = (float)(s / 255.0)
+//                                                         Convert.c hsv2rgb
+//   rcp[n] = 1.0 / n    (float)(a * rcp[n]) == a / (float)n exactly for 0 <= a <= n <= 255: the
+//                       double product is within 2^-52 of a / n, which is either a float or at
+//                       least 2^-32 (relative) away from every float rounding boundary
+struct Tables {
+    double rcp[256];
+    float u2f[256], f[256], fs[256];
+    int i[256];
+};
+constexpr int TAB_INTS = (int)(sizeof(Tables) / 4);
+
+void fill_tables(Tables* t) {
+    for (int v = 0; v < 256; ++v) {
+        const double x = (double)(float)v * 6.0 / 255.0;
+        const int i = (int)std::floor(x);
+        t->i[v] = i;
+        t->f[v] = (float)(x - (double)(float)i);
+        t->fs[v] = (float)((double)(float)v / 255.0);
+        t->rcp[v] = v ? 1.0 / (double)v : 0.0;
+        t->u2f[v] = (float)v / 255.0f;
+    }
+}
+
 struct Dims {
     int crop_w, crop_h, kh, kv, y0, rows_tmp;
-    long long off_bh, off_ch, off_bv, off_cv, total;
+    long long off_bh, off_ch, off_bv, off_cv, off_tab, total;
 };
 
 int dims(const psfm_augment_params* p, Dims& d) {
@@ -127,7 +155,8 @@ int dims(const psfm_augment_params* p, Dims& d) {
     d.off_ch = d.off_bh + 2LL * p->out_w;
     d.off_bv = d.off_ch + (long long)d.kh * p->out_w;
     d.off_cv = d.off_bv + 2LL * p->out_h;
-    d.total = d.off_cv + (long long)d.kv * p->out_h;
+    d.off_tab = (d.off_cv + (long long)d.kv * p->out_h + 3) & ~3LL;  // 16-byte aligned
+    d.total = d.off_tab + TAB_INTS;
     return 0;
 }
 
@@ -171,35 +200,38 @@ __device__ __forceinline__ int clip8i(int v) { return v <= 0 ? 0 : v >= 255 ? 25
 // hsv2rgb's per-byte quantities (Convert.c), computed once per workgroup with the reference's
 // double expressions: i(h) = floor(h * 6.0 / 255.0), f(h) = (float)(h * 6.0 / 255.0 - i),
 // fs(s) = (float)(s / 255.0).
-struct HueTables {
-    float f[256], fs[256];
-    int i[256];
-};
-__device__ __forceinline__ void fill_hue_tables(HueTables& t) {
-#pragma clang fp contract(off)
-    for (int v = threadIdx.x; v < 256; v += blockDim.x) {
-        const double x = (double)(float)v * 6.0 / 255.0;
-        const int i = (int)floor(x);
-        t.i[v] = i;
-        t.f[v] = (float)(x - (double)(float)i);
-        t.fs[v] = (float)((double)(float)v / 255.0);
-    }
+// Copy of the per-byte tables the host appended to the plan (psfm_augment_plan: fill_tables),
+// staged in LDS once per workgroup with 16-byte loads.
+__device__ __forceinline__ void load_tables(Tables& t, const int32_t* __restrict__ src) {
+    const uint4* s4 = (const uint4*)src;
+    uint4* d4 = (uint4*)&t;
+    for (int k = threadIdx.x; k < (int)(sizeof(Tables) / 16); k += blockDim.x) d4[k] = s4[k];
 }
 
 // Convert.c rgb2hsv_row -> h += shift (uint8) -> hsv2rgb
-__device__ __forceinline__ void hue_shift(int& R, int& G, int& B, int shift, const HueTables& T) {
+__device__ __forceinline__ void hue_shift(int& R, int& G, int& B, int shift, const Tables& T) {
 #pragma clang fp contract(off)
     const int r = R, g = G, b = B;
     const int maxc = max(r, max(g, b)), minc = min(r, min(g, b));
     int uh = 0, us = 0;
     const int uv = maxc;
     if (minc != maxc) {
-        const float cr = (float)(maxc - minc);
-        const float s = cr / (float)maxc;
-        float h;
-        if (r == maxc) h = ((float)(maxc - b)) / cr - ((float)(maxc - g)) / cr;
-        else if (g == maxc) h = (float)(2.0 + (double)(((float)(maxc - r)) / cr) - (double)(((float)(maxc - b)) / cr));
-        else h = (float)(4.0 + (double)(((float)(maxc - g)) / cr) - (double)(((float)(maxc - r)) / cr));
+        // The float quotients of small integers a / n (a <= n <= 255) are computed as
+        // (float)((double)a * (1.0 / n)): the double product is within 2^-52 of a / n, and a / n
+        // is either a float itself or at least 2^-32 (relative) from every float rounding
+        // boundary, so the conversion rounds to the IEEE float quotient.  (Exhaustively checked
+        // against Pillow over all 2^24 colours, tests/test_augment.py.)
+        const int cr = maxc - minc;
+        const double rc = T.rcp[cr];
+        const float s = (float)((double)cr * T.rcp[maxc]);
+        // h = bc - gc (float) | 2.0 + rc - bc | 4.0 + gc - rc (double): one select, one formula
+        // ((0.0 + bc) - gc in double is exact, so its float rounding is the float subtraction)
+        int base, an, bn;
+        if (r == maxc) { base = 0; an = maxc - b; bn = maxc - g; }
+        else if (g == maxc) { base = 2; an = maxc - r; bn = maxc - b; }
+        else { base = 4; an = maxc - g; bn = maxc - r; }
+        const float qa = (float)((double)an * rc), qb = (float)((double)bn * rc);
+        float h = (float)(((double)base + (double)qa) - (double)qb);
         // fmod(h / 6.0 + 1.0, 1.0) with h in [-1, 5]: the argument lies in [5/6, 11/6), where
         // fmod is the exact subtraction of 1 (Sterbenz) — no libm loop
         double y = (double)h / 6.0 + 1.0;
@@ -230,7 +262,7 @@ __device__ __forceinline__ void hue_shift(int& R, int& G, int& B, int shift, con
 }
 
 template <int V>
-__device__ __forceinline__ void apply_op_v(int op, int (&c)[3][V], const psfm_jitter& j, int mean, const HueTables& T) {
+__device__ __forceinline__ void apply_op_v(int op, int (&c)[3][V], const psfm_jitter& j, int mean, const Tables& T) {
     if (op == PSFM_JIT_HUE) {
 #pragma unroll
         for (int e = 0; e < V; ++e) hue_shift(c[0][e], c[1][e], c[2][e], j.hue_shift, T);
@@ -264,7 +296,7 @@ struct Geo {
     int n_samples, src_h, src_w, crop_l, crop_t, out_h, out_w, crop_w;
     long long src_stride;
     int kh, kv, y0, rows_tmp, seg0, seg_len;
-    int off_bh, off_ch, off_bv, off_cv;
+    int off_bh, off_ch, off_bv, off_cv, off_tab;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -359,9 +391,6 @@ __device__ __forceinline__ void pack(const int* o, uint32_t& v) {
 }
 // ToTensor through a 256-entry LDS table of the IEEE quotients u / 255.0f (u * (1/255) is not
 // exact for 126 of the 256 bytes)
-__device__ __forceinline__ void fill_u2f(float* t) {
-    for (int v = threadIdx.x; v < 256; v += blockDim.x) t[v] = to_float(v);
-}
 __device__ __forceinline__ void tofloat(const int* o, float& v, const float* t) { v = t[o[0]]; }
 __device__ __forceinline__ void tofloat(const int* o, float4& v, const float* t) {
     v = make_float4(t[o[0]], t[o[1]], t[o[2]], t[o[3]]);
@@ -378,22 +407,20 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
     typedef typename Vec<V>::u8 U8;
     typedef typename Vec<V>::f32 F32;
     __shared__ uint32_t red[NT / 64];
-    __shared__ HueTables T;
-    __shared__ float u2f[256];
+    __shared__ Tables T;       // hue tables: staged only when hue runs before contrast
+    __shared__ float u2f[256];  // ToTensor quotients, computed in place (no memory dependency)
     const int img = blockIdx.y, tid = threadIdx.x;
     const int hw = g.out_h * g.out_w;
     const int pidx = (blockIdx.x * NT + tid) * V;
-    fill_u2f(u2f);
-    __syncthreads();
     const bool live = pidx < hw;
     int v[3][V];
+    int32_t s[3][V];
     if (live) {
         const int y = pidx / g.out_w, x = pidx - y * g.out_w;
         const int ymin = plan[g.off_bv + 2 * y], yn = plan[g.off_bv + 2 * y + 1];
         const int32_t* k = plan + g.off_cv + (size_t)y * g.kv;
         const size_t plane = (size_t)g.rows_tmp * g.out_w;
         const uint8_t* col = tmp + (size_t)img * 3 * plane + (size_t)ymin * g.out_w + x;
-        int32_t s[3][V];
 #pragma unroll
         for (int c = 0; c < 3; ++c)
 #pragma unroll
@@ -430,6 +457,10 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
                 }
             }
         }
+    }
+    for (int u = tid; u < 256; u += NT) u2f[u] = to_float(u);
+    __syncthreads();
+    if (live) {
         float* o = orig + (size_t)img * 3 * hw + pidx;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -446,9 +477,13 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
     const psfm_jitter j = jit[img % g.n_samples];
     bool hue_first = false;
     if (j.apply)
-        for (int k = 0; k < 4 && j.order[k] != PSFM_JIT_CONTRAST; ++k) hue_first |= j.order[k] == PSFM_JIT_HUE;
-    if (hue_first) {  // uniform
-        fill_hue_tables(T);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (j.order[k] == PSFM_JIT_CONTRAST) break;
+            hue_first |= j.order[k] == PSFM_JIT_HUE;
+        }
+    if (hue_first) {  // uniform per workgroup
+        load_tables(T, plan + g.off_tab);
         __syncthreads();
     }
     uint32_t l = 0;
@@ -466,28 +501,26 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
         for (int e = 0; e < V; ++e) l += (uint32_t)rgb2l(v[0][e], v[1][e], v[2][e]);
     }
     if (!j.apply) return;  // uniform per workgroup
-    const uint32_t s = block_sum(l, red);
-    if (tid == 0) part[(size_t)img * gridDim.x + blockIdx.x] = s;
+    const uint32_t tot = block_sum(l, red);
+    if (tid == 0) part[(size_t)img * gridDim.x + blockIdx.x] = tot;
 }
 
 template <int V>
-__global__ void __launch_bounds__(NT) k_jitter(Geo g, const psfm_jitter* __restrict__ jit,
+__global__ void __launch_bounds__(NT) k_jitter(Geo g, const int32_t* __restrict__ plan, const psfm_jitter* __restrict__ jit,
                                                const uint8_t* __restrict__ resized, const uint32_t* __restrict__ part,
                                                float* __restrict__ rgb) {
     typedef typename Vec<V>::u8 U8;
     typedef typename Vec<V>::f32 F32;
     __shared__ unsigned long long red[NT / 64];
     __shared__ int s_mean;
-    __shared__ HueTables T;
-    __shared__ float u2f[256];
+    __shared__ Tables T;
     const int img = blockIdx.y, tid = threadIdx.x;
     const int hw = g.out_h * g.out_w;
     const int nblk = gridDim.x;
     const psfm_jitter j = jit[img % g.n_samples];
-    fill_u2f(u2f);
+    load_tables(T, plan + g.off_tab);
     int mean = 0;
     if (j.apply) {
-        fill_hue_tables(T);
         // the whole image's L sum (exact integers; each partial <= NT * V * 255)
         unsigned long long s = 0;
         for (int i = tid; i < nblk; i += NT) s += part[(size_t)img * nblk + i];
@@ -525,7 +558,7 @@ __global__ void __launch_bounds__(NT) k_jitter(Geo g, const psfm_jitter* __restr
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         F32 f;
-        tofloat(c3[c], f, u2f);
+        tofloat(c3[c], f, T.u2f);
         *(F32*)(o + (size_t)c * hw) = f;
     }
 }
@@ -542,6 +575,7 @@ long long psfm_augment_plan(const psfm_augment_params* p, int32_t* plan) {
     plan[0] = d.kh; plan[1] = d.kv; plan[2] = d.rows_tmp;
     plan[3] = (int32_t)d.off_bh; plan[4] = (int32_t)d.off_ch; plan[5] = (int32_t)d.off_bv;
     plan[6] = (int32_t)d.off_cv; plan[7] = d.y0;
+    fill_tables((Tables*)(plan + d.off_tab));
     plan_dir(d.crop_w, p->out_w, plan + d.off_bh, plan + d.off_ch);
     plan_dir(d.crop_h, p->out_h, plan + d.off_bv, plan + d.off_cv);
     // the vertical pass reads the intermediate, which starts at crop row y0
@@ -571,6 +605,7 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     g.out_h = p->out_h; g.out_w = p->out_w; g.crop_w = d.crop_w; g.src_stride = p->src_stride;
     g.kh = d.kh; g.kv = d.kv; g.y0 = d.y0; g.rows_tmp = d.rows_tmp;
     g.off_bh = (int)d.off_bh; g.off_ch = (int)d.off_ch; g.off_bv = (int)d.off_bv; g.off_cv = (int)d.off_cv;
+    g.off_tab = (int)d.off_tab;
     // the source columns the horizontal pass reads (host copy of the first / last bounds)
     {
         std::vector<int32_t> bh(2 * (size_t)p->out_w);
@@ -584,7 +619,9 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     uint8_t* resized = rgb ? base + wl.resized : nullptr;
     uint32_t* part = (uint32_t*)(base + wl.part);
     const int hw = p->out_h * p->out_w;
-    const int vec = p->out_w % 4 == 0 ? 4 : 1;  // 4-pixel groups never straddle a row
+    int vec = p->out_w % 4 == 0 ? 4 : 1;  // 4-pixel groups never straddle a row
+    if (const char* e = getenv("PSFM_AUGMENT_VEC"))  // A/B knob (tools/augment_scan.sh)
+        if (atoi(e) == 1) vec = 1;
     const int nblk = (hw / vec + NT - 1) / NT;
     const size_t lds = (size_t)((3 * g.seg_len + 3) & ~3);
     const int nth = NT;
@@ -593,13 +630,13 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
         hipLaunchKernelGGL(k_resize_v<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,
                            rgb_original, resized, part);
         if (rgb)
-            hipLaunchKernelGGL(k_jitter<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, jitter, (const uint8_t*)resized,
+            hipLaunchKernelGGL(k_jitter<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, jitter, (const uint8_t*)resized,
                                (const uint32_t*)part, rgb);
     } else {
         hipLaunchKernelGGL(k_resize_v<1>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,
                            rgb_original, resized, part);
         if (rgb)
-            hipLaunchKernelGGL(k_jitter<1>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, jitter, (const uint8_t*)resized,
+            hipLaunchKernelGGL(k_jitter<1>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, jitter, (const uint8_t*)resized,
                                (const uint32_t*)part, rgb);
     }
     const hipError_t e = hipGetLastError();
