@@ -102,6 +102,14 @@ torch.cuda.synchronize()
 us_pcie = (time.perf_counter() - t0) * 1e6 / args.iters
 
 bytes_img = h * w * 3 + 2 * 3 * H * W * 4      # algorithmic: read the frame once, write rgb + rgb_original
+# HBM traffic per call from the PMC passes (tools/gpu_augment_pmc.sh; default workload only):
+# FETCH_SIZE taken as is (byte / dword loads, not the 16-B/lane reads the gfx950 halving applies
+# to: the raw count matches the bytes the kernels read) + WRITE_SIZE
+traffic = None
+tpath = os.path.join(ROOT, "profiles", "r01_augment", "pmc_traffic.json")
+if os.path.exists(tpath) and (B, args.N, h, w, H, W) == (4, 2, 375, 1242, 192, 640):
+    t = json.load(open(tpath))["per_call_bytes"]
+    traffic = round(t["fetch_raw"] + t["write"])
 img_s = n_img / (us_call * 1e-6)
 achieved = bytes_img * img_s / 1e9
 res = {"metric": "augmented training images/s (KITTI raw frame -> LANCZOS 640x192 + jitter + ToTensor)",
@@ -111,8 +119,10 @@ res = {"metric": "augmented training images/s (KITTI raw frame -> LANCZOS 640x19
        "us_per_call": round(us_call, 2), "us_per_call_eager_api": round(us_eager, 2),
        "us_per_call_with_h2d_upload": round(us_pcie, 2),
        "roofline": {"bound": "hbm", "kernel": "k_resize_h + k_resize_v + k_jitter (one call)", "achieved": round(achieved, 1),
-                    "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
-                    "algorithmic_bytes_per_image": bytes_img, "timing": "HIP events around graph replays (10 calls)"}}
+                    "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": traffic,
+                    "traffic_unit": "bytes per call (PMC FETCH_SIZE + WRITE_SIZE)",
+                    "algorithmic_bytes_per_image": bytes_img,
+                    "algorithmic_bytes_per_call": bytes_img * n_img, "timing": "HIP events around graph replays (10 calls)"}}
 
 if not args.no_cpu_baseline:
     from PIL import Image, ImageEnhance
