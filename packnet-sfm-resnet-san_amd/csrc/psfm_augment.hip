@@ -180,6 +180,9 @@ WsLayout ws_layout(const psfm_augment_params* p, const Dims& d) {
 // ---------------------------------------------------------------------------------------------
 // device: Pillow's 8-bit pixel arithmetic
 // ---------------------------------------------------------------------------------------------
+// Taps are pixel (0..255) x coefficient (22-bit signed fixed point): both fit the signed 24-bit
+// multiplier (v_mad_i32_i24, full rate), not the quarter-rate v_mul_lo_u32 the compiler picks for
+// a plain 32-bit product.
 __device__ __forceinline__ int clip8_fixed(int32_t v) {
     v >>= PREC;
     return v < 0 ? 0 : v > 255 ? 255 : v;
@@ -355,9 +358,9 @@ __global__ void __launch_bounds__(1024) k_resize_h(Geo g, const uint8_t* __restr
 #pragma unroll 4
         for (int t = 0; t < xn; ++t) {
             const int32_t c = k[t];
-            s0 += px[3 * t] * c;
-            s1 += px[3 * t + 1] * c;
-            s2 += px[3 * t + 2] * c;
+            s0 += __mul24((int)px[3 * t], c);
+            s1 += __mul24((int)px[3 * t + 1], c);
+            s2 += __mul24((int)px[3 * t + 2], c);
         }
         out[x] = (uint8_t)clip8_fixed(s0);
         out[plane + x] = (uint8_t)clip8_fixed(s1);
@@ -441,7 +444,7 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
                     int u[V];
                     unpack(raw[t][c], u);
 #pragma unroll
-                    for (int e = 0; e < V; ++e) s[c][e] += u[e] * cf;
+                    for (int e = 0; e < V; ++e) s[c][e] += __mul24(u[e], cf);
                 }
             }
         } else {
@@ -453,7 +456,7 @@ __global__ void __launch_bounds__(NT) k_resize_v(Geo g, const int32_t* __restric
                     int u[V];
                     unpack(*(const U8*)(q + c * plane), u);
 #pragma unroll
-                    for (int e = 0; e < V; ++e) s[c][e] += u[e] * cf;
+                    for (int e = 0; e < V; ++e) s[c][e] += __mul24(u[e], cf);
                 }
             }
         }
