@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="torch.backends.cudnn.benchmark = False (MIOpen heuristics instead of find)")
+    ap.add_argument("--data-path", default="resident", choices=["resident", "gpu-augment"],
+                    help="gpu-augment: every step first runs the reference's train_transforms on the GPU "
+                         "(datasets/augmentations.train_transforms_batch) from raw 375x1242 uint8 KITTI-sized "
+                         "frames resident in HBM: LANCZOS resize + colour jitter (0.2,0.2,0.2,0.05) + ToTensor")
     ap.add_argument("--fused-nets", action="store_true",
                     help="run the nets' BN/GN/bias+activation epilogues as fused HIP kernels (psfm_netops)")
     return ap.parse_args()
@@ -82,6 +86,20 @@ def synthetic_batch(B, H, W, device, seed, channels_last=False):
         cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
         batch["rgb"], batch["rgb_context"] = cl(rgb), [cl(c) for c in ctx]
     return batch
+
+
+def raw_frames(B, device, seed, h=375, w=1242):
+    """Seeded decoded-frame stand-ins (uint8 [B,h,w,3], smooth textures) for --data-path gpu-augment."""
+    g = torch.Generator().manual_seed(seed)
+
+    def frame():
+        base = torch.rand(B, 3, h // 8, w // 8, generator=g)
+        img = torch.nn.functional.interpolate(base, size=(h, w), mode="bilinear", align_corners=False)
+        img = (img + 0.05 * torch.randn(B, 3, h, w, generator=g)).clamp(0, 1)
+        return (img * 255).round().to(torch.uint8).permute(0, 2, 3, 1).contiguous().to(device)
+
+    K = torch.tensor([[721.5, 0, 609.6], [0, 721.5, 172.9], [0, 0, 1.0]]).repeat(B, 1, 1)
+    return {"rgb": frame(), "rgb_context": [frame() for _ in range(N_CTX)], "intrinsics": K.to(device)}
 
 
 def to_channels_last(model):
@@ -215,6 +233,20 @@ def main():
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
                          graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager))
     batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank, channels_last=not args.nchw)
+    next_batch = lambda: batch  # noqa: E731
+    if args.data_path == "gpu-augment":
+        import random as _random
+        from packnet_sfm_amd.datasets.augmentations import train_transforms_batch
+        raw, rng = raw_frames(args.batch, device, seed=rank), _random.Random(rank)
+
+        def next_batch():
+            b = train_transforms_batch(raw, (args.height, args.width), (0.2, 0.2, 0.2, 0.05), (), rng=rng)
+            return {k: b[k] for k in ("rgb", "rgb_context", "rgb_original", "rgb_context_original", "intrinsics")}
+
+        batch = next_batch()   # the captured (static) batch, in the nets' layout
+        if not args.nchw:
+            cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
+            batch["rgb"], batch["rgb_context"] = cl(batch["rgb"]), [cl(c) for c in batch["rgb_context"]]
 
     for i in range(args.warmup):   # the first steps include MIOpen find and the HIP-graph capture
         t_w = time.perf_counter()
@@ -229,7 +261,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.train_step(batch)
+        trainer.train_step(next_batch())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -254,7 +286,9 @@ def main():
                                       f"min-reprojection, Adam (train_resnet_san_kitti_tiny.yaml shapes)",
                           "model": f"{args.depth_net}+{args.pose_net}", "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "image_hw": [args.height, args.width],
-                          "parallelism": f"dp{world}", "net_dtype": args.amp, "loss_dtype": "fp32",
+                          "parallelism": f"dp{world}",
+                          "data_path": "resident synthetic batch" if args.data_path == "resident" else
+                          "gpu-augment: raw 375x1242 uint8 frames -> train_transforms on the GPU inside every timed step", "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)

@@ -78,6 +78,25 @@ class _Plans:
 
     def __init__(self):
         self.plans, self.ws = {}, {}
+        self.ring, self.ring_pos = [], 0
+
+    def upload(self, raw, device):
+        """Jitter records -> device without a host sync: a ring of pinned staging buffers, each
+        reused only after its previous asynchronous copy has completed (event)."""
+        n = len(raw)
+        if not self.ring or self.ring[0][0].numel() < n:
+            self.ring = [(torch.empty(max(n, 4096), dtype=torch.uint8).pin_memory(), None) for _ in range(8)]
+        host, ev = self.ring[self.ring_pos]
+        if ev is not None:
+            ev.synchronize()
+        host[:n].copy_(torch.frombuffer(raw, dtype=torch.uint8))
+        dev = torch.empty(n, dtype=torch.uint8, device=device)
+        dev.copy_(host[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self.ring[self.ring_pos] = (host, ev)
+        self.ring_pos = (self.ring_pos + 1) % len(self.ring)
+        return dev
 
     def get(self, p, device):
         key = (p.crop_r - p.crop_l, p.crop_b - p.crop_t, p.out_h, p.out_w, device)
@@ -124,7 +143,7 @@ def augment_images(images, n_samples, box, shape, jitter_params=None):
         if len(jitter_params) != n_samples:
             raise ValueError("one jitter record per sample")
         recs = (_hip.Jitter * n_samples)(*[jitter_record(j) for j in jitter_params])
-        jit = torch.frombuffer(bytearray(recs), dtype=torch.uint8).to(images.device)
+        jit = _PLANS.upload(bytearray(recs), images.device)
         rgb = torch.empty_like(orig)
     rc = _hip.lib().psfm_train_augment(ctypes.byref(p), _hip.ptr(images), _hip.ptr(plan), _hip.ptr(jit), _hip.ptr(ws),
                                        _hip.ptr(orig), _hip.ptr(rgb), _hip.stream(images.device))
