@@ -96,6 +96,7 @@ def test_full_sample_golden(aug):
     ((370, 1224), (-352, 0, 0.5, 1216), (), (0.5, 0.5, 0.5, 0.2), 2, 1),            # crop only (no resize)
     ((48, 160), (), (96, 320), (0.2, 0.2, 0.2, 0.05), 3, 2),                        # upscale
     ((64, 200), (), (64, 200), (), 2, 2),                                            # identity, no jitter
+    ((1216, 1936), (), (384, 640), (0.2, 0.2, 0.2, 0.05), 1, 2),                     # DDAD: 21-tap generic paths
 ])
 def test_batch_matches_oracle(aug, src, borders, shape, jit, B, N):
     g = np.random.default_rng(hash((src, shape, B)) & 0xffff)

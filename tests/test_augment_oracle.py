@@ -103,7 +103,8 @@ def hip():
                                          ((375, 1242), (0, 0, 1242, 375), (192, 640)),
                                          ((24, 80), (0, 0, 80, 24), (48, 160)),
                                          ((61, 40), (0, 0, 40, 61), (30, 40)),
-                                         ((50, 90), (-7, 5, 80, 58), (20, 33))])
+                                         ((50, 90), (-7, 5, 80, 58), (20, 33)),
+                                         ((1216, 1936), (0, 0, 1936, 1216), (384, 640))])
 def test_plan_matches_oracle(hip, src, box, out):
     """psfm_augment_plan (host code of the C-ABI library) == Pillow's precompute_coeffs."""
     p = hip.AugmentParams(n_samples=1, n_img=1, src_h=src[0], src_w=src[1], src_stride=src[0] * src[1] * 3,
