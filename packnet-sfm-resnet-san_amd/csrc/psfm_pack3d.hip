@@ -37,6 +37,7 @@ constexpr int ND = 8;  // Conv3d output features (PackNet d = 8)
 
 struct P3 {
     int B, C, Hv, Wv, r, K, KG;  // K volume channels, KG chunks of channels per workgroup
+    int dy32;                    // every in-image element offset of dy fits int32 (host-checked)
     int64_t xs[4], ys[4];
     const void* x;
     const void* dy;
@@ -69,6 +70,17 @@ __device__ __forceinline__ void st<uint16_t>(void* p, int64_t i, float v) {
     uint32_t u = __float_as_uint(v);
     u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite values)
     static_cast<uint16_t*>(p)[i] = (uint16_t)(u >> 16);
+}
+
+template <typename T>
+__device__ __forceinline__ float ldi(const T* p, int i);
+template <>
+__device__ __forceinline__ float ldi<float>(const float* p, int i) {
+    return p[i];
+}
+template <>
+__device__ __forceinline__ float ldi<uint16_t>(const uint16_t* p, int i) {
+    return __uint_as_float((uint32_t)p[i] << 16);
 }
 
 // element offset of volume voxel (b, k, y, x) in x
@@ -160,11 +172,37 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WA
     for (int ch = c_lo; ch < c_hi; ++ch) {
         const int k0 = ch * DC;
         __syncthreads();
-        for (int e = threadIdx.x; e < LY * LX * ND * LK; e += NTH) {
-            const int kk = e % LK, r1 = e / LK, o = r1 % ND, r2 = r1 / ND, xx = r2 % LX, yy = r2 / LX;
-            const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
-            const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
-            sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, o, gk, gy, gx)) : 0.0f;
+        if (MODE == PSFM_P3D_PACK && a.dy32) {
+            // e = ((yy LX + xx) ND + o) LK + kk walked in steps of NTH as a mixed-radix counter
+            // (no divisions), 32-bit offsets from the image's base
+            constexpr int S0 = NTH % LK, C0 = NTH / LK, S1 = C0 % ND, C1 = C0 / ND, S2 = C1 % LX, S3 = C1 / LX;
+            const T* dyb = static_cast<const T*>(a.dy) + b * a.ys[0];
+            const int ys1 = (int)a.ys[1], ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
+            const int t = threadIdx.x;
+            int kk = t % LK, o = (t / LK) % ND, xx = (t / (LK * ND)) % LX, yy = t / (LK * ND * LX);
+            for (int e = t; e < LY * LX * ND * LK; e += NTH) {
+                const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+                const bool in = (unsigned)gk < (unsigned)a.K && (unsigned)gy < (unsigned)a.Hv &&
+                                (unsigned)gx < (unsigned)a.Wv;
+                sg[e] = in ? ldi<T>(dyb, (o * a.K + gk) * ys1 + gy * ys2 + gx * ys3) : 0.0f;
+                kk += S0;
+                int c = kk >= LK;
+                kk -= c ? LK : 0;
+                o += S1 + c;
+                c = o >= ND;
+                o -= c ? ND : 0;
+                xx += S2 + c;
+                c = xx >= LX;
+                xx -= c ? LX : 0;
+                yy += S3 + c;
+            }
+        } else {
+            for (int e = threadIdx.x; e < LY * LX * ND * LK; e += NTH) {
+                const int kk = e % LK, r1 = e / LK, o = r1 % ND, r2 = r1 / ND, xx = r2 % LX, yy = r2 / LX;
+                const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+                const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
+                sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, o, gk, gy, gx)) : 0.0f;
+            }
         }
         __syncthreads();
         const int k = k0 + dl;
@@ -351,6 +389,11 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
     a.dy = dy;
     a.dx = dx;
     a.w = w;
+    {
+        // the fast staging path indexes dy with int32 offsets from each image's base
+        const int64_t mx = (int64_t)(ND * a.K - 1) * a.ys[1] + (int64_t)(a.Hv - 1) * a.ys[2] + (int64_t)(a.Wv - 1) * a.ys[3];
+        a.dy32 = a.ys[1] >= 0 && a.ys[2] >= 0 && a.ys[3] >= 0 && mx < (int64_t)INT32_MAX;
+    }
     if (dx) {
         const dim3 grid = grid_of(a, 4, 8, 16);
         P3D_LAUNCH(k_p3d_bwd_x, grid, st, a, t);
