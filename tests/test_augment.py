@@ -161,3 +161,28 @@ def test_validation_transform(aug):
 def test_rejects_host_tensors(aug):
     with pytest.raises(RuntimeError, match="ROCm"):
         aug.augment_images(torch.zeros(1, 8, 8, 3, dtype=torch.uint8), 1, (0, 0, 8, 8), (4, 4))
+
+
+def test_per_sample_api_matches_batch(aug):
+    """datasets.transforms.train_transforms / get_transforms (per sample, the reference's call
+    shape) == one sample of the batched transform with the same random stream."""
+    from packnet_sfm_amd.datasets import transforms as T
+    g = np.random.default_rng(21)
+    frames = [torch.from_numpy(g.integers(0, 256, (375, 1242, 3), dtype=np.uint8)).to(DEV) for _ in range(3)]
+    K = torch.tensor([[721.5, 0, 609.6], [0, 721.5, 172.9], [0, 0, 1]])
+    sample = {"rgb": frames[0], "rgb_context": frames[1:], "intrinsics": K, "idx": 7}
+    tf = T.get_transforms("train", image_shape=(192, 640), jittering=(0.2, 0.2, 0.2, 0.05),
+                          crop_train_borders=(-352, 0, 0.5, 1216))
+    out = tf(sample, rng=random.Random(9))
+    ref = aug.train_transforms_batch({"rgb": frames[0][None], "rgb_context": [f[None] for f in frames[1:]],
+                                      "intrinsics": K[None]}, (192, 640), (0.2, 0.2, 0.2, 0.05),
+                                     (-352, 0, 0.5, 1216), rng=random.Random(9))
+    assert out["idx"] == 7 and out["rgb"].shape == (3, 192, 640) and len(out["rgb_context"]) == 2
+    assert torch.equal(out["rgb"], ref["rgb"][0]) and torch.equal(out["rgb_original"], ref["rgb_original"][0])
+    for a, b in zip(out["rgb_context"], ref["rgb_context"]):
+        assert torch.equal(a, b[0])
+    assert torch.equal(out["intrinsics"], ref["intrinsics"][0])
+    assert torch.equal(out["intrinsics_full"], K)
+    val = T.get_transforms("validation", image_shape=(192, 640), crop_eval_borders=(-352, 0, 0.5, 1216))(
+        {"rgb": frames[0], "intrinsics": K})
+    assert val["rgb"].shape == (3, 192, 640)
