@@ -1,9 +1,9 @@
 #!/bin/bash
-# A/B scan of the augment micro-bench (batch size, jitter on/off, vertical-pass vector width).
+# A/B scan of the augment micro-bench: horizontal-pass workgroup size and vertical-pass vector
+# width (env knobs of psfm_augment.hip), batch size.
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-for a in "--B 4" "--B 16" "--B 4 --jitter none" "VEC1 --B 4" "VEC1 --B 16"; do
-  env=""; args=$a
-  case $a in VEC1*) env="PSFM_AUGMENT_VEC=1"; args=${a#VEC1 };; esac
+for v in "X=1" "PSFM_AUGMENT_NTH=320" "PSFM_AUGMENT_NTH=640" "PSFM_AUGMENT_NTH=128" "X=1 --B 16" "PSFM_AUGMENT_NTH=320 --B 16"; do
+  env=${v%% --*}; args=""; [ "$v" != "$env" ] && args=--${v#* --}
   env $env timeout -k 10 120 python tools/augment_bench.py --no-cpu-baseline --iters 50 $args > gpurun_out/scan.json 2>/dev/null || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/scan.json'));print('$a', d['us_per_call'], d['value'], d['roofline']['frac'])"
+  python -c "import json;d=json.load(open('gpurun_out/scan.json'));print('$v', d['us_per_call'], d['value'], d['roofline']['frac'])"
 done
