@@ -1,20 +1,30 @@
 #!/usr/bin/env python3
 """Self-supervised depth training step throughput (BASELINE.json metric) on MI355X.
 
-Workload (BASELINE.json configs[1]): SelfSupModel = ResNetSAN01('18A') depth net + PoseNet,
-KITTI-shaped 192x640 RGB triplets (target + 2 contexts), per-GPU batch 4, 4 full-resolution
-scales, automask + min-reprojection, Adam.  Nets under bf16 autocast (MIOpen); the photometric
-loss (view synthesis + SSIM/L1 + min + smoothness, fwd+bwd) runs in fp32 on the HIP kernels.
+Default workload (BASELINE.json configs[1], train_resnet_san_kitti_tiny.yaml shapes):
+SelfSupModel = ResNetSAN01('18A') depth net + PoseNet, KITTI-shaped 192x640 RGB triplets
+(target + 2 contexts), per-GPU batch 4, 4 full-resolution scales, automask + min-reprojection,
+Adam.  Nets under bf16 autocast (MIOpen); the photometric loss (view synthesis + SSIM/L1 + min
++ smoothness, fwd+bwd) in fp32 on the HIP kernels.  Other BASELINE configs: --config.
 
-  python bench.py [--gpus N --steps K --warmup W]          (N>1: launched by torch.distributed.run)
+  python bench.py [--gpus N --steps K --warmup W] [--config NAME]
 
-Prints ONE JSON line on rank 0 with `roofline` (live HIP-event timing of the photometric kernel
-group K1+K2+K3) and `cpu_baseline` (the CPU restatement — same nets on CPU + oracle loss — timed
-on this host, rank 0 at N=1 only).
+--gpus N > 1 without a torch.distributed.run environment re-launches itself under
+`python -m torch.distributed.run --nproc-per-node N` (before anything touches the GPU) and exits
+with its status.  Every rank trains on its DistributedSampler partition of a synthetic dataset
+resident in HBM (datasets/synthetic.py); gradients are averaged by one RCCL all-reduce per step.
+
+Prints ONE JSON line on rank 0 with `roofline` (live HIP-event timing of the photometric kernels
+on this step's own inputs; the dominant kernel K12 against SURVEY §8(d)'s algorithmic bytes)
+and `cpu_baseline` (the CPU restatement — same nets on CPU in fp32 + the oracle loss — timed on
+this host's cores, rank 0 at N=1 only).
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -25,11 +35,36 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "training images/sec (whole node), KITTI 640x192; Abs Rel parity vs ref"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-LOSS_KW = dict(num_scales=4, ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4,
-               C2=9e-4, photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
-               padding_mode="zeros", automask_loss=True, min_depth=0.5, max_depth=80.0)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs; max shader clock (VALU floor is then a lower bound)
 N_CTX, N_SCALES = 2, 4
+
+# BASELINE.json configs -> bench presets (reference YAML in parentheses)
+CONFIGS = {
+    "overfit": dict(depth_net="DepthResNet", pose_net="PoseResNet", batch=6, height=192, width=640, cameras=1,
+                    amp="fp32", min_depth=0.5, max_depth=80.0,
+                    yaml="configs/overfit_kitti.yaml (DepthResNet 18pt + PoseResNet 18pt, fp32)"),
+    "kitti-resnet-san": dict(depth_net="ResNetSAN01", pose_net="PoseNet", batch=4, height=192, width=640,
+                             cameras=1, amp="bf16", min_depth=0.5, max_depth=80.0,
+                             yaml="configs/train_resnet_san_kitti_tiny.yaml (ResNetSAN01 18A + PoseNet)"),
+    "kitti-packnet": dict(depth_net="PackNet01", pose_net="PoseNet", batch=6, height=192, width=640, cameras=1,
+                          amp="bf16", min_depth=0.5, max_depth=80.0,
+                          yaml="PackNet01 1A + PoseNet at train_packnet_san_kitti.yaml shapes"),
+    "kitti-packnet-san": dict(depth_net="PackNetSAN01", pose_net="PoseNet", batch=6, height=192, width=640,
+                              cameras=1, amp="bf16", min_depth=0.5, max_depth=80.0,
+                              yaml="configs/train_packnet_san_kitti.yaml (PackNetSAN01 1A RGB path + PoseNet)"),
+    "ddad-packnet-san": dict(depth_net="PackNetSAN01", pose_net="PoseNet", batch=1, height=384, width=640,
+                             cameras=4, amp="bf16", min_depth=0.5, max_depth=200.0,
+                             yaml="configs/train_packnet_san_ddad.yaml (PackNetSAN01 1A, 384x640, "
+                                  "cameras 01/05/06/09 per sample)"),
+}
+DEFAULT_CONFIG = "kitti-resnet-san"
+
+
+def loss_kw(min_depth, max_depth):
+    return dict(num_scales=4, ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001, C1=1e-4,
+                C2=9e-4, photometric_reduce_op="min", disp_norm=True, clip_loss=0.0, progressive_scaling=0.0,
+                padding_mode="zeros", automask_loss=True, min_depth=min_depth, max_depth=max_depth)
 
 
 def algorithmic_bytes_per_image(H, W, N=N_CTX, S=N_SCALES):
@@ -38,32 +73,66 @@ def algorithmic_bytes_per_image(H, W, N=N_CTX, S=N_SCALES):
     return H * W * (2 * 12 * (1 + N) + 12 * S)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=4, help="per-GPU batch (train_resnet_san_kitti_tiny.yaml: 4)")
-    ap.add_argument("--height", type=int, default=192)
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--depth-net", default="ResNetSAN01", choices=["ResNetSAN01", "PackNet01", "DepthResNet"])
-    ap.add_argument("--pose-net", default="PoseNet", choices=["PoseNet", "PoseResNet"])
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--config", default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU samples (preset: the config's YAML)")
+    ap.add_argument("--cameras", type=int, default=None, help="cameras per sample (DDAD: 4)")
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--depth-net", default=None, choices=["ResNetSAN01", "PackNet01", "PackNetSAN01", "DepthResNet"])
+    ap.add_argument("--pose-net", default=None, choices=["PoseNet", "PoseResNet"])
+    ap.add_argument("--amp", default=None, choices=["bf16", "fp32"])
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N>1 on one GPU (ranks share the device, host all-reduce)")
+    ap.add_argument("--comm", default="split", choices=["split", "graph"],
+                    help="split: all_reduce between two graph replays; graph: captured into the step graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU steps (median; +1 warm-up)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="for rocprofv3 runs")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     ap.add_argument("--nchw", action="store_true", help="keep the nets in NCHW (default: channels_last)")
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="torch.backends.cudnn.benchmark = False (MIOpen heuristics instead of find)")
-    ap.add_argument("--data-path", default="resident", choices=["resident", "gpu-augment"],
-                    help="gpu-augment: every step first runs the reference's train_transforms on the GPU "
-                         "(datasets/augmentations.train_transforms_batch) from raw 375x1242 uint8 KITTI-sized "
-                         "frames resident in HBM: LANCZOS resize + colour jitter (0.2,0.2,0.2,0.05) + ToTensor")
+    ap.add_argument("--data-path", default="sampler", choices=["sampler", "resident", "gpu-augment"],
+                    help="sampler: every step gathers the next batch of this rank's DistributedSampler "
+                         "partition of a synthetic dataset resident in HBM; resident: one fixed batch; "
+                         "gpu-augment: the reference's train_transforms on the GPU from raw 375x1242 uint8 "
+                         "frames inside every timed step")
     ap.add_argument("--fused-nets", action="store_true",
                     help="run the nets' BN/GN/bias+activation epilogues as fused HIP kernels (psfm_netops)")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    preset = CONFIGS[args.config]
+    for k in ("batch", "cameras", "height", "width", "depth_net", "pose_net", "amp"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
+    args.min_depth, args.max_depth, args.yaml = preset["min_depth"], preset["max_depth"], preset["yaml"]
+    return args
+
+
+def config_key(args):
+    """Identifies the workload of a stamped profile file (profiles/pmc/<key>.json)."""
+    return (f"{args.depth_net}+{args.pose_net}_B{args.batch}x{args.cameras}_{args.height}x{args.width}_{args.amp}"
+            f"{'_nchw' if args.nchw else ''}")
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch_distributed(args):
+    """`bench.py --gpus N` outside torch.distributed.run: start one process per GPU as a CHILD
+    (nothing here has touched the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def synthetic_batch(B, H, W, device, seed, channels_last=False):
@@ -83,8 +152,19 @@ def synthetic_batch(B, H, W, device, seed, channels_last=False):
     rgb, ctx, K = to(rgb), [to(c) for c in ctx], to(K)
     batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K)
     if channels_last:
-        cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
-        batch["rgb"], batch["rgb_context"] = cl(rgb), [cl(c) for c in ctx]
+        net_layout(batch)
+    return batch
+
+
+def net_layout(batch):
+    """The nets' inputs in channels_last beside the NCHW loss inputs (separate tensors)."""
+    cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
+    if batch["rgb"] is batch.get("rgb_original"):
+        batch["rgb"] = torch.empty_like(batch["rgb"], memory_format=torch.channels_last).copy_(batch["rgb"])
+    else:
+        batch["rgb"] = cl(batch["rgb"])
+    batch["rgb_context"] = [torch.empty_like(c, memory_format=torch.channels_last).copy_(c)
+                            for c in batch["rgb_context"]]
     return batch
 
 
@@ -103,8 +183,8 @@ def raw_frames(B, device, seed, h=375, w=1242):
 
 
 def to_channels_last(model):
-    """NHWC for every 4-D parameter (the MIOpen NHWC conv kernels); PackNet01's Conv3d weights
-    (5-D) stay as they are (Module.to(memory_format=...) refuses a model that has them)."""
+    """NHWC for every 4-D parameter (the MIOpen NHWC conv kernels); Conv3d weights (5-D) stay as
+    they are (Module.to(memory_format=...) refuses a model that has them)."""
     with torch.no_grad():
         for p in model.parameters():
             if p.dim() == 4:   # explicit NHWC strides (also for 1x1 kernels, as Module.to does)
@@ -116,27 +196,47 @@ def build_model(args, device):
     import packnet_sfm_amd  # noqa: F401
     from packnet_sfm_amd.models.SelfSupModel import SelfSupModel
     from packnet_sfm_amd.networks import load_depth_net, load_pose_net
-    model = SelfSupModel(**LOSS_KW, upsample_depth_maps=True, rotation_mode="euler")
-    dkw = {"ResNetSAN01": dict(version="18A", min_depth=0.5, max_depth=80.0),
-           "PackNet01": dict(version="1A"), "DepthResNet": dict(version="18pt")}[args.depth_net]
+    mn, mx = getattr(args, "min_depth", 0.5), getattr(args, "max_depth", 80.0)
+    model = SelfSupModel(**loss_kw(mn, mx), upsample_depth_maps=True, rotation_mode="euler")
+    dkw = {"ResNetSAN01": dict(version="18A", min_depth=mn, max_depth=mx),
+           "PackNet01": dict(version="1A"), "PackNetSAN01": dict(version="1A", dropout=0.5),
+           "DepthResNet": dict(version="18pt")}[args.depth_net]
     model.add_depth_net(load_depth_net(args.depth_net, **dkw))
     model.add_pose_net(load_pose_net(args.pose_net, **({"nb_ref_imgs": 2} if args.pose_net == "PoseNet"
                                                         else {"version": "18pt"})))
     return model.to(device).train()
 
 
+def host_cores():
+    """Cores this job may use on the host: the affinity mask, capped by a cgroup CPU quota and by
+    the box's per-GPU share (OMP_NUM_THREADS, set by the GPU pool)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(args):
     """The reference's CPU training step restated: the same nets on CPU in fp32 + the oracle loss
-    (oracle/photometric_oracle.py, fixture-proven equal to the reference), Adam step."""
+    (oracle/photometric_oracle.py, fixture-proven equal to the reference), Adam step.  1 warm-up
+    + `cpu_steps` timed steps, median."""
     from oracle import photometric_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     dev = torch.device("cpu")
     model = build_model(args, dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    batch = synthetic_batch(args.batch, args.height, args.width, dev, seed=1234)
+    B = args.batch * args.cameras
+    batch = synthetic_batch(B, args.height, args.width, dev, seed=1234)
     kw = dict(num_scales_=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
-              automask_loss=True, clip_loss=0.0, min_depth=0.5, max_depth=80.0)
+              automask_loss=True, clip_loss=0.0, min_depth=args.min_depth, max_depth=args.max_depth)
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -150,30 +250,34 @@ def cpu_baseline(args):
         opt.step()
 
     def loss_only():
-        sig = [torch.rand(args.batch, 1, args.height, args.width, generator=torch.Generator().manual_seed(i))
-               .mul(0.19).add(0.01).requires_grad_(True) for i in range(4)]
-        vec = torch.zeros(args.batch, N_CTX, 6)
+        g = torch.Generator().manual_seed(5)
+        sig = [torch.rand(B, 1, args.height, args.width, generator=g).mul(0.19).add(0.01).requires_grad_(True)
+               for _ in range(4)]
+        vec = torch.zeros(B, N_CTX, 6)
         vec[:, :, 2] = torch.tensor([-1.0, 1.0])
         vec.requires_grad_(True)
         mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(N_CTX)]
         O.photometric_loss(batch["rgb"], batch["rgb_context"], sig, batch["intrinsics"], batch["intrinsics"],
                            mats, None, **kw)[0].sum().backward()
 
-    step()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        step()
-    dt = (time.perf_counter() - t0) / args.cpu_steps
-    loss_only()
-    t0 = time.perf_counter()
-    for _ in range(3):
-        loss_only()
-    dl = (time.perf_counter() - t0) / 3
-    return {"value": round(args.batch / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} timed steps (+1 warm-up) of the full SelfSupModel step "
-                      f"({args.depth_net}+{args.pose_net}, fp32, B={args.batch}, {args.height}x{args.width}, "
-                      f"Adam) with the oracle loss",
-            "s_per_step": round(dt, 3), "loss_only_images_per_s": round(args.batch / dl, 3)}
+    def timed(fn, n):
+        fn()  # warm-up
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    dt = timed(step, args.cpu_steps)
+    dl = timed(loss_only, args.cpu_steps)
+    return {"value": round(B / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"median of {args.cpu_steps} timed steps (+1 warm-up) of the full SelfSupModel training "
+                      f"step ({args.depth_net}+{args.pose_net}, fp32, {B} images of {args.height}x{args.width}, "
+                      f"Adam) with the oracle loss, {threads} threads",
+            "s_per_step": round(dt, 3), "loss_only_images_per_s": round(B / dl, 3),
+            "cores_note": "host_cores(): affinity mask, capped by the cgroup quota and the box's per-GPU share "
+                          "(OMP_NUM_THREADS)"}
 
 
 def time_photometric_kernels(args, trainer, batch, HP):
@@ -201,17 +305,76 @@ def time_photometric_kernels(args, trainer, batch, HP):
     return HP.graph_replay_times_us(rec, sigs[0].device, reps=10, iters=args.kernel_iters)
 
 
+def stamped_profile(args):
+    """profiles/pmc/<config_key>.json written by tools/pmc_bench.py from rocprofv3 --pmc passes over
+    THIS command's workload; None when no file carries this config's key."""
+    path = os.path.join(ROOT, "profiles", "pmc", config_key(args) + ".json")
+    if not os.path.exists(path):
+        return None, path
+    with open(path) as f:
+        prof = json.load(f)
+    return (prof if prof.get("config_key") == config_key(args) else None), path
+
+
+def roofline(args, ktimes):
+    """Dominant kernel K12 (the fused warp + SSIM + min + smoothness fwd/bwd sweep) against
+    SURVEY §8(d)'s algorithmic bytes of the photometric fwd+bwd per image; the whole photometric
+    group beside it; HBM traffic and VALU occupancy from the stamped PMC profile of this config."""
+    images = args.batch * args.cameras
+    bytes_step = algorithmic_bytes_per_image(args.height, args.width) * images
+    group_us = sum(v for k, v in ktimes.items() if k != "clip_stats")
+    dom = "K12_photometric_fwd_grad" if "K12_photometric_fwd_grad" in ktimes else "K2_photometric_bwd"
+    dom_us = ktimes[dom]
+    achieved = bytes_step / (dom_us * 1e-6) / 1e9
+    out = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "algorithmic_bytes_per_launch": bytes_step,
+           "algorithmic_bytes_note": "SURVEY §8(d): H*W*(2*12*(1+N) + 12*S) B per image (120 B/px), x images "
+                                     "per launch",
+           "dominant_us_per_launch": round(dom_us, 2),
+           "group": {"kernels": "prepass (K0 automask + sigmoid sums) + K12 + finalize + grad finish + pose reduce",
+                     "us_per_step": round(group_us, 2),
+                     "achieved": round(bytes_step / (group_us * 1e-6) / 1e9, 1),
+                     "frac": round(bytes_step / (group_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
+           "kernels_us_per_step": {k: round(v, 2) for k, v in ktimes.items()},
+           "timing": "HIP events around graph replays of each recorded C-ABI call (replay stream)"}
+    prof, path = stamped_profile(args)
+    out["profile"] = os.path.relpath(path, ROOT) + ("" if prof else " (absent for this config: traffic null)")
+    if prof:
+        k = prof["kernels"].get(dom)
+        if k and k.get("hbm_bytes") is not None:
+            out["traffic"] = int(k["hbm_bytes"])
+            out["traffic_vs_algorithmic"] = round(k["hbm_bytes"] / bytes_step, 3)
+        if k and k.get("SQ_ACTIVE_INST_VALU") is not None:
+            floor_us = k["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / CLOCK_HZ * 1e6
+            out["valu"] = {"active_quad_cycles": k["SQ_ACTIVE_INST_VALU"], "insts": k.get("SQ_INSTS_VALU"),
+                           "floor_us_at_2.4GHz": round(floor_us, 2),
+                           "busy_frac": round(floor_us / dom_us, 3),
+                           "note": "SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / 1024 SIMDs / 2.4 GHz = the launch's "
+                                   "VALU issue time if perfectly spread; busy_frac = that / measured duration"}
+    return out
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    assert world == args.gpus or (world == 1 and args.gpus == 1), \
-        f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run"
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks need {world} GPUs for RCCL, {ndev} visible "
+                         f"(rehearse on fewer GPUs with --dist-backend gloo)")
+    torch.cuda.set_device(local_rank % ndev)
+    device = torch.device("cuda", local_rank % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     import __graft_entry__
     if rank == 0 or world == 1:
@@ -221,23 +384,36 @@ def main():
         __graft_entry__.build()
     from packnet_sfm_amd.losses import _hip_photometric as HP
     from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    from packnet_sfm_amd.datasets.synthetic import ResidentLoader, SyntheticSfmDataset, get_datasampler
 
     from packnet_sfm_amd.networks.layers import fused
     fused.ENABLED = bool(args.fused_nets)
-    torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
+    torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     model = build_model(args, device)
     if not args.nchw:
         to_channels_last(model)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
-                         graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager))
-    batch = synthetic_batch(args.batch, args.height, args.width, device, seed=rank, channels_last=not args.nchw)
-    next_batch = lambda: batch  # noqa: E731
-    if args.data_path == "gpu-augment":
+                         graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager),
+                         comm=args.comm)
+    images_per_step = args.batch * args.cameras
+    loader = None
+    if args.data_path == "sampler":
+        dataset = SyntheticSfmDataset(8 * args.batch * world, args.height, args.width, N_CTX, args.cameras, seed=0)
+        loader = ResidentLoader(dataset, args.batch, get_datasampler(dataset, "train"), device)
+        batch = loader.next_into(None)
+        if not args.nchw:
+            net_layout(batch)
+        next_batch = lambda: loader.next_into(trainer.static_batch if trainer.graphs else batch)  # noqa: E731
+    elif args.data_path == "resident":
+        batch = synthetic_batch(images_per_step, args.height, args.width, device, seed=rank,
+                                channels_last=not args.nchw)
+        next_batch = lambda: batch  # noqa: E731
+    else:
         import random as _random
         from packnet_sfm_amd.datasets.augmentations import train_transforms_batch
-        raw, rng = raw_frames(args.batch, device, seed=rank), _random.Random(rank)
+        raw, rng = raw_frames(images_per_step, device, seed=rank), _random.Random(rank)
 
         def next_batch():
             b = train_transforms_batch(raw, (args.height, args.width), (0.2, 0.2, 0.2, 0.05), (), rng=rng)
@@ -245,12 +421,11 @@ def main():
 
         batch = next_batch()   # the captured (static) batch, in the nets' layout
         if not args.nchw:
-            cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
-            batch["rgb"], batch["rgb_context"] = cl(batch["rgb"]), [cl(c) for c in batch["rgb_context"]]
+            net_layout(batch)
 
     for i in range(args.warmup):   # the first steps include MIOpen find and the HIP-graph capture
         t_w = time.perf_counter()
-        trainer.train_step(batch)
+        trainer.train_step(next_batch() if i else batch)
         torch.cuda.synchronize()
         if rank == 0:
             print(f"[bench] warmup step {i}: {time.perf_counter() - t_w:.2f} s", file=sys.stderr, flush=True)
@@ -267,57 +442,45 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     trainer.check_finite()
-    ktimes = {} if args.no_kernel_timing else time_photometric_kernels(args, trainer, batch, HP)
+    batch_now = trainer.static_batch if trainer.graphs else batch
+    ktimes = {} if args.no_kernel_timing else time_photometric_kernels(args, trainer, batch_now, HP)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        if args.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
     if rank == 0:
-        images = args.batch * world * args.steps
+        images = images_per_step * world * args.steps
         value = images / elapsed
         per_step_ms = 1000.0 * elapsed / args.steps
+        data = {"sampler": f"DistributedSampler(world={world}, rank) partition of a {8 * args.batch * world}-sample "
+                           f"synthetic dataset resident in HBM, gathered per step",
+                "resident": "one resident synthetic batch",
+                "gpu-augment": "raw 375x1242 uint8 frames -> train_transforms on the GPU inside every timed step"
+                }[args.data_path]
         out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_step_ms, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "bf16" if args.amp == "bf16" else "fp32", "data": "synthetic",
-               "config": {"workload": f"SelfSupModel {args.depth_net}('18A' if ResNetSAN01) + {args.pose_net}, "
-                                      f"KITTI {args.width}x{args.height}, 2 contexts, 4 full-res scales, automask "
-                                      f"min-reprojection, Adam (train_resnet_san_kitti_tiny.yaml shapes)",
-                          "model": f"{args.depth_net}+{args.pose_net}", "global_batch": args.batch * world,
-                          "per_gpu_batch": args.batch, "image_hw": [args.height, args.width],
-                          "parallelism": f"dp{world}",
-                          "data_path": "resident synthetic batch" if args.data_path == "resident" else
-                          "gpu-augment: raw 375x1242 uint8 frames -> train_transforms on the GPU inside every timed step", "net_dtype": args.amp, "loss_dtype": "fp32",
+               "config": {"workload": f"SelfSupModel {args.depth_net} + {args.pose_net}, {args.width}x{args.height}, "
+                                      f"{args.batch} sample(s) x {args.cameras} camera(s) per GPU, 2 contexts, "
+                                      f"4 full-res scales, automask min-reprojection, Adam; {args.yaml}",
+                          "preset": args.config, "model": f"{args.depth_net}+{args.pose_net}",
+                          "global_batch": images_per_step * world, "per_gpu_images": images_per_step,
+                          "image_hw": [args.height, args.width], "parallelism": f"dp{world}",
+                          "dist_backend": args.dist_backend if world > 1 else None,
+                          "comm": args.comm if world > 1 else None, "data_path": data,
+                          "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
                           "net_epilogues": "fused HIP (psfm_netops)" if args.fused_nets else "reference op chain",
-                          "weights": "random init (no network / checkpoints)"}}
+                          "weights": "random init (no network / checkpoints)", "config_key": config_key(args)}}
         if ktimes:
-            # the photometric fwd+bwd group of one training step (all its HIP launches); the
-            # dominant kernel is K12
-            group = [k for k in ktimes if k not in ("clip_stats",)]
-            group_us = sum(ktimes[k] for k in group)
-            bytes_step = algorithmic_bytes_per_image(args.height, args.width) * args.batch
-            achieved = bytes_step / (group_us * 1e-6) / 1e9
-            dom = "K12_photometric_fwd_grad" if "K12_photometric_fwd_grad" in ktimes else "K2_photometric_bwd"
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                with open(pmc) as f:
-                    traffic = json.load(f).get("bytes_per_step")
-            out["roofline"] = {"bound": "hbm",
-                               "kernel": "photometric fwd+bwd group: prepass (K0 automask + sigmoid sums) + K12 "
-                                         "fused fwd/bwd sweep + finalize + grad finish + pose reduce",
-                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                               "algorithmic_bytes_per_step": bytes_step,
-                               "group_us_per_step": round(group_us, 2),
-                               "dominant_kernel": dom, "dominant_us_per_step": round(ktimes[dom], 2),
-                               "kernels_us_per_step": {k: round(v, 2) for k, v in ktimes.items()},
-                               "timing": "HIP events around graph replays of each recorded C-ABI call"}
+            out["roofline"] = roofline(args, ktimes)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

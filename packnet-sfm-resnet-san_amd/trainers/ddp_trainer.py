@@ -3,18 +3,26 @@ packnet_sfm/trainers/horovod_trainer.py, whose Horovod is a mock â€” SURVEY.md Â
 
 Per step (horovod_trainer.py:222-284): zero_grad -> forward (depth/pose nets under bf16
 autocast, photometric loss in fp32 on the HIP kernels) -> backward -> gradient average across
-ranks -> optimizer.step().
+ranks -> optimizer.step() â€” exactly one optimizer step per batch.
 
-Two execution modes:
+Execution modes:
   * graph (default on a ROCm device): the step is captured into HIP graphs once and replayed â€”
     the eager step is host-bound (~1.5k launches, MIOpen host overhead; DESIGN.md Â§Perf).
-    Autograd writes each gradient into its own (graph-static) tensor; for world size > 1 they are
-    packed into ONE flat fp32 buffer (one batched copy), averaged by a single RCCL all-reduce
-    between two graph replays (fwd+bwd+pack graph | all_reduce | unpack+Adam graph) and unpacked
-    (one foreach copy).  At world size 1 the whole step is one graph.
-  * eager: torch DDP (bucketed all-reduce overlapped with backward) â€” CPU/gloo and debugging.
-The reference's per-step anomaly detection and `.item()` syncs are not on the hot path: the
-non-finite check accumulates on the device and is tested every `check_every` steps.
+    Warm-up steps before the capture (MIOpen algorithm search, allocator) run on a snapshot of
+    the training state that is restored afterwards, so they do not train.  Autograd writes each
+    gradient into its own graph-static tensor; for world size > 1 they are packed into ONE flat
+    fp32 buffer and averaged by RCCL:
+      - comm='split': fwd+bwd+pack graph | all_reduce (host-enqueued, async) | Adam graph;
+      - comm='graph': the all_reduce is captured into the same graph (RCCL graph capture).
+    At world size 1 the whole step is one graph.
+  * eager: torch DDP (bucketed all-reduce overlapped with backward) â€” CPU/gloo and debugging;
+    `flat=True` runs the graph mode's flat-buffer algebra eagerly.
+Host-side values a graph would freeze are guarded: ProgressiveScaling's scale count triggers a
+re-capture when it changes; random flips (flip_lr_prob > 0) are refused in graph mode; a plain
+torch optimizer's float learning rates must not change after capture (the fused optimizer
+re-reads them every step).  The reference's per-step anomaly detection and `.item()` syncs are
+not on the hot path: the non-finite check accumulates on the device, tested every
+`check_every` steps.
 """
 import contextlib
 
@@ -38,7 +46,7 @@ def make_optimizer(model, depth_lr=1e-4, pose_lr=1e-4, name="Adam", **kw):
 
 class DDPTrainer:
     def __init__(self, model, optimizer, device, amp_dtype=torch.bfloat16, bucket_cap_mb=64,
-                 check_every=0, graph=None, flat=None, bf16_weights=False, fused_optim=None):
+                 check_every=0, graph=None, flat=None, bf16_weights=False, fused_optim=None, comm="split"):
         self.device = device
         self.model = model
         self.optimizer = optimizer
@@ -48,6 +56,9 @@ class DDPTrainer:
         self.nonfinite = torch.zeros((), device=device)
         self.world = hvd.world_size()
         self.use_graph = (device.type == "cuda") if graph is None else graph
+        if comm not in ("split", "graph"):
+            raise ValueError(f"comm must be 'split' or 'graph', got {comm!r}")
+        self.comm = comm
         # flat: gradients packed into one flat buffer + one all-reduce per step (the graph mode's
         # algebra; also runnable eagerly, e.g. on CPU/gloo for tests)
         self.flat = self.use_graph if flat is None else (flat or self.use_graph)
@@ -64,6 +75,8 @@ class DDPTrainer:
             else:
                 from .mixed_precision import Bf16MasterWeights
                 self.mp = Bf16MasterWeights(model, optimizer, dtype=amp_dtype or torch.bfloat16)
+        # BatchNorm step counters: host-side while graphs replay (see _detach_bn_counters)
+        self._bn, self._bn_step0 = [], 0
         if self.flat:
             self._broadcast_initial()
             self.ddp = model
@@ -142,12 +155,57 @@ class DDPTrainer:
             self.mp.master_to_model()
 
     # ------------------------------------------------------------------------------------------
+    def _snapshot(self):
+        """Training state the warm-up steps mutate: weights, buffers (BN running stats),
+        optimizer state (fused flat buffers or torch.optim per-parameter state)."""
+        snap = {"params": [p.detach().clone() for p in self.params],
+                "buffers": [b.detach().clone() for b in self.model.buffers()],
+                "opt": {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                        for p, st in self.optimizer.state.items()}}
+        if self.fused is not None:
+            f = self.fused
+            snap["fused"] = [t.clone() for t in (f.master, f.exp_avg, f.exp_avg_sq, f.step_count)]
+        if self.mp is not None:
+            snap["mp"] = [m.detach().clone() for m in self.mp.master]
+        return snap
+
+    @torch.no_grad()
+    def _restore(self, snap):
+        """In-place restore (the tensors keep their addresses: captured graphs hold them).
+        Optimizer state created by the warm-up (lazy Adam state) is reset to its initial value."""
+        for p, v in zip(self.params, snap["params"]):
+            p.copy_(v)
+        for b, v in zip(self.model.buffers(), snap["buffers"]):
+            b.copy_(v)
+        for p, st in self.optimizer.state.items():
+            old = snap["opt"].get(id(p))
+            for k, v in st.items():
+                if not torch.is_tensor(v):
+                    if old is not None and k in old:
+                        st[k] = old[k]
+                    continue
+                if old is not None and k in old:
+                    v.copy_(old[k])
+                else:
+                    v.zero_()
+        if self.fused is not None:
+            f = self.fused
+            for t, v in zip((f.master, f.exp_avg, f.exp_avg_sq, f.step_count), snap["fused"]):
+                t.copy_(v)
+        if self.mp is not None:
+            for m, v in zip(self.mp.master, snap["mp"]):
+                m.copy_(v)
+
     def capture(self, static_batch, warmup=3, progress=0.0):
-        """Warm up on a side stream (MIOpen algorithm selection, allocator), then capture."""
+        """Warm up on a side stream (MIOpen algorithm selection, allocator) from a snapshot of
+        the training state, restore it, then capture: the captured step is the first update."""
         assert self.use_graph
+        if getattr(self.model, "flip_lr_prob", 0.0) > 0.0:
+            raise NotImplementedError("graph mode freezes the host-side random flip (flip_lr_prob > 0): "
+                                      "use graph=False")
         self.static_batch = static_batch
-        self._detach_bn_counters(warmup)
-        inv_world = 1.0 / self.world
+        self._detach_bn_counters()
+        snap = self._snapshot()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -158,14 +216,23 @@ class DDPTrainer:
                 self._opt_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
+        self._restore(snap)
+        del snap
         self.nonfinite.zero_()
+        torch.cuda.synchronize(self.device)
         # grads None before capture: autograd allocates them from the graph pool (static
         # addresses, no accumulate kernels); every replay rewrites them
         self._zero_grad()
-        if self.world == 1:
+        inv_world = 1.0 / self.world
+        if self.world == 1 or self.comm == "graph":
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.static_output = self._forward_backward(static_batch, progress)
+                if self.world > 1:
+                    self._pack(capturing=True)
+                    dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+                    if self.fused is None:
+                        self._unpack(inv_world)
                 self._opt_step(capturing=True)
             self.graphs = (g,)
         else:
@@ -180,26 +247,55 @@ class DDPTrainer:
             self.graphs = (g1, g2)
         if self.fused is not None:  # gradient addresses of the captured graph -> kernel tables
             self.fused.finish_capture()
+        self._captured_n = self._scale_count(progress)
+        self._captured_lr = [g["lr"] for g in self.optimizer.param_groups]
 
-    def _detach_bn_counters(self, warmup):
+    def _scale_count(self, progress):
+        loss = getattr(self.model, "_photometric_loss", None)
+        return loss.progressive_scaling(progress) if loss is not None else None
+
+    def _detach_bn_counters(self):
         """BatchNorm's `num_batches_tracked += 1` is one kernel per BN layer per step and is only
         read when momentum is None (cumulative average).  With a fixed momentum the counters are
-        taken out of the replayed step and kept on the host; `bn_counters_to_model()` writes them
-        back (state_dict compatible with the reference's checkpoints)."""
-        self._bn = []
+        taken out of the replayed step and kept on the host (base value + steps replayed);
+        `state_dict()` / `bn_counters_to_model()` put the current value back."""
+        if self._bn:
+            return
         for m in self.model.modules():
             if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.track_running_stats \
                     and m.momentum is not None and m.num_batches_tracked is not None:
-                self._bn.append((m, m.num_batches_tracked))
+                self._bn.append((m, int(m.num_batches_tracked)))
                 m.num_batches_tracked = None
-        self._bn_warmup, self._bn_step0 = warmup, self.step_idx
+        self._bn_step0 = self.step_idx
+
+    def _bn_count(self, base):
+        return base + self.step_idx - self._bn_step0
 
     def bn_counters_to_model(self):
-        """Re-attach the BatchNorm step counters (value = counter at capture + steps run)."""
-        for m, t in getattr(self, "_bn", []):
-            t.add_(self._bn_warmup + self.step_idx - self._bn_step0)
-            m.num_batches_tracked = t
-        self._bn = []
+        """Write the BatchNorm step counters (value at capture + steps run) into the modules.
+        Idempotent; replays keep counting on the host (the graphs never touch the tensors)."""
+        for m, base in self._bn:
+            m.num_batches_tracked = torch.tensor(self._bn_count(base), dtype=torch.long,
+                                                 device=m.running_mean.device)
+
+    def state_dict(self):
+        """model.state_dict() in the reference checkpoint format (model_checkpoint.py:66-76
+        'state_dict'): fp32 master weights in place of the bf16 working copies, and every
+        BatchNorm `num_batches_tracked` present and current."""
+        sd = self.model.state_dict()
+        names = {id(m): n for n, m in self.model.named_modules()}
+        for m, base in self._bn:
+            key = (names[id(m)] + "." if names[id(m)] else "") + "num_batches_tracked"
+            sd[key] = torch.tensor(self._bn_count(base), dtype=torch.long)
+        if self.fused is not None or self.mp is not None:
+            pname = {id(p): n for n, p in self.model.named_parameters()}
+            if self.fused is not None:
+                for p in self.fused.params:
+                    sd[pname[id(p)]] = self.fused.master_view(p).detach().clone()
+            else:
+                for p, m in zip(self.mp.lp, self.mp.master):
+                    sd[pname[id(p)]] = m.detach().clone()
+        return sd
 
     def _zero_grad(self):
         """Model grads -> None (autograd then owns fresh, graph-static tensors); the fp32 master
@@ -218,20 +314,27 @@ class DDPTrainer:
 
     # ------------------------------------------------------------------------------------------
     def train_step(self, batch, progress=0.0):
+        """One optimizer step on `batch`.  Returns {'loss', 'metrics', ...}: loss and metrics are
+        this step's own (detached copies â€” a replayed graph rewrites its static outputs); the
+        other entries (inv_depths, poses) are the graph's static tensors in graph mode."""
         if self.fused is not None:
             self.fused.sync_hparams()  # lr schedulers act on optimizer.param_groups
         if self.use_graph:
+            if self.graphs is not None and self._scale_count(progress) != self._captured_n:
+                self._release_graphs()   # ProgressiveScaling changed the scale count: re-capture
             if self.graphs is None:
                 self.capture(batch, progress=progress)
             elif batch is not self.static_batch:
                 _copy_into(self.static_batch, batch)
-            if self.world == 1:
-                self.graphs[0].replay()
-            else:
-                self.graphs[0].replay()
+            if self.fused is None and [g["lr"] for g in self.optimizer.param_groups] != self._captured_lr:
+                raise RuntimeError("learning rate changed after the step was captured: a plain torch optimizer "
+                                   "bakes float lr into the graph (use bf16_weights=True for the fused "
+                                   "optimizer, or graph=False)")
+            self.graphs[0].replay()
+            if len(self.graphs) == 2:
                 dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
                 self.graphs[1].replay()
-            output = self.static_output
+            output = _step_output(self.static_output)
         elif self.flat:
             self._zero_grad()
             output = self._forward_backward(batch, progress)
@@ -246,12 +349,27 @@ class DDPTrainer:
             self.check_finite()
         return output
 
+    def _release_graphs(self):
+        torch.cuda.synchronize(self.device)
+        self.graphs = None
+        self.static_output = None
+        for p in self.params:
+            p.grad = None
+
     def check_finite(self):
         flag = self.nonfinite.clone()
         if self.world > 1 and dist.is_initialized():
             dist.all_reduce(flag)
         if float(flag) > 0:
             raise ValueError(f"Non-finite loss within the last steps (step {self.step_idx})")
+
+
+def _step_output(static):
+    out = dict(static)
+    out["loss"] = static["loss"].detach().clone()
+    if "metrics" in static:
+        out["metrics"] = {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in static["metrics"].items()}
+    return out
 
 
 def _copy_into(dst, src):

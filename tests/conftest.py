@@ -10,3 +10,10 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP path)")
     config.addinivalue_line("markers", "slow: long CPU test")
+
+
+def pytest_sessionstart(session):
+    """Build the C oracle of the sample transform (test infrastructure, the checker only — the
+    product build in __graft_entry__.build() does not touch oracle/)."""
+    from oracle import augment_oracle
+    augment_oracle.build()

@@ -81,3 +81,104 @@ def test_comm_api_single_process_is_identity():
     t = torch.ones(3)
     assert torch.equal(hvd.allreduce(t), t)
     assert hvd.reduce_value(2.5) == 2.5
+
+
+# -------------------------------------------------------------------------------------------------
+# data partition (DistributedSampler, model_wrapper.py:1138-1144) and the eval reduction
+# (utils/reduce.py all_reduce_metrics, reduce.py:31-80) with two real ranks
+class _EvalNet(torch.nn.Module):
+    """SfmModel-shaped eval stand-in: depth_net-like output of a sigmoid map per image."""
+
+    def forward(self, batch):
+        s = batch["rgb"].mean(1, keepdim=True) * 0.15 + 0.02
+        return {"inv_depths": [s]}
+
+
+def _eval_dataset():
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.datasets.synthetic import SyntheticSfmDataset
+
+    class WithDepth(SyntheticSfmDataset):
+        def __getitem__(self, i):
+            s = super().__getitem__(i)
+            g = torch.Generator().manual_seed(500 + i)
+            d = 1.0 + 70.0 * torch.rand(1, self.H, self.W, generator=g)
+            d[torch.rand(1, self.H, self.W, generator=g) < 0.5] = 0.0
+            s["depth"] = d
+            return s
+    return WithDepth(9, 24, 80, seed=3)   # odd length: the sampler pads rank 1 with a repeat
+
+
+def _oracle_metrics(cfg, gt, pred, use_gt_scale=True):
+    from oracle import photometric_oracle as O
+    return O.depth_metrics(gt, pred, cfg.min_depth, cfg.max_depth, crop=cfg.crop, use_gt_scale=use_gt_scale)
+
+
+def _dist_worker(rank, world, init_file, out_dir):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.datasets.synthetic import ResidentLoader, get_datasampler, setup_dataloader
+    from packnet_sfm_amd.models.evaluate import validate
+    ds = _eval_dataset()
+    # training partition: resident loader over this rank's sampler indices
+    loader = ResidentLoader(ds, 2, get_datasampler(ds, "train"), torch.device("cpu"))
+    seen, parts = [], []
+    for _ in range(3 * len(loader)):   # three epochs (reshuffled by set_epoch)
+        if loader.step_in_epoch == 0 or loader.step_in_epoch >= loader.steps_per_epoch:
+            b = loader.next_into(None)
+            parts.append(list(loader.partition))
+        else:
+            b = loader.next_into(None)
+        seen.append((len(parts) - 1, b["rgb"].reshape(b["rgb"].shape[0], -1)[:, :4].clone()))
+    # validation: per-rank partition -> all_reduce_metrics
+    vloaders = setup_dataloader([ds], batch_size=1, mode="validation")  # default_config validation batch 1
+    res = validate(_EvalNet(), vloaders, [ds], 0.0, 80.0, crop="", metrics_fn=_oracle_metrics)
+    torch.save({"parts": parts, "seen": seen, "metrics": dict(res[0])},
+               os.path.join(out_dir, f"d{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sampler_partition_and_eval_reduction():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dist_worker, args=(world, os.path.join(d, "init"), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"d{k}.pt"), weights_only=True) for k in range(world)]
+    ds = _eval_dataset()
+    # every epoch the two partitions cover the dataset (the shorter rank padded with one repeat)
+    # and reshuffle between epochs
+    assert len(r[0]["parts"]) == 3
+    for e in range(3):
+        p0, p1 = r[0]["parts"][e], r[1]["parts"][e]
+        assert sorted(set(p0) | set(p1)) == list(range(len(ds))) and len(p0) == len(p1) == 5
+        assert len(set(p0) & set(p1)) <= 1
+    assert r[0]["parts"][0] != r[0]["parts"][1]
+    # every gathered batch row is one of that epoch's samples of that rank
+    for k in range(world):
+        for e, rows in r[k]["seen"]:
+            keys = {tuple(ds[i]["rgb"].reshape(-1)[:4].tolist()) for i in r[k]["parts"][e]}
+            assert all(tuple(row.tolist()) in keys for row in rows)
+    # both ranks report the same reduced metrics, equal to a single-process evaluation of every
+    # sample once (the padded repeat is averaged out by the seen count)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.models.evaluate import evaluate_depth
+    net = _EvalNet()
+    per = []
+    for i in range(len(ds)):
+        s = ds[i]
+        b = {"rgb": s["rgb"][None], "depth": s["depth"][None]}
+        per.append(evaluate_depth(net, b, 0.0, 80.0, crop="", metrics_fn=_oracle_metrics)["metrics"])
+    for key in r[0]["metrics"]:
+        ref = torch.stack([p[key] for p in per]).double().mean(0).float()
+        torch.testing.assert_close(r[0]["metrics"][key], r[1]["metrics"][key])
+        torch.testing.assert_close(r[0]["metrics"][key], ref, rtol=1e-5, atol=1e-6)
+
+
+def test_all_reduce_metrics_asserts_every_sample_seen():
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.utils.reduce import all_reduce_metrics
+    outs = [{"idx": torch.tensor([0, 1]), "depth": torch.ones(7)}]
+    with pytest.raises(AssertionError):
+        all_reduce_metrics(outs, [list(range(3))])
+    res = all_reduce_metrics(outs + [{"idx": torch.tensor([2]), "depth": 3 * torch.ones(7)}], [list(range(3))])
+    torch.testing.assert_close(res[0]["depth"], torch.full((7,), 5.0 / 3))

@@ -102,11 +102,21 @@ def test_graph_trainer_step_on_fused_adam():
     losses = [float(tr.train_step(batch)["loss"]) for _ in range(12)]
     torch.cuda.synchronize()
     tr.check_finite()
-    assert int(tr.fused.step_count) == 3 + 12  # 3 warm-up steps inside capture()
+    assert int(tr.fused.step_count) == 12  # warm-up steps inside capture() are rolled back
     assert losses[-1] < losses[0]
     for p in tr.fused.params:
         assert torch.equal(storage_flat(p.detach()), storage_flat(tr.fused.master_view(p).to(p.dtype)))
-    # BatchNorm step counters were taken out of the replayed step; written back on request
+    # BatchNorm step counters were taken out of the replayed step: the trainer's state_dict has
+    # them (one per optimizer step) and the fp32 master weights (reference checkpoint format)
+    sd = tr.state_dict()
+    ref_keys = set(k for k in model.state_dict()) | {k for k in sd if k.endswith("num_batches_tracked")}
+    assert set(sd) == ref_keys
+    bns = [n for n, m in model.named_modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    assert bns and all(int(sd[n + ".num_batches_tracked"]) == 12 for n in bns)
+    pname = {id(p): n for n, p in model.named_parameters()}
+    for p in tr.fused.params:
+        assert sd[pname[id(p)]].dtype == torch.float32
+        assert torch.equal(sd[pname[id(p)]], tr.fused.master_view(p))
     tr.bn_counters_to_model()
-    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
-    assert bns and all(int(m.num_batches_tracked) == 15 for m in bns)
+    tr.bn_counters_to_model()   # idempotent
+    assert all(int(m.num_batches_tracked) == 12 for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d))

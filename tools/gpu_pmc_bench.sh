@@ -1,0 +1,24 @@
+#!/bin/bash
+# PMC passes over bench.py for one config -> profiles/pmc/<config_key>.json (tools/pmc_bench.py).
+# One rocprofv3 run per counter group (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass; at most
+# 8 SQ counters per pass).  Stops at the first crash-like exit.
+# usage: tools/gpu_pmc_bench.sh [bench.py args...]
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/pmc
+rm -rf "$OUT"; mkdir -p "$OUT"
+export TMPDIR=/tmp
+KEY=$(cd "$ROOT" && python3 -c "import sys, bench; print(bench.config_key(bench.parse(sys.argv[1:])))" "$@")
+echo "[pmc] config $KEY"
+crash() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"; do
+  i=$((i+1))
+  (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
+     -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --no-kernel-timing "$@") > "$OUT/p$i.log" 2>&1; rc=$?
+  echo "[pmc pass $i: $grp] rc=$rc"; tail -2 "$OUT/p$i.log"
+  crash $rc && exit $rc
+  [ $rc -ne 0 ] && exit $rc
+done
+python3 "$ROOT/tools/pmc_bench.py" "$KEY" "$OUT/$KEY.json" "$OUT"/p1 "$OUT"/p2 "$OUT"/p3
