@@ -196,23 +196,31 @@ def smoothness(sigs, images, n):
 
 
 def num_scales(progressive_scaling, num, progress):
-    """losses/loss_base.py:10-49."""
+    """losses/loss_base.py:10-49.  The reference stores the thresholds as an np.float32 ARRAY and
+    then tests them with is_list() (utils/types.py:21-23: isinstance(data, list)), which is False:
+    the scale count never decreases (goldens loss_progressive_p03 / _p06 pin this)."""
     if progressive_scaling > 0.0:
         import numpy as np
         steps = np.float32([progressive_scaling * (i + 1) for i in range(num - 1)] + [1.0])
-        return int(num - np.searchsorted(steps, progress))
+        if isinstance(steps, list):   # never true (the reference's is_list test)
+            return int(num - np.searchsorted(steps, progress))
     return num
 
 
 def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_scales_=4,
                      ssim_loss_weight=0.85, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
                      photometric_reduce_op="min", clip_loss=0.0, automask_loss=True,
-                     min_depth=0.5, max_depth=80.0, progressive_scaling=0.0, progress=0.0):
+                     min_depth=0.5, max_depth=80.0, progressive_scaling=0.0, progress=0.0, tie_flip=None):
     """MultiViewPhotometricLoss.forward restated.  losses/multiview_photometric_loss.py:331-410.
 
     sigs: list of [B,1,h,w] sigmoid maps (the fork feeds sigmoid outputs, :362-369);
     pose_mats: list of [B,4,4] target->context transforms.  Pinhole cameras.
     Returns (loss[1], photometric metric, smoothness, per-scale reduced maps).
+
+    `tie_flip` (test instrument, not the reference): per-scale boolean maps [B,1,h,w]; at those
+    pixels the min-reprojection selects the SECOND-smallest candidate instead of the smallest —
+    the other legitimate fp32 outcome at a near-tie (tests bound the gradient at
+    `sensitive_pixels` by "matches either selection").
 
     Note the reference's metric aliasing: `add_metric` stores `photometric_loss.detach()`
     (:296, loss_base.py:73-81) and `loss += smoothness` (:405) then adds IN PLACE into that
@@ -259,6 +267,13 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
         if photometric_reduce_op == "mean":
             r = sum(c.mean() for c in cands[i]) / len(cands[i])
             reduced.append(None)
+        elif tie_flip is not None:
+            vals = torch.cat(cands[i], 1)
+            order = vals.detach().sort(1, stable=True)[1]          # first index first on exact ties
+            pick = torch.where(tie_flip[i].to(vals.device), order[:, 1:2], order[:, 0:1])
+            m = vals.gather(1, pick)
+            reduced.append(m)
+            r = m.mean()
         else:
             m = torch.cat(cands[i], 1).min(1, True)[0]
             reduced.append(m)
@@ -311,7 +326,7 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="garg", use_gt_scale=True
 # test helpers: where is a fp32 implementation allowed to disagree with the reference's gradient?
 # ---------------------------------------------------------------------------------------------------------------------
 def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, automask=True,
-                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-5, margin_eps=5e-5):
+                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-5, margin_eps=5e-5, return_ties=False):
     """Per-scale boolean maps [B,1,h,w] of pixels whose gradient is discontinuous at fp32 precision:
 
     * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer — d(warp)/d(ix)
@@ -321,9 +336,10 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
       carries ~1e-5 absolute error from the E[x^2]-mu^2 cancellation, so two fp32 implementations
       can order candidates differently below that) — the
       selected candidate (and so the gradient of the 3x3 SSIM window around it) can flip.
-    Computed in float64 from the same inputs.  Full-resolution scales only.
+    Computed in float64 from the same inputs.  Full-resolution scales only.  With `return_ties`
+    also the (undilated) near-tie maps, the `tie_flip` argument of photometric_loss.
     """
-    out = []
+    out, ties = [], []
     img = image.double()
     ctx = [c.double() for c in contexts]
     fish = isinstance(K, dict)
@@ -345,11 +361,12 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
             cands.append(photometric_map(synthesize(c, depth, Kd, Kd, T), img, ssim_w, C1, C2))
             if automask:
                 cands.append(photometric_map(c, img, ssim_w, C1, C2))
+        tie = torch.zeros_like(s, dtype=torch.bool)
         if len(cands) > 1 and cands[0].shape[1] == 1:
             srt = torch.cat(cands, 1).sort(1)[0]
             tie = (srt[:, 1:2] - srt[:, 0:1]) < margin_eps
             # a flipped selection moves the gradient of the whole 3x3 SSIM window
-            tie = F.max_pool2d(tie.double(), 3, 1, 1) > 0
-            bad |= tie
+            bad |= F.max_pool2d(tie.double(), 3, 1, 1) > 0
         out.append(bad)
-    return out
+        ties.append(tie)
+    return (out, ties) if return_ties else out

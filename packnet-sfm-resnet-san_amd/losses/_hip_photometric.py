@@ -166,9 +166,13 @@ class PhotometricLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, image, mask, K, ref_K, T, n_ctx, *rest):
-        contexts = [c.contiguous() for c in rest[:n_ctx]]
-        sigs = [s.contiguous() for s in rest[n_ctx:]]
-        image = image.contiguous()
+        # detached: the per-call records (_Call) live on ctx, and an input with a grad_fn stored
+        # there would form a ctx -> tensor -> graph -> ctx cycle that keeps every step's autograd
+        # graph (and its AccumulateGrad nodes) alive until the garbage collector runs
+        contexts = [c.detach().contiguous() for c in rest[:n_ctx]]
+        sigs = [s.detach().contiguous() for s in rest[n_ctx:]]
+        image = image.detach().contiguous()
+        mask = mask.detach() if mask is not None else None
         _hip.require_device(image, mask, T, *contexts, *sigs)
         dev = image.device
         B, _, H, W = image.shape

@@ -5,10 +5,15 @@ import torch.nn as nn
 
 
 class ProgressiveScaling:
-    """After each `progressive_scaling` fraction of training, drop one scale."""
+    """After each `progressive_scaling` fraction of training, drop one scale — as documented.  As
+    executed by the reference, never: it keeps the thresholds in an np.float32 array and tests
+    `is_list(...)` (utils/types.py:21-23, isinstance(data, list)), which is False for an array,
+    so __call__ always returns num_scales (loss_base.py:23-49; goldens loss_progressive_p03 /
+    _p06).  `reference_quirk=False` applies the documented schedule instead."""
 
-    def __init__(self, progressive_scaling, num_scales=4):
+    def __init__(self, progressive_scaling, num_scales=4, reference_quirk=True):
         self.num_scales = num_scales
+        self.reference_quirk = reference_quirk
         if progressive_scaling > 0.0:
             self.progressive_scaling = np.float32(
                 [progressive_scaling * (i + 1) for i in range(num_scales - 1)] + [1.0])
@@ -16,7 +21,7 @@ class ProgressiveScaling:
             self.progressive_scaling = progressive_scaling
 
     def __call__(self, progress):
-        if isinstance(self.progressive_scaling, np.ndarray):
+        if isinstance(self.progressive_scaling, np.ndarray) and not self.reference_quirk:
             return int(self.num_scales - np.searchsorted(self.progressive_scaling, progress))
         return self.num_scales
 

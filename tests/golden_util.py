@@ -108,3 +108,31 @@ def grad_check(got, ref, sensitive=None, tol=1e-3):
         bad &= ~np.asarray(sensitive, dtype=bool)
     n = int(bad.sum())
     return n == 0, f"{n} pixels over {tol:g}*max (max err {d.max():.3e}, lim {lim:.3e})"
+
+
+def grad_check_bounded(got, ref, ref_alt, sensitive, tol=1e-3, cap=5e-2, max_frac=0.05):
+    """Per-pixel gradient parity with a BOUNDED exclusion set.
+
+    Every pixel must be within tol*max|ref| of the oracle gradient `ref`, except pixels that
+    oracle.sensitive_pixels flags (bilinear kinks / min near-ties: fp32-ambiguous).  A flagged
+    pixel passes when it is within tol*max of `ref` OR of `ref_alt` (the oracle with the other
+    selection at every near-tie, photometric_loss(tie_flip=...)), or — a kink, where the two
+    bilinear cells give different slopes, or interacting ties — within cap*max.  At most
+    `max_frac` of the pixels may be flagged.  Returns (ok, stats dict)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    alt = np.asarray(ref_alt, dtype=np.float64) if ref_alt is not None else ref
+    sens = np.zeros(got.shape, bool) if sensitive is None else np.asarray(sensitive, dtype=bool)
+    scale = max(np.abs(ref).max(), 1e-20)
+    lim, lim_cap = tol * scale, cap * scale
+    da, db = np.abs(got - ref), np.abs(got - alt)
+    plain_bad = (da > lim) & ~sens
+    ok_a, ok_b = (da <= lim) & sens, (db <= lim) & sens & ~((da <= lim) & sens)
+    capped = sens & (da > lim) & (db > lim)
+    cap_bad = capped & (np.minimum(da, db) > lim_cap)
+    stats = {"pixels": int(got.size), "excluded": int(sens.sum()), "excluded_frac": float(sens.mean()),
+             "match_ref": int(ok_a.sum()), "match_alt": int(ok_b.sum()), "capped": int(capped.sum()),
+             "max_capped_err_over_tol": float(np.minimum(da, db)[capped].max() / lim) if capped.any() else 0.0,
+             "bad": int(plain_bad.sum() + cap_bad.sum())}
+    ok = stats["bad"] == 0 and stats["excluded_frac"] <= max_frac
+    return ok, stats

@@ -6,9 +6,11 @@ Tolerances (BASELINE.json north_star: 1e-4 rel fp32):
   * loss / metrics: 1e-4 relative;
   * dL/dsig: every pixel within 1e-3 * max|g|, except pixels that oracle.sensitive_pixels flags
     (bilinear kinks: a sampling coordinate within 1e-5 px of an integer, where grid_sample's
-    derivative jumps; min-reprojection near-ties within 1e-5 and their SSIM window).  There two
+    derivative jumps; min-reprojection near-ties within 5e-5 and their SSIM window).  There two
     fp32 implementations legitimately differ — ATen-GPU vs ATen-CPU shows the same effect
-    (tools/debug_grads.py);
+    (tools/debug_grads.py).  The exclusion is bounded (golden_util.grad_check_bounded): a flagged
+    pixel must match the oracle with either min selection at the near-ties within 1e-3 * max,
+    or stay within 5e-2 * max; at most 5 % of the pixels may be flagged; counts are printed;
   * dL/dpose: 1e-3 relative on inputs with no sensitive pixel (test_kink_free_*); on golden
     inputs that contain kinks, 2e-2 (one kink pixel moves the 24x80 pose gradient by ~1e-2).
 """
@@ -22,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 LOSS_TOL, GRAD_TOL = 1e-4, 1e-3
 CASES = ["default", "mindepth0", "no_automask", "reduce_mean", "rand_mask", "clip", "l1_only",
-         "multires", "one_ctx", "wide_motion"]
+         "multires", "one_ctx", "wide_motion", "progressive_p03", "progressive_p06"]
 
 
 @pytest.fixture(scope="module")
@@ -62,24 +64,39 @@ def run_hip_case(z, dev, mask_none=False):
     loss_fn = MultiViewPhotometricLoss(**kw)
     out = loss_fn(_T(z["image"], dev), [_T(z[f"ctx{j}"], dev) for j in range(nctx)], sigs,
                   _T(z["K"], dev), _T(z["K"], dev), [Pose.from_vec(vec[:, j], "euler") for j in range(nctx)],
-                  mask=None if mask_none else _T(z["mask"], dev))
+                  mask=None if mask_none else _T(z["mask"], dev), progress=float(z.get("progress", 0.0)))
     out["loss"].sum().backward()
     torch.cuda.synchronize()
     return out, sigs, vec
 
 
 def _sensitive(z):
+    """(sensitive maps, oracle dL/dsig with every near-tie flipped) — or (None, None) for a
+    multi-resolution case (checked without exclusions)."""
     from oracle import photometric_oracle as O
     kw = _kw(z)
     nctx = sum(1 for k in z if k.startswith("ctx"))
     T = torch.from_numpy
     sigs = [T(z[f"sig{i}"]) for i in range(kw["num_scales"])]
     if any(s.shape[-2:] != sigs[0].shape[-2:] for s in sigs):
-        return None  # multi-resolution: check without exclusions
-    return [m.numpy() for m in O.sensitive_pixels(
-        T(z["image"]), [T(z[f"ctx{j}"]) for j in range(nctx)], sigs, T(z["K"]),
-        [O.pose_vec_to_mat(T(z["vec"])[:, j]) for j in range(nctx)], kw["min_depth"], kw["max_depth"],
-        kw["automask_loss"], kw["ssim_loss_weight"])]
+        return None, None
+    mats = [O.pose_vec_to_mat(T(z["vec"])[:, j]) for j in range(nctx)]
+    image, ctx = T(z["image"]), [T(z[f"ctx{j}"]) for j in range(nctx)]
+    sens, ties = O.sensitive_pixels(image, ctx, sigs, T(z["K"]), mats, kw["min_depth"], kw["max_depth"],
+                                    kw["automask_loss"], kw["ssim_loss_weight"], return_ties=True)
+    alt = None
+    if kw["photometric_reduce_op"] == "min" and any(bool(t.any()) for t in ties):
+        s_c = [x.clone().requires_grad_(True) for x in sigs]
+        out = O.photometric_loss(image, ctx, s_c, T(z["K"]), T(z["K"]), mats, T(z["mask"]),
+                                 num_scales_=kw["num_scales"], ssim_loss_weight=kw["ssim_loss_weight"],
+                                 smooth_loss_weight=kw["smooth_loss_weight"], C1=kw["C1"], C2=kw["C2"],
+                                 photometric_reduce_op="min", clip_loss=kw["clip_loss"],
+                                 automask_loss=kw["automask_loss"], min_depth=kw["min_depth"],
+                                 max_depth=kw["max_depth"], progressive_scaling=kw["progressive_scaling"],
+                                 progress=float(z.get("progress", 0.0)), tie_flip=ties)
+        out[0].sum().backward()
+        alt = [x.grad.numpy() if x.grad is not None else np.zeros(x.shape, np.float32) for x in s_c]
+    return [m.numpy() for m in sens], alt
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -89,10 +106,16 @@ def test_loss_and_grads_match_reference_golden(dev, case):
     assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["photometric_loss"].cpu(), z["photometric_loss"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < LOSS_TOL
-    sens = _sensitive(z)
+    sens, alt = _sensitive(z)
+    n_used = int(z.get("n_used", len(sigs)))
     for i, s in enumerate(sigs):
-        ok, msg = gu.grad_check(s.grad.cpu(), z[f"grad_sig{i}"], None if sens is None else sens[i], GRAD_TOL)
-        assert ok, f"dL/dsig{i}: {msg}"
+        if i >= n_used:   # ProgressiveScaling dropped this scale: no gradient, as in the reference
+            assert s.grad is None and not z[f"grad_sig{i}"].any()
+            continue
+        ok, st = gu.grad_check_bounded(s.grad.cpu(), z[f"grad_sig{i}"], None if alt is None else alt[i],
+                                       None if sens is None else sens[i], GRAD_TOL)
+        print(f"{case} dL/dsig{i}: {st}")
+        assert ok, f"dL/dsig{i}: {st}"
     n_sens = 0 if sens is None else int(sum(m.sum() for m in sens))
     assert gu.rel_err(vec.grad.cpu(), z["grad_vec"]) < (GRAD_TOL if n_sens == 0 else 2e-2)
 
@@ -178,16 +201,20 @@ def test_kitti_full_res_golden(dev):
     # golden differs by 2.8e-3 on this pose gradient (tools/debug_grads.py) -> 5e-3 here
     assert gu.rel_err(v_d.grad.cpu(), z["grad_vec"]) < 5e-3
     from oracle import photometric_oracle as O
-    sens = O.sensitive_pixels(image, ctx, sigs, K, [O.pose_vec_to_mat(vec[:, j]) for j in range(2)], 0.5, 80.0)
+    mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+    sens, ties = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0, return_ties=True)
     s_c = [s.clone().requires_grad_(True) for s in sigs]
-    ref = O.photometric_loss(image, ctx, s_c, K, K, [O.pose_vec_to_mat(vec[:, j]) for j in range(2)], None)
+    ref = O.photometric_loss(image, ctx, s_c, K, K, mats, None)
     ref[0].sum().backward()
+    s_a = [s.clone().requires_grad_(True) for s in sigs]
+    O.photometric_loss(image, ctx, s_a, K, K, mats, None, tie_flip=ties)[0].sum().backward()
     idx = torch.from_numpy(z["sample_idx"])
     for i in range(4):
         g_cpu = s_c[i].grad.reshape(-1)
         assert gu.rel_err(g_cpu[idx], z[f"grad_sig{i}_samples"]) < 1e-3   # oracle == reference here
-        ok, msg = gu.grad_check(s_d[i].grad.cpu(), s_c[i].grad, sens[i], GRAD_TOL)
-        assert ok, f"dL/dsig{i}: {msg}"
+        ok, st = gu.grad_check_bounded(s_d[i].grad.cpu(), s_c[i].grad, s_a[i].grad, sens[i], GRAD_TOL)
+        print(f"kitti dL/dsig{i}: {st}")
+        assert ok, f"dL/dsig{i}: {st}"
 
 
 def test_view_synthesis_matches_reference(dev):

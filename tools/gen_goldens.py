@@ -188,6 +188,11 @@ LOSS_CASES = {
     "multires": dict(kw=dict(), mask="ones", multires=True),
     "one_ctx": dict(kw=dict(), mask="ones", nctx=1),
     "wide_motion": dict(kw=dict(), mask="ones", motion=8.0),
+    # ProgressiveScaling (loss_base.py:10-49, used at :372): thresholds [0.25, 0.5, 0.75, 1.0] would
+    # give n = 3 / 2, but the reference tests them with is_list() (utils/types.py:21-23), which is
+    # False for the np.float32 array it builds: n stays num_scales (pinned here, `n_used`)
+    "progressive_p03": dict(kw=dict(progressive_scaling=0.25), mask="ones", progress=0.3),
+    "progressive_p06": dict(kw=dict(progressive_scaling=0.25), mask="ones", progress=0.6),
 }
 
 BASE_KW = dict(num_scales=4, ssim_loss_weight=0.85, occ_reg_weight=0.1, smooth_loss_weight=0.001,
@@ -219,9 +224,11 @@ def run_loss_case(name, case, B=2, H=24, W=80, seed=100):
     vec_p = vec.clone().requires_grad_(True)
     poses = [Pose.from_vec(vec_p[:, j], "euler") for j in range(nctx)]
     loss_fn = HarnessLoss(**kw)
-    out = loss_fn(image, ctx, sig_p, K, K, poses, progress=0.0, mask=mask)
+    progress = case.get("progress", 0.0)
+    out = loss_fn(image, ctx, sig_p, K, K, poses, progress=progress, mask=mask)
     out["loss"].sum().backward()
     res = dict(image=np32(image), K=np32(K), vec=np32(vec), mask=np32(mask),
+               progress=np.float64(progress), n_used=np.int64(loss_fn.n),
                loss=np32(out["loss"]),
                photometric_loss=np32(out["metrics"]["photometric_loss"]),
                smoothness_loss=np32(out["metrics"]["smoothness_loss"]),
@@ -230,16 +237,19 @@ def run_loss_case(name, case, B=2, H=24, W=80, seed=100):
         res[f"ctx{j}"] = np32(ctx[j])
     for i in range(S):
         res[f"sig{i}"] = np32(sig[i])
-        res[f"grad_sig{i}"] = np32(sig_p[i].grad)
-        if hasattr(loss_fn, "captured_min"):
+        # scales beyond ProgressiveScaling's n get no gradient in the reference (None -> zeros)
+        res[f"grad_sig{i}"] = np32(sig_p[i].grad) if sig_p[i].grad is not None else np.zeros_like(np32(sig[i]))
+        if hasattr(loss_fn, "captured_min") and i < len(loss_fn.captured_min):
             res[f"min{i}"] = np32(loss_fn.captured_min[i])
     res["kwargs_keys"] = np.array(sorted(kw.keys()))
     res["kwargs_vals"] = np.array([repr(kw[k]) for k in sorted(kw.keys())])
     return res
 
 
-def gen_losses():
+def gen_losses(only=None):
     for name, case in LOSS_CASES.items():
+        if only and name not in only:
+            continue
         res = run_loss_case(name, case)
         np.savez_compressed(os.path.join(OUT, f"loss_{name}.npz"), **res)
         print(f"  loss_{name}: loss={float(res['loss'][0]):.6f}")
@@ -391,6 +401,9 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["geom", "ssim", "losses", "kitti", "metrics", "step", "fisheye"]
     for w in which:
         print(f"[gen] {w}")
+        if w.startswith("losses:"):   # a subset of the loss cases: losses:name1,name2
+            gen_losses(w.split(":", 1)[1].split(","))
+            continue
         quiet = io.StringIO()
         with contextlib.redirect_stdout(quiet) if w == "metrics" else contextlib.nullcontext():
             {"geom": gen_geom, "ssim": gen_ssim, "losses": gen_losses, "kitti": gen_kitti_1img,
