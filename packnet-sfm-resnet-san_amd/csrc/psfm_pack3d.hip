@@ -30,10 +30,8 @@ int fail(int code, const std::string& msg) {
 }
 
 constexpr int NTH = 256;
-#ifndef PSFM_P3D_WAVES
-#define PSFM_P3D_WAVES 2
-#endif
-constexpr int ND = 8;  // Conv3d output features (PackNet d = 8)
+constexpr int P3D_WAVES = 2;
+// ND: Conv3d output features d — 8 (PackNet01) or 4 (PackNetSAN01, num_3d_feat = 4)
 
 struct P3 {
     int B, C, Hv, Wv, r, K, KG;  // K volume channels, KG chunks of channels per workgroup
@@ -102,6 +100,7 @@ __device__ __forceinline__ int64_t yaddr(const P3& a, int b, int o, int k, int y
     return b * a.ys[0] + c * a.ys[1] + (int64_t)(y * a.r + i) * a.ys[2] + (int64_t)(x * a.r + j) * a.ys[3];
 }
 
+template <int ND>
 __device__ __forceinline__ void load_weights(const P3& a, float* sw) {
     // sw[tap * 8 + o] = w[o][tap]; sw[216 + o] = bias[o]
     for (int i = threadIdx.x; i < 27 * ND; i += NTH) sw[i] = a.w[(i % ND) * 27 + i / ND];
@@ -109,12 +108,12 @@ __device__ __forceinline__ void load_weights(const P3& a, float* sw) {
 }
 
 // --------------------------------------------------------------------------------------------
-template <typename T, int MODE>
-__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WAVES))) void k_p3d_fwd(P3 a) {
+template <typename T, int MODE, int ND>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_fwd(P3 a) {
     constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sv[LY * LX * LK];
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
-    load_weights(a, sw);
+    load_weights<ND>(a, sw);
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
     const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
@@ -147,9 +146,12 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WA
                     for (int dx = 0; dx < 3; ++dx) {
                         const float v = sv[((py + dy) * LX + (px + dx)) * LK + dl + dz];
                         const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
-                        const float4 wa = w4[0], wb = w4[1];
-                        acc[0] += wa.x * v; acc[1] += wa.y * v; acc[2] += wa.z * v; acc[3] += wa.w * v;
-                        acc[4] += wb.x * v; acc[5] += wb.y * v; acc[6] += wb.z * v; acc[7] += wb.w * v;
+#pragma unroll
+                        for (int h = 0; h < ND / 4; ++h) {
+                            const float4 wv = w4[h];
+                            acc[4 * h + 0] += wv.x * v; acc[4 * h + 1] += wv.y * v;
+                            acc[4 * h + 2] += wv.z * v; acc[4 * h + 3] += wv.w * v;
+                        }
                     }
 #pragma unroll
             for (int o = 0; o < ND; ++o) st<T>(a.y, yaddr<MODE>(a, b, o, k, gy, gx), acc[o]);
@@ -159,12 +161,12 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WA
 
 // --------------------------------------------------------------------------------------------
 // dV[k, y, x] = sum_o sum_taps w[o, dz, dy, dx] dy[o, k - dz + 1, y - dy + 1, x - dx + 1]
-template <typename T, int MODE>
-__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WAVES))) void k_p3d_bwd_x(P3 a) {
+template <typename T, int MODE, int ND>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_bwd_x(P3 a) {
     constexpr int TY = 4, TX = 8, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sg[LY * LX * ND * LK];  // [yy][xx][o][kk]
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
-    load_weights(a, sw);
+    load_weights<ND>(a, sw);
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
     const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
@@ -221,9 +223,12 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WA
                     for (int dx = 0; dx < 3; ++dx) {
                         const float* g = sg + (((py + 2 - dy) * LX + (px + 2 - dx)) * ND) * LK + dl + 2 - dz;
                         const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
-                        const float4 wa = w4[0], wb = w4[1];
-                        acc += wa.x * g[0 * LK] + wa.y * g[1 * LK] + wa.z * g[2 * LK] + wa.w * g[3 * LK] +
-                               wb.x * g[4 * LK] + wb.y * g[5 * LK] + wb.z * g[6 * LK] + wb.w * g[7 * LK];
+#pragma unroll
+                        for (int h = 0; h < ND / 4; ++h) {
+                            const float4 wv = w4[h];
+                            acc += wv.x * g[(4 * h + 0) * LK] + wv.y * g[(4 * h + 1) * LK] +
+                                   wv.z * g[(4 * h + 2) * LK] + wv.w * g[(4 * h + 3) * LK];
+                        }
                     }
             st<T>(a.dx, vaddr<MODE>(a, b, k, gy, gx), acc);
         }
@@ -231,8 +236,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(PSFM_P3D_WA
 }
 
 // --------------------------------------------------------------------------------------------
-// per-workgroup partials: thread t < 216 -> (tap = t / 8, o = t % 8) of dw; 216..223 -> dbias[o]
-template <typename T, int MODE>
+// per-workgroup partials: thread t < 27 ND -> (tap = t / ND, o = t % ND) of dw; the next ND -> dbias[o]
+template <typename T, int MODE, int ND>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) {
     constexpr int TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sv[LY * LX * LK];         // [yy][xx][kk] with halo
@@ -283,6 +288,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) {
 
 // fixed-order fp64 reduction of the partials -> dw [o][tap], dbias [o]: one workgroup per output
 // (strided fp64 partial sums per thread, then the wave butterflies and the 4 waves in order)
+template <int ND>
 __global__ __launch_bounds__(NTH) void k_p3d_reduce_w(const float* ws, int64_t nblk, float* dw, float* db) {
     __shared__ double red[NTH / 64];
     const int t = blockIdx.x, tid = threadIdx.x;
@@ -312,8 +318,8 @@ int check_desc(const psfm_p3d_desc* t) {
     if (t->mode != PSFM_P3D_PACK && t->mode != PSFM_P3D_UNPACK) return fail(-2, "bad mode");
     if (t->dtype != PSFM_P3D_F32 && t->dtype != PSFM_P3D_BF16) return fail(-2, "bad dtype");
     if (t->B < 1 || t->C < 1 || t->Hv < 1 || t->Wv < 1 || t->r < 1) return fail(-3, "bad shape");
-    if (t->d != ND) return fail(-4, "d (3-D features) must be 8");
-    if (t->mode == PSFM_P3D_UNPACK && (ND * t->C) % (t->r * t->r)) return fail(-3, "d*C not divisible by r^2");
+    if (t->d != 4 && t->d != 8) return fail(-4, "d (3-D features) must be 4 or 8");
+    if (t->mode == PSFM_P3D_UNPACK && (t->d * t->C) % (t->r * t->r)) return fail(-3, "d*C not divisible by r^2");
     return 0;
 }
 
@@ -332,19 +338,26 @@ P3 make(const psfm_p3d_desc* t) {
     return a;
 }
 
-#define P3D_LAUNCH(KERNEL, grid, st, a, t)                                                              \
+#define P3D_LAUNCH_D(KERNEL, ND, grid, st, a, t)                                                        \
     do {                                                                                                \
         if ((t)->dtype == PSFM_P3D_BF16) {                                                              \
             if ((t)->mode == PSFM_P3D_PACK)                                                             \
-                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);       \
+                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_PACK, ND>), grid, dim3(NTH), 0, st, a);   \
             else                                                                                        \
-                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);     \
+                hipLaunchKernelGGL((KERNEL<uint16_t, PSFM_P3D_UNPACK, ND>), grid, dim3(NTH), 0, st, a); \
         } else {                                                                                        \
             if ((t)->mode == PSFM_P3D_PACK)                                                             \
-                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);          \
+                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_PACK, ND>), grid, dim3(NTH), 0, st, a);      \
             else                                                                                        \
-                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);        \
+                hipLaunchKernelGGL((KERNEL<float, PSFM_P3D_UNPACK, ND>), grid, dim3(NTH), 0, st, a);    \
         }                                                                                               \
+    } while (0)
+#define P3D_LAUNCH(KERNEL, grid, st, a, t)                                                              \
+    do {                                                                                                \
+        if ((t)->d == 4)                                                                                \
+            P3D_LAUNCH_D(KERNEL, 4, grid, st, a, t);                                                    \
+        else                                                                                            \
+            P3D_LAUNCH_D(KERNEL, 8, grid, st, a, t);                                                    \
     } while (0)
 
 dim3 grid_of(P3& a, int TY, int TX, int DC) {
@@ -375,7 +388,7 @@ int64_t psfm_p3d_ws_floats(const psfm_p3d_desc* t) {
     if (check_desc(t)) return -1;
     P3 a = make(t);
     const dim3 g = grid_of(a, 4, 16, 16);
-    return (int64_t)g.x * g.y * g.z * (27 * ND + ND);
+    return (int64_t)g.x * g.y * g.z * 28 * t->d;
 }
 
 int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const void* dy, void* dx, float* dw,
@@ -391,7 +404,7 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
     a.w = w;
     {
         // the fast staging path indexes dy with int32 offsets from each image's base
-        const int64_t mx = (int64_t)(ND * a.K - 1) * a.ys[1] + (int64_t)(a.Hv - 1) * a.ys[2] + (int64_t)(a.Wv - 1) * a.ys[3];
+        const int64_t mx = (int64_t)(t->d * a.K - 1) * a.ys[1] + (int64_t)(a.Hv - 1) * a.ys[2] + (int64_t)(a.Wv - 1) * a.ys[3];
         a.dy32 = a.ys[1] >= 0 && a.ys[2] >= 0 && a.ys[3] >= 0 && mx < (int64_t)INT32_MAX;
     }
     if (dx) {
@@ -405,8 +418,11 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         aw.ws = ws;
         const dim3 grid = grid_of(aw, 4, 16, 16);
         P3D_LAUNCH(k_p3d_bwd_w, grid, st, aw, t);
-        hipLaunchKernelGGL(k_p3d_reduce_w, dim3(27 * ND + ND), dim3(NTH), 0, st, (const float*)ws,
-                           (int64_t)grid.x * grid.y * grid.z, dw, dbias);
+        const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
+        if (t->d == 4)
+            hipLaunchKernelGGL(k_p3d_reduce_w<4>, dim3(28 * 4), dim3(NTH), 0, st, (const float*)ws, nblk, dw, dbias);
+        else
+            hipLaunchKernelGGL(k_p3d_reduce_w<8>, dim3(28 * 8), dim3(NTH), 0, st, (const float*)ws, nblk, dw, dbias);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail((int)e, std::string("launch: ") + hipGetErrorString(e));

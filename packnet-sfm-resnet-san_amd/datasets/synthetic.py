@@ -114,7 +114,8 @@ class ResidentLoader:
         self._load_epoch()
 
     def _load_epoch(self):
-        self.sampler.set_epoch(self.epoch)
+        if hasattr(self.sampler, "set_epoch"):
+            self.sampler.set_epoch(self.epoch)
         self.partition = list(iter(self.sampler))   # this epoch's sample indices for this rank
         local = torch.tensor(self.partition, dtype=torch.int64)
         n = (len(local) // self.B) * self.B if self.drop_last else len(local)

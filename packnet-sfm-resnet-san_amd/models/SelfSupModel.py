@@ -11,6 +11,7 @@ import torch
 from ..losses.multiview_photometric_loss import MultiViewPhotometricLoss
 from .SfmModel import SfmModel
 from .model_utils import merge_outputs
+from ..datasets.synthetic import flatten_cameras
 
 
 class SelfSupModel(SfmModel):
@@ -29,6 +30,8 @@ class SelfSupModel(SfmModel):
                                       return_logs=return_logs, progress=progress, mask=mask)
 
     def forward(self, batch, return_logs=False, progress=0.0, masks=None, **kwargs):
+        if batch["rgb"].dim() == 5:   # multi-camera samples: cameras -> batch (SfmModel.forward)
+            batch = flatten_cameras(batch)
         output = super().forward(batch, return_logs=return_logs)
         if not self.training:
             return output

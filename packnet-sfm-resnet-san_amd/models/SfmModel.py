@@ -7,6 +7,7 @@ import torch
 from ..geometry.pose import Pose
 from .base_model import BaseModel
 from .model_utils import flip_batch_input, flip_output, upsample_output
+from ..datasets.synthetic import flatten_cameras
 from ..utils.misc import filter_dict
 
 
@@ -57,6 +58,8 @@ class SfmModel(BaseModel):
         return self._side_streams[device]
 
     def forward(self, batch, return_logs=False, force_flip=False, **kwargs):
+        if batch["rgb"].dim() == 5:   # multi-camera samples [B, cams, 3, H, W] (DDAD): cameras -> batch
+            batch = flatten_cameras(batch)   # == model_utils.stack_batch for B = 1 (model_utils.py:68-94)
         poses = None
         want_pose = "rgb_context" in batch and self.pose_net is not None
         if want_pose and self.overlap_pose_net and batch["rgb"].is_cuda:

@@ -4,8 +4,10 @@
 def load_depth_net(name, **kwargs):
     from .depth.DepthResNet import DepthResNet
     from .depth.PackNet01 import PackNet01
+    from .depth.PackNetSAN01 import PackNetSAN01
     from .depth.ResNetSAN01 import ResNetSAN01
-    nets = {"DepthResNet": DepthResNet, "PackNet01": PackNet01, "ResNetSAN01": ResNetSAN01}
+    nets = {"DepthResNet": DepthResNet, "PackNet01": PackNet01, "PackNetSAN01": PackNetSAN01,
+            "ResNetSAN01": ResNetSAN01}
     if name not in nets:
         raise ValueError(f"depth net {name} is not provided (available: {sorted(nets)})")
     return nets[name](**kwargs)

@@ -182,3 +182,24 @@ def test_all_reduce_metrics_asserts_every_sample_seen():
         all_reduce_metrics(outs, [list(range(3))])
     res = all_reduce_metrics(outs + [{"idx": torch.tensor([2]), "depth": 3 * torch.ones(7)}], [list(range(3))])
     torch.testing.assert_close(res[0]["depth"], torch.full((7,), 5.0 / 3))
+
+
+def test_multicamera_batches_fold_cameras_into_the_batch():
+    """DDAD samples carry [cameras, 3, H, W] per key (train_packnet_san_ddad.yaml: 4 cameras); the
+    resident loader and the models fold cameras into the batch like model_utils.stack_batch, with
+    each camera keeping its own intrinsics."""
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.datasets.synthetic import ResidentLoader, SyntheticSfmDataset, flatten_cameras
+    from packnet_sfm_amd.models.model_utils import stack_batch
+    ds = SyntheticSfmDataset(4, 16, 32, cameras=4, seed=1)
+    s = ds[2]
+    assert s["rgb"].shape == (4, 3, 16, 32) and s["intrinsics"].shape == (4, 3, 3)
+    one = {"rgb": s["rgb"][None], "rgb_context": [c[None] for c in s["rgb_context"]],
+           "intrinsics": s["intrinsics"][None]}
+    flat, ref = flatten_cameras(dict(one)), stack_batch(dict(one))
+    assert torch.equal(flat["rgb"], ref["rgb"]) and torch.equal(flat["intrinsics"], ref["intrinsics"])
+    assert all(torch.equal(a, b) for a, b in zip(flat["rgb_context"], ref["rgb_context"]))
+    loader = ResidentLoader(ds, 2, torch.utils.data.SequentialSampler(ds), torch.device("cpu"))
+    b = loader.next_into(None)
+    assert b["rgb"].shape == (8, 3, 16, 32) and b["intrinsics"].shape == (8, 3, 3)
+    assert torch.equal(b["rgb"][4:8], ds[1]["rgb"]) and torch.equal(b["intrinsics"][4:8], ds[1]["intrinsics"])

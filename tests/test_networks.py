@@ -99,3 +99,88 @@ def test_selfsup_step_on_gpu_matches_reference():
     for name, ref in zip(z["grad_names"], z["grad_norms"]):
         got = float(params[str(name)].grad.double().norm())
         assert abs(got - ref) / ref < 2e-2, (name, got, ref)
+
+
+def _packnet_san_model():
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.networks.depth.PackNetSAN01 import PackNetSAN01
+    from packnet_sfm_amd.networks.pose.PoseNet import PoseNet
+    depth, pose = PackNetSAN01(version="1A", dropout=None), PoseNet(nb_ref_imgs=2)
+    gu.det_init_(depth)
+    gu.det_init_(pose)
+    return depth, pose
+
+
+def test_packnet_san_parameters_match_reference():
+    """PackNetSAN01 RGB path: the reference's parameter names (checkpoint keys, minus the absent
+    MinkowskiEncoder) and count (BASELINE configs 3 / 5)."""
+    z = gu.load_golden("step_packnet_san_tiny")
+    depth, _ = _packnet_san_model()
+    assert [n for n, _ in depth.named_parameters()] == [str(n) for n in z["param_names"]]
+    assert sum(p.numel() for p in depth.parameters()) == int(z["param_count"])
+
+
+def test_packnet_san_step_matches_reference_cpu():
+    """PackNetSAN01 + PoseNet forward (ours, CPU: the reference op chain) + oracle loss == the
+    reference SelfSupModel step (tests/golden/step_packnet_san_tiny.npz)."""
+    from oracle import photometric_oracle as O
+    z = gu.load_golden("step_packnet_san_tiny")
+    depth, pose = _packnet_san_model()
+    depth.train()
+    pose.train()
+    g = torch.Generator().manual_seed(78)
+    rgb = gu.smooth_texture(g, 1, 3, 64, 192)
+    ctx = [gu.smooth_texture(g, 1, 3, 64, 192) for _ in range(2)]
+    K = gu.kitti_K(1, 64, 192)
+    torch.set_num_threads(8)
+    inv = depth(rgb)["inv_depths"]
+    assert [list(t.shape) for t in inv] == [[1, 1, 64 >> i, 192 >> i] for i in range(4)]
+    inv_up = [torch.nn.functional.interpolate(i, size=(64, 192), mode="nearest") for i in inv]
+    assert [list(t.shape) for t in inv_up] == z["inv_shapes"].tolist()   # SfmModel.upsample_output
+    for t, ref in zip(inv_up, z["inv_sums"]):
+        assert abs(float(t.double().sum()) - ref) / abs(ref) < 1e-4
+    np.testing.assert_allclose(inv_up[0].reshape(-1)[::997].detach().numpy(), z["inv0_samples"], rtol=1e-4)
+    vec = pose(rgb, ctx)
+    mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+    np.testing.assert_allclose(torch.stack(mats, 1).detach().numpy(), z["pose_mats"], rtol=1e-4, atol=1e-6)
+    loss, photo, smooth, _ = O.photometric_loss(rgb, ctx, inv_up, K, K, mats, torch.ones(1, 1, 64, 192))
+    assert gu.rel_err(loss.detach(), z["loss"]) < 1e-4
+    assert gu.rel_err(smooth.detach(), z["smoothness_loss"]) < 1e-4
+    depth.eval()
+    with torch.no_grad():
+        ev = depth(rgb)["inv_depths"]
+    assert len(ev) == int(z["eval_len"]) == 1
+    assert abs(float(ev[0].double().sum()) - float(z["eval_inv0_sum"])) / abs(float(z["eval_inv0_sum"])) < 1e-4
+
+
+@pytest.mark.gpu
+def test_selfsup_packnet_san_step_on_gpu_matches_reference():
+    """PackNetSAN01 (fused d=4 pack / unpack kernels) + PoseNet + HIP loss on the GPU vs the
+    reference golden: loss, smoothness, and 16 parameter-gradient norms."""
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.models.SelfSupModel import SelfSupModel
+    z = gu.load_golden("step_packnet_san_tiny")
+    dev = torch.device("cuda:0")
+    depth, pose = _packnet_san_model()
+    model = SelfSupModel(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
+                         automask_loss=True, clip_loss=0.0, min_depth=0.5, max_depth=80.0,
+                         upsample_depth_maps=True, rotation_mode="euler")
+    model.add_depth_net(depth)
+    model.add_pose_net(pose)
+    model = model.to(dev).train()
+    g = torch.Generator().manual_seed(78)
+    rgb = gu.smooth_texture(g, 1, 3, 64, 192).to(dev)
+    ctx = [gu.smooth_texture(g, 1, 3, 64, 192).to(dev) for _ in range(2)]
+    K = gu.kitti_K(1, 64, 192).to(dev)
+    batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx, intrinsics=K,
+                 mask=torch.ones(1, 1, 64, 192, device=dev))
+    out = model(batch, progress=0.0)
+    out["loss"].sum().backward()
+    assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < 1e-4
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < 1e-4
+    params = {f"depth_net.{n}": p for n, p in model.depth_net.named_parameters()}
+    params.update({f"pose_net.{n}": p for n, p in model.pose_net.named_parameters()})
+    for name, ref in zip(z["grad_names"], z["grad_norms"]):
+        got = float(params[str(name)].grad.double().norm())
+        assert abs(got - ref) / ref < 2e-2, (name, got, ref)

@@ -24,7 +24,7 @@ def dev():
 
 def _ref(mode, x, w, b, r):
     from packnet_sfm_amd.networks.layers.packnet.layers01 import packing
-    conv = nn.Conv3d(1, 8, 3, 1, 1).double()
+    conv = nn.Conv3d(1, w.shape[0], 3, 1, 1).double()
     with torch.no_grad():
         conv.weight.copy_(w.double())
         conv.bias.copy_(b.double())
@@ -38,18 +38,21 @@ def _ref(mode, x, w, b, r):
     return xd, conv, y
 
 
+@pytest.mark.parametrize("d", [8, 4])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape,cl", [((2, 5, 14, 38), True), ((1, 16, 24, 40), False), ((2, 3, 6, 70), True)])
-def test_matches_reference_chain(dev, mode, dtype, shape, cl):
+@pytest.mark.parametrize("shape,cl", [((2, 5, 14, 38), True), ((1, 16, 24, 40), False), ((2, 3, 6, 70), True),
+                                      ((1, 40, 10, 36), True)])
+def test_matches_reference_chain(dev, mode, dtype, shape, cl, d):
+    """d = 8: PackNet01; d = 4: PackNetSAN01 (num_3d_feat = 4)."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
-    g = torch.Generator().manual_seed(sum(shape) + mode)
+    g = torch.Generator().manual_seed(sum(shape) + mode + d)
     B, C, H, W = shape
     if mode == 1:
-        C = C * 4 // 4 * 2  # d*C divisible by r^2 = 4 (d = 8: always)
+        C = C * 2  # d*C divisible by r^2 = 4
     x = torch.randn(B, C, H, W, generator=g).to(dtype)
-    w = (torch.randn(8, 1, 3, 3, 3, generator=g) * 0.2)
-    b = torch.randn(8, generator=g) * 0.1
+    w = (torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2)
+    b = torch.randn(d, generator=g) * 0.1
     xd, conv, yref = _ref(mode, x.float(), w, b, 2)
     gy = torch.randn(yref.shape, generator=g).to(dtype).float()   # the upstream gradient in storage dtype
     (yref * gy.double()).sum().backward()
@@ -75,7 +78,9 @@ def test_pack_layers_use_fused_op_and_match_torch(dev):
     from packnet_sfm_amd.networks.layers.packnet import pack3d
     from packnet_sfm_amd.networks.layers.packnet.layers01 import PackLayerConv3d, UnpackLayerConv3d
     torch.manual_seed(0)
-    for mod, shape in ((PackLayerConv3d(16, 3), (2, 16, 16, 32)), (UnpackLayerConv3d(32, 32, 3), (2, 32, 8, 16))):
+    for mod, shape in ((PackLayerConv3d(16, 3), (2, 16, 16, 32)), (UnpackLayerConv3d(32, 32, 3), (2, 32, 8, 16)),
+                       (PackLayerConv3d(32, 5, d=4), (2, 32, 16, 32)),
+                       (UnpackLayerConv3d(64, 32, 3, d=4), (2, 64, 8, 16))):
         mod = mod.to(dev)
         x = torch.randn(shape, device=dev)
         pack3d.ENABLED = False

@@ -329,6 +329,63 @@ def gen_step_packnet():
     print(f"  step_packnet_tiny: loss={float(res['loss'][0]):.6f}")
 
 
+def gen_step_packnet_san():
+    """SelfSupModel(PackNetSAN01 '1A' RGB path + PoseNet) forward+backward, B=1, 64x192 — the depth
+    net of BASELINE configs 3 and 5.  Harness stub: `MinkowskiEncoder` (the SAN LiDAR branch, which
+    needs the absent MinkowskiEngine and is never called without input_depth) is replaced by a
+    parameter-free module.  dropout=None (the YAMLs' 0.5 makes the training forward random)."""
+    import torch.nn as nn
+    stub = types.ModuleType("packnet_sfm.networks.layers.minkowski_encoder")
+    stub.MinkowskiEncoder = lambda *a, **k: nn.Module()
+    sys.modules["packnet_sfm.networks.layers.minkowski_encoder"] = stub
+    from packnet_sfm.models.SelfSupModel import SelfSupModel
+    from packnet_sfm.networks.depth.PackNetSAN01 import PackNetSAN01
+    from packnet_sfm.networks.pose.PoseNet import PoseNet
+
+    B, H, W = 1, 64, 192
+    torch.manual_seed(0)
+    model = SelfSupModel(**{**BASE_KW, "upsample_depth_maps": True, "rotation_mode": "euler"})
+    model.add_depth_net(PackNetSAN01(version="1A", dropout=None))
+    model.add_pose_net(PoseNet(nb_ref_imgs=2))
+    model._photometric_loss = HarnessLoss(**BASE_KW)   # pinhole warp override (§8c step 3)
+    gu.det_init_(model.depth_net)
+    gu.det_init_(model.pose_net)
+    model.train()
+    g = torch.Generator().manual_seed(78)
+    rgb = gu.smooth_texture(g, B, 3, H, W)
+    ctx = [gu.smooth_texture(g, B, 3, H, W) for _ in range(2)]
+    K = gu.kitti_K(B, H, W)
+    batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx,
+                 intrinsics=K, distortion_coeffs=K, mask=torch.ones(B, 1, H, W))
+    out = model(batch, progress=0.0)
+    out["loss"].sum().backward()
+    names, norms = [], []
+    for net in ("depth_net", "pose_net"):
+        for n, p in sorted(getattr(model, net).named_parameters()):
+            if p.grad is not None and p.dim() >= 2:
+                names.append(f"{net}.{n}")
+                norms.append(float(p.grad.double().norm()))
+    sel = list(range(0, len(names), max(1, len(names) // 16)))[:16]
+    inv = out["inv_depths"]
+    model.depth_net.eval()
+    with torch.no_grad():
+        ev = model.depth_net(rgb)["inv_depths"]
+    res = dict(loss=np32(out["loss"]),
+               photometric_loss=np32(out["metrics"]["photometric_loss"]),
+               smoothness_loss=np32(out["metrics"]["smoothness_loss"]),
+               inv_sums=np.array([float(t.double().sum()) for t in inv]),
+               inv_shapes=np.array([list(t.shape) for t in inv]),
+               inv0_samples=np32(inv[0].reshape(-1)[::997]),
+               eval_len=np.int64(len(ev)), eval_inv0_sum=np.float64(ev[0].double().sum()),
+               pose_mats=np32(torch.stack([p.mat for p in out["poses"]], 1)),
+               param_names=np.array([n for n, _ in model.depth_net.named_parameters()]),
+               param_count=np.int64(sum(p.numel() for p in model.depth_net.parameters())),
+               grad_names=np.array([names[i] for i in sel]),
+               grad_norms=np.array([norms[i] for i in sel], dtype=np.float64))
+    np.savez_compressed(os.path.join(OUT, "step_packnet_san_tiny.npz"), **res)
+    print(f"  step_packnet_san_tiny: loss={float(res['loss'][0]):.6f} params={int(res['param_count'])}")
+
+
 def gen_fisheye():
     """FisheyeCamera (VADAS) geometry + the photometric loss on fisheye cameras (24x80, B=2)."""
     from packnet_sfm.geometry.camera import FisheyeCamera
@@ -407,5 +464,6 @@ if __name__ == "__main__":
         quiet = io.StringIO()
         with contextlib.redirect_stdout(quiet) if w == "metrics" else contextlib.nullcontext():
             {"geom": gen_geom, "ssim": gen_ssim, "losses": gen_losses, "kitti": gen_kitti_1img,
-             "metrics": gen_depth_metrics, "step": gen_step_packnet, "fisheye": gen_fisheye}[w]()
+             "metrics": gen_depth_metrics, "step": gen_step_packnet, "fisheye": gen_fisheye,
+             "step_san": gen_step_packnet_san}[w]()
     print("done")
