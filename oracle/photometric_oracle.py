@@ -269,7 +269,7 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
             reduced.append(None)
         elif tie_flip is not None:
             vals = torch.cat(cands[i], 1)
-            order = vals.detach().sort(1, stable=True)[1]          # first index first on exact ties
+            order = vals.detach().sort(dim=1, stable=True)[1]          # first index first on exact ties
             pick = torch.where(tie_flip[i].to(vals.device), order[:, 1:2], order[:, 0:1])
             m = vals.gather(1, pick)
             reduced.append(m)

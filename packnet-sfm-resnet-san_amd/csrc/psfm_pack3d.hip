@@ -8,7 +8,9 @@
 // weights in LDS ([tap][o]: two b128 broadcast reads per tap), and write every folded /
 // pixel-shuffled output element exactly once, straight into the caller's layout (strides).
 //   k_p3d_fwd      y  = conv3d(V)            4 x 16 pixels x 32 k per chunk
-//   k_p3d_bwd_x    dV = conv3d^T(dy)         4 x 8 pixels x 16 k, dy tile with halo in LDS
+//   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: 4 x 16 pixels x 16 k,
+//                                            16-byte staged halo tile, 4 pixels per thread
+//   k_p3d_bwd_x    dV = conv3d^T(dy)         any other layout: 4 x 8 pixels x 16 k
 //   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (tap, o)), fixed-order fp64 reduce
 // V is the virtual volume: pack = space-to-depth view of x (channel k = c r^2 + i r + j),
 // unpack = x itself; the output channel o K + k is folded (pack) or pixel-shuffled (unpack).
@@ -174,37 +176,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
     for (int ch = c_lo; ch < c_hi; ++ch) {
         const int k0 = ch * DC;
         __syncthreads();
-        if (MODE == PSFM_P3D_PACK && a.dy32) {
-            // e = ((yy LX + xx) ND + o) LK + kk walked in steps of NTH as a mixed-radix counter
-            // (no divisions), 32-bit offsets from the image's base
-            constexpr int S0 = NTH % LK, C0 = NTH / LK, S1 = C0 % ND, C1 = C0 / ND, S2 = C1 % LX, S3 = C1 / LX;
-            const T* dyb = static_cast<const T*>(a.dy) + b * a.ys[0];
-            const int ys1 = (int)a.ys[1], ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
-            const int t = threadIdx.x;
-            int kk = t % LK, o = (t / LK) % ND, xx = (t / (LK * ND)) % LX, yy = t / (LK * ND * LX);
-            for (int e = t; e < LY * LX * ND * LK; e += NTH) {
-                const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
-                const bool in = (unsigned)gk < (unsigned)a.K && (unsigned)gy < (unsigned)a.Hv &&
-                                (unsigned)gx < (unsigned)a.Wv;
-                sg[e] = in ? ldi<T>(dyb, (o * a.K + gk) * ys1 + gy * ys2 + gx * ys3) : 0.0f;
-                kk += S0;
-                int c = kk >= LK;
-                kk -= c ? LK : 0;
-                o += S1 + c;
-                c = o >= ND;
-                o -= c ? ND : 0;
-                xx += S2 + c;
-                c = xx >= LX;
-                xx -= c ? LX : 0;
-                yy += S3 + c;
-            }
-        } else {
-            for (int e = threadIdx.x; e < LY * LX * ND * LK; e += NTH) {
-                const int kk = e % LK, r1 = e / LK, o = r1 % ND, r2 = r1 / ND, xx = r2 % LX, yy = r2 / LX;
-                const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
-                const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
-                sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, o, gk, gy, gx)) : 0.0f;
-            }
+        for (int e = threadIdx.x; e < LY * LX * ND * LK; e += NTH) {
+            const int kk = e % LK, r1 = e / LK, o = r1 % ND, r2 = r1 / ND, xx = r2 % LX, yy = r2 / LX;
+            const int gk = k0 - 1 + kk, gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+            const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
+            sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, o, gk, gy, gx)) : 0.0f;
         }
         __syncthreads();
         const int k = k0 + dl;
@@ -231,6 +207,95 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
                         }
                     }
             st<T>(a.dx, vaddr<MODE>(a, b, k, gy, gx), acc);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// dx for PACK with a channel-contiguous dy (channels_last: the folded channel o K + k is the
+// innermost index — the layout the nets run in).  Per 4 x 16 pixels x 16 k chunk the dy halo tile
+// (6 x 18 pixels x ND x 18 k) is staged with 16-byte loads (every load of a thread issued before
+// the first LDS write) into fp32 LDS [yy][xx][o][pos], pos = k - k0 + 2; each thread then
+// computes 4 neighbouring pixels of one k (register blocking along x: 6 LDS reads per 12 FMAs;
+// the per-pixel stride is 4 mod 8 words, so the x-blocked reads of a half-wave hit 32 distinct
+// banks).  Weights are wave-uniform and come through the scalar path (SGPR operands).
+template <typename T, int ND>
+__global__ __launch_bounds__(NTH, 2) void k_p3d_bwd_x_cl(P3 a) {
+    constexpr int TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2;
+    constexpr int OS = 20;                // per-o run: pos 1 = k0-1, 2..17 = k0..k0+15, 18 = k0+16
+    constexpr int PS = ND * OS + 4;       // per-pixel stride (4 mod 8)
+    constexpr int VEC = 16 / sizeof(T);   // elements per 16-byte load
+    constexpr int UNITS = LY * LX * ND;   // (pixel, o) runs per chunk
+    constexpr int ITER = (UNITS + NTH - 1) / NTH;
+    __shared__ __attribute__((aligned(16))) float sg[LY * LX * PS];
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int t = threadIdx.x, dl = t % DC, r = t / DC, py = r / 4, px0 = (r % 4) * 4;
+    const T* dyb = static_cast<const T*>(a.dy) + b * a.ys[0];
+    const int ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC;
+        uint4 v[ITER][DC / VEC];
+        float e0[ITER], e1[ITER];
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+            const int u = t + i * NTH;
+            const int yy = u / (LX * ND), rem = u - yy * (LX * ND), xx = rem / ND, o = rem - xx * ND;
+            const int gy = y0 - 1 + yy, gx = x0 - 1 + xx;
+            const bool in = u < UNITS && (unsigned)gy < (unsigned)a.Hv && (unsigned)gx < (unsigned)a.Wv;
+            const T* src = dyb + (in ? gy * ys2 + gx * ys3 + o * a.K + k0 : 0);
+#pragma unroll
+            for (int j = 0; j < DC / VEC; ++j)
+                v[i][j] = in ? reinterpret_cast<const uint4*>(src)[j] : make_uint4(0, 0, 0, 0);
+            e0[i] = in && k0 > 0 ? ldi<T>(src, -1) : 0.0f;
+            e1[i] = in && k0 + DC < a.K ? ldi<T>(src, DC) : 0.0f;
+        }
+        __syncthreads();   // the previous chunk's reads of sg are done
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+            const int u = t + i * NTH;
+            if (u >= UNITS) break;
+            const int yy = u / (LX * ND), rem = u - yy * (LX * ND), xx = rem / ND, o = rem - xx * ND;
+            float* d = sg + (yy * LX + xx) * PS + o * OS;
+            d[1] = e0[i];
+            d[DC + 2] = e1[i];
+            float2* d2 = reinterpret_cast<float2*>(d + 2);
+#pragma unroll
+            for (int j = 0; j < DC / VEC; ++j) {
+                const uint32_t w4[4] = {v[i][j].x, v[i][j].y, v[i][j].z, v[i][j].w};
+                if (sizeof(T) == 2) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        d2[j * 4 + q] = make_float2(__uint_as_float(w4[q] << 16), __uint_as_float(w4[q] & 0xffff0000u));
+                } else {
+                    d2[j * 2 + 0] = make_float2(__uint_as_float(w4[0]), __uint_as_float(w4[1]));
+                    d2[j * 2 + 1] = make_float2(__uint_as_float(w4[2]), __uint_as_float(w4[3]));
+                }
+            }
+        }
+        __syncthreads();
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+        for (int o = 0; o < ND; ++o)
+#pragma unroll
+            for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    const float* g = sg + ((py + 2 - dy) * LX + px0) * PS + o * OS + dl + 3 - dz;
+                    float g6[6];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) g6[j] = g[j * PS];
+                    const float* w = a.w + o * 27 + (dz * 3 + dy) * 3;
+                    const float w0 = w[0], w1 = w[1], w2 = w[2];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] += w0 * g6[q + 2] + w1 * g6[q + 1] + w2 * g6[q];
+                }
+        const int k = k0 + dl, gy = y0 + py;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int gx = x0 + px0 + q;
+            if (gy < a.Hv && gx < a.Wv) st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k, gy, gx), acc[q]);
         }
     }
 }
@@ -408,8 +473,24 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         a.dy32 = a.ys[1] >= 0 && a.ys[2] >= 0 && a.ys[3] >= 0 && mx < (int64_t)INT32_MAX;
     }
     if (dx) {
-        const dim3 grid = grid_of(a, 4, 8, 16);
-        P3D_LAUNCH(k_p3d_bwd_x, grid, st, a, t);
+        // channel-contiguous dy of a pack layer (channels_last), every 16-k run 16-byte aligned
+        const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
+        const bool cl = t->mode == PSFM_P3D_PACK && a.dy32 && a.ys[1] == 1 && a.K % 16 == 0 &&
+                        a.ys[0] % vec == 0 && a.ys[2] % vec == 0 && a.ys[3] % vec == 0 &&
+                        (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+        if (cl) {
+            const dim3 grid = grid_of(a, 4, 16, 16);
+            if (t->dtype == PSFM_P3D_BF16) {
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 4>), grid, dim3(NTH), 0, st, a);
+                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 8>), grid, dim3(NTH), 0, st, a);
+            } else {
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 4>), grid, dim3(NTH), 0, st, a);
+                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 8>), grid, dim3(NTH), 0, st, a);
+            }
+        } else {
+            const dim3 grid = grid_of(a, 4, 8, 16);
+            P3D_LAUNCH(k_p3d_bwd_x, grid, st, a, t);
+        }
     }
     if (dw || dbias) {
         P3 aw = make(t);

@@ -81,9 +81,9 @@ def test_world2_flat_allreduce_algebra_on_fused_adam():
     world = 2
     g = torch.Generator(device=dev).manual_seed(3)
     for step in range(3):
-        per_rank = [[torch.randn(q.shape, device=dev, generator=g).to(p.dtype)
-                     .contiguous(memory_format=torch.channels_last if q.dim() == 4 else torch.contiguous_format)
-                     for p, q in zip(ps, qs)] for _ in range(world)]
+        per_rank = [[torch.empty_strided(p.shape, p.stride(), device=dev, dtype=p.dtype)
+                     .copy_(torch.randn(q.shape, device=dev, generator=g)) for p, q in zip(ps, qs)]
+                    for _ in range(world)]
         total = fused.new_flat_grad()
         for grads in per_rank:
             for p, gr in zip(ps, grads):

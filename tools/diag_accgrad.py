@@ -1,4 +1,7 @@
-"""Which phase of the graph trainer emits the AccumulateGrad stream-mismatch warning?"""
+"""Which configuration of the graph trainer emits the AccumulateGrad stream-mismatch warning at
+capture?  (a) default, (b) pose net on the current stream, (c) gc.collect() before capture,
+(d) no autocast (fp32 nets)."""
+import gc
 import os
 import sys
 import warnings
@@ -18,29 +21,41 @@ class A:
     depth_net, pose_net, batch, height, width = "ResNetSAN01", "PoseNet", 2, 64, 192
 
 
-torch.manual_seed(0)
-m = bench.to_channels_last(bench.build_model(A, dev))
-tr = T.DDPTrainer(m, T.make_optimizer(m, 1e-4, 1e-4, capturable=True, fused=True), dev, amp_dtype=torch.bfloat16,
-                  graph=True, bf16_weights=True)
-b = bench.synthetic_batch(2, 64, 192, dev, seed=0, channels_last=True)
-orig_fb = tr._forward_backward
-phase = {"name": "?", "i": 0}
+def run(tag, overlap=True, collect=False, amp=True):
+    torch.manual_seed(0)
+    m = bench.to_channels_last(bench.build_model(A, dev))
+    m.overlap_pose_net = overlap
+    tr = T.DDPTrainer(m, T.make_optimizer(m, 1e-4, 1e-4, capturable=True, fused=amp), dev,
+                      amp_dtype=torch.bfloat16 if amp else None, graph=True, bf16_weights=amp)
+    b = bench.synthetic_batch(2, 64, 192, dev, seed=0, channels_last=True)
+    orig_fb, hits, n = tr._forward_backward, [], [0]
+
+    def fb(batch, progress):
+        n[0] += 1
+        if collect and torch.cuda.is_current_stream_capturing():
+            pass
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            out = orig_fb(batch, progress)
+        if any("AccumulateGrad" in str(x.message) for x in w):
+            hits.append((n[0], torch.cuda.is_current_stream_capturing()))
+        return out
+
+    tr._forward_backward = fb
+    if collect:
+        orig_restore = tr._restore
+
+        def restore(snap):
+            orig_restore(snap)
+            gc.collect()
+        tr._restore = restore
+    tr.train_step(b)
+    tr.train_step(b)
+    torch.cuda.synchronize()
+    print(f"[diag] {tag}: warnings at forward_backward calls (call, capturing) {hits}", flush=True)
 
 
-def fb(batch, progress):
-    phase["i"] += 1
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        out = orig_fb(batch, progress)
-    for x in w:
-        if "AccumulateGrad" in str(x.message):
-            print(f"[diag] warning in forward_backward call {phase['i']} "
-                  f"(capturing={torch.cuda.is_current_stream_capturing()})", flush=True)
-    return out
-
-
-tr._forward_backward = fb
-tr.train_step(b)
-tr.train_step(b)
-torch.cuda.synchronize()
-print("[diag] done", phase["i"], "forward_backward calls", flush=True)
+run("default")
+run("pose net on the current stream", overlap=False)
+run("gc.collect() after the warm-up", collect=True)
+run("fp32 nets, torch Adam", amp=False)

@@ -16,6 +16,8 @@ import __graft_entry__  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", action="append", default=[])
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--net", default="packnet", choices=["packnet", "packnet-san"],
+                help="packnet: PackNet01 (d=8, n1=64); packnet-san: PackNetSAN01 (d=4, n1=32)")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -23,8 +25,14 @@ from packnet_sfm_amd.networks.layers.packnet import pack3d as P  # noqa: E402
 
 dev = torch.device("cuda:0")
 B = 6
-PACK = [(64, 192, 640), (64, 96, 320), (128, 48, 160), (256, 24, 80), (512, 12, 40)]
-UNPACK = [(256, 6, 20), (128, 12, 40), (64, 24, 80), (32, 48, 160), (32, 96, 320)]  # conv2d outputs
+if args.net == "packnet":
+    D = 8
+    PACK = [(64, 192, 640), (64, 96, 320), (128, 48, 160), (256, 24, 80), (512, 12, 40)]
+    UNPACK = [(256, 6, 20), (128, 12, 40), (64, 24, 80), (32, 48, 160), (32, 96, 320)]  # conv2d outputs
+else:
+    D = 4
+    PACK = [(32, 192, 640), (64, 96, 320), (128, 48, 160), (256, 24, 80), (512, 12, 40)]
+    UNPACK = [(512, 6, 20), (256, 12, 40), (128, 24, 80), (64, 48, 160), (32, 96, 320)]
 cases = [(0, c) for c in PACK] + [(1, c) for c in UNPACK]
 
 
@@ -55,16 +63,16 @@ for lib in (args.lib or [None]):
     res, tot = {}, [0.0, 0.0, 0.0]
     for mode, (C, H, W) in cases:
         x = torch.randn(B, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        w = torch.randn(8, 1, 3, 3, 3, device=dev) * 0.2
-        b = torch.randn(8, device=dev) * 0.1
-        y = torch.empty(P._out_shape(mode, x, 2), device=dev, dtype=x.dtype, memory_format=torch.channels_last)
+        w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+        b = torch.randn(D, device=dev) * 0.1
+        y = torch.empty(P._out_shape(mode, x, 2, D), device=dev, dtype=x.dtype, memory_format=torch.channels_last)
         gy = torch.randn(y.shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         gx = torch.empty_like(x)
-        gw = torch.empty(8, 27, device=dev)
-        gb = torch.empty(8, device=dev)
-        d = P._desc(mode, x, y, 2)
+        gw = torch.empty(D, 27, device=dev)
+        gb = torch.empty(D, device=dev)
+        d = P._desc(mode, x, y, 2, D)
         ws = torch.empty(max(_hip.lib().psfm_p3d_ws_floats(ctypes.byref(d)), 1), device=dev)
-        wf = w.reshape(8, 27).contiguous()
+        wf = w.reshape(D, 27).contiguous()
         L, st = _hip.lib(), lambda: _hip.stream(dev)
         t_f = timed(lambda: L.psfm_p3d_fwd(ctypes.byref(d), _hip.ptr(x), _hip.ptr(wf), _hip.ptr(b), _hip.ptr(y), st()), args.iters)
         t_x = timed(lambda: L.psfm_p3d_bwd(ctypes.byref(d), _hip.ptr(x), _hip.ptr(wf), _hip.ptr(gy), _hip.ptr(gx), None, None, None,
