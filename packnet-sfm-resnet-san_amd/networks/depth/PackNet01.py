@@ -4,6 +4,7 @@ decoder with inverse-depth heads at 4 scales.  Versions '1A' (skip concatenation
 import torch
 import torch.nn as nn
 
+from ...utils.image import UpsampleNearest
 from ..layers.packnet.layers01 import (Conv2D, InvDepth, PackLayerConv3d, ResidualBlock,
                                        UnpackLayerConv3d)
 
@@ -48,9 +49,9 @@ class PackNet01(nn.Module):
         self.iconv2 = Conv2D(ins[2], n2, iconv_k[3], 1)
         self.iconv1 = Conv2D(ins[1], n1, iconv_k[4], 1)
         self.unpack_disps = nn.PixelShuffle(2)
-        self.unpack_disp4 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
-        self.unpack_disp3 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
-        self.unpack_disp2 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
+        self.unpack_disp4 = UpsampleNearest(2)
+        self.unpack_disp3 = UpsampleNearest(2)
+        self.unpack_disp2 = UpsampleNearest(2)
         self.disp4_layer = InvDepth(n4, out_channels=no)
         self.disp3_layer = InvDepth(n3, out_channels=no)
         self.disp2_layer = InvDepth(n2, out_channels=no)

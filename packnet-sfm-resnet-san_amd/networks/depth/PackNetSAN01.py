@@ -16,6 +16,7 @@ convolutions run on the fused HIP kernels (layers01.PackLayerConv3d / UnpackLaye
 import torch
 import torch.nn as nn
 
+from ...utils.image import UpsampleNearest
 from ..layers.packnet.layers01 import (Conv2D, InvDepth, PackLayerConv3d, ResidualBlock,
                                        UnpackLayerConv3d)
 
@@ -68,9 +69,9 @@ class Decoder(nn.Module):
         self.iconv2 = Conv2D(n2i, n2, iconv_kernel[3], 1)
         self.iconv1 = Conv2D(n1i, n1, iconv_kernel[4], 1)
         self.unpack_disps = nn.PixelShuffle(2)
-        self.unpack_disp4 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
-        self.unpack_disp3 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
-        self.unpack_disp2 = nn.Upsample(scale_factor=2, mode="nearest", align_corners=None)
+        self.unpack_disp4 = UpsampleNearest(2)
+        self.unpack_disp3 = UpsampleNearest(2)
+        self.unpack_disp2 = UpsampleNearest(2)
         self.disp4_layer = InvDepth(n4, out_channels=out_channels)
         self.disp3_layer = InvDepth(n3, out_channels=out_channels)
         self.disp2_layer = InvDepth(n2, out_channels=out_channels)

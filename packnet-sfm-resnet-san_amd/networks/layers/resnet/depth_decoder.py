@@ -43,5 +43,6 @@ class DepthDecoder(nn.Module):
                 head = self.convs[("dispconv", i)]  # Conv3x3 + sigmoid, fused epilogue (fp32 maps)
                 xin = head.pad(x) if head.pad is not None else x
                 out[("disp", i)] = bias_act(conv_nobias(head.conv, xin), head.conv.bias, ACT_SIGMOID, head)
-        self.outputs = out
+        # not kept on the module (the reference stores self.outputs): a reference held between steps
+        # keeps the previous step's autograd graph alive, and with it its AccumulateGrad nodes
         return out

@@ -4,6 +4,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..fused import ACT_RELU, bias_act, conv_nobias
+from ....utils.image import upsample_nearest
 
 
 def disp_to_depth(disp, min_depth, max_depth):
@@ -36,4 +37,5 @@ class ConvBlock(nn.Module):
 
 
 def upsample(x):
-    return F.interpolate(x, scale_factor=2, mode="nearest")
+    """F.interpolate(x, scale_factor=2, mode='nearest') with a deterministic backward."""
+    return upsample_nearest(x, 2)

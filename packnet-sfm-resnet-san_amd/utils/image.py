@@ -31,9 +31,53 @@ def interpolate_image(image, shape, mode="bilinear", align_corners=True):
     return funct.interpolate(image, size=shape, mode=mode, align_corners=align_corners)
 
 
+class _UpsampleNearest(torch.autograd.Function):
+    """Nearest upsampling by an integer factor f — the same values as F.interpolate(mode='nearest')
+    for an exact multiple — with a deterministic backward: each f x f block of the gradient is
+    summed by a reshape + sum reduction (fp32 accumulation, fixed order).  ATen's
+    upsample_nearest2d_backward accumulates with atomics; in bf16 every add rounds, which made the
+    bf16 training step's gradients differ by ~5 % between identical runs (tools/diag_cycles.py)."""
+
+    @staticmethod
+    def forward(ctx, x, f):
+        ctx.f = f
+        return funct.interpolate(x, scale_factor=f, mode="nearest")
+
+    @staticmethod
+    def backward(ctx, g):
+        f = ctx.f
+        B, C, H, W = g.shape
+        return g.reshape(B, C, H // f, f, W // f, f).sum((3, 5)), None
+
+
+def upsample_nearest(x, factor=2):
+    """x [B,C,H,W] -> [B,C,fH,fW] nearest, deterministic backward (see _UpsampleNearest)."""
+    return x if factor == 1 else _UpsampleNearest.apply(x, int(factor))
+
+
+class UpsampleNearest(torch.nn.Module):
+    """nn.Upsample(scale_factor=f, mode='nearest') with the deterministic backward (no parameters:
+    state dicts unchanged)."""
+
+    def __init__(self, scale_factor=2):
+        super().__init__()
+        self.scale_factor = int(scale_factor)
+
+    def forward(self, x):
+        return upsample_nearest(x, self.scale_factor)
+
+
 def interpolate_scales(images, shape=None, mode="bilinear", align_corners=False):
     shape = tuple((images[0].shape if shape is None else shape)[-2:])
-    return [funct.interpolate(im, shape, mode=mode, align_corners=align_corners) for im in images]
+    out = []
+    for im in images:
+        h, w = im.shape[-2:]
+        f = shape[0] // h
+        if mode == "nearest" and f * h == shape[0] and f * w == shape[1]:
+            out.append(upsample_nearest(im, f))   # exact integer factor: deterministic backward
+        else:
+            out.append(funct.interpolate(im, shape, mode=mode, align_corners=align_corners))
+    return out
 
 
 def match_scales(image, targets, num_scales, mode="bilinear", align_corners=True):

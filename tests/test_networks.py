@@ -184,3 +184,26 @@ def test_selfsup_packnet_san_step_on_gpu_matches_reference():
     for name, ref in zip(z["grad_names"], z["grad_norms"]):
         got = float(params[str(name)].grad.double().norm())
         assert abs(got - ref) / ref < 2e-2, (name, got, ref)
+
+
+@pytest.mark.parametrize("f,cl", [(2, False), (2, True), (4, True), (8, False)])
+def test_upsample_nearest_equals_interpolate(f, cl):
+    """utils.image.upsample_nearest (deterministic block-sum backward) == F.interpolate nearest,
+    forward and backward, any memory format."""
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.utils.image import upsample_nearest, interpolate_scales
+    g = torch.Generator().manual_seed(f)
+    x = torch.randn(2, 3, 5, 7, generator=g, dtype=torch.float64)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    a, b = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya = upsample_nearest(a, f)
+    yb = torch.nn.functional.interpolate(b, scale_factor=f, mode="nearest")
+    assert torch.equal(ya, yb)
+    gy = torch.randn(ya.shape, generator=g, dtype=torch.float64)
+    ya.backward(gy)
+    yb.backward(gy)
+    torch.testing.assert_close(a.grad, b.grad, rtol=1e-12, atol=1e-12)
+    ups = interpolate_scales([x, x[..., :3, :4]], shape=(5 * f, 7 * f), mode="nearest")
+    assert torch.equal(ups[0], yb)    # exact multiple -> the deterministic op
+    assert ups[1].shape[-2:] == (5 * f, 7 * f)   # not a multiple -> F.interpolate
