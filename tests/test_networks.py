@@ -204,6 +204,6 @@ def test_upsample_nearest_equals_interpolate(f, cl):
     ya.backward(gy)
     yb.backward(gy)
     torch.testing.assert_close(a.grad, b.grad, rtol=1e-12, atol=1e-12)
-    ups = interpolate_scales([x, x[..., :3, :4]], shape=(5 * f, 7 * f), mode="nearest")
+    ups = interpolate_scales([x, x[..., :3, :4]], shape=(5 * f, 7 * f), mode="nearest", align_corners=None)
     assert torch.equal(ups[0], yb)    # exact multiple -> the deterministic op
     assert ups[1].shape[-2:] == (5 * f, 7 * f)   # not a multiple -> F.interpolate
