@@ -25,6 +25,7 @@ not on the hot path: the non-finite check accumulates on the device, tested ever
 `check_every` steps.
 """
 import contextlib
+import gc
 
 import torch
 import torch.distributed as dist
@@ -218,6 +219,7 @@ class DDPTrainer:
         torch.cuda.synchronize(self.device)
         self._restore(snap)
         del snap
+        gc.collect()   # nothing of the warm-up's autograd graphs may survive into the capture
         self.nonfinite.zero_()
         torch.cuda.synchronize(self.device)
         # grads None before capture: autograd allocates them from the graph pool (static
