@@ -98,6 +98,9 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="torch.backends.cudnn.benchmark = False (MIOpen heuristics instead of find)")
+    ap.add_argument("--deterministic", default="cudnn", choices=["none", "cudnn", "all"],
+                    help="cudnn: torch.backends.cudnn.deterministic = True, as the reference trainer sets "
+                         "(horovod_trainer.py:23); all: torch.use_deterministic_algorithms(True)")
     ap.add_argument("--data-path", default="sampler", choices=["sampler", "resident", "gpu-augment"],
                     help="sampler: every step gathers the next batch of this rank's DistributedSampler "
                          "partition of a synthetic dataset resident in HBM; resident: one fixed batch; "
@@ -390,6 +393,9 @@ def main():
     fused.ENABLED = bool(args.fused_nets)
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
+    torch.backends.cudnn.deterministic = args.deterministic != "none"
+    if args.deterministic == "all":
+        torch.use_deterministic_algorithms(True, warn_only=True)
     model = build_model(args, device)
     if not args.nchw:
         to_channels_last(model)
@@ -475,6 +481,7 @@ def main():
                           "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
+                          "deterministic": args.deterministic,
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
                           "net_epilogues": "fused HIP (psfm_netops)" if args.fused_nets else "reference op chain",

@@ -125,14 +125,49 @@ def fisheye_project_to_grid(X, cam, T):
     return torch.stack([2 * u / (W - 1) - 1.0, 2 * v / (H - 1) - 1.0], -1).view(B, H, W, 2)
 
 
-def synthesize(ref, depth, K_tgt, K_ref, T):
+def synthesize(ref, depth, K_tgt, K_ref, T, kink_flip_eps=0.0):
     """Inverse warp of `ref` into the target view.  geometry/camera_utils.py:27-59.  K_* are
-    pinhole [B,3,3] tensors or FisheyeCamera (VADAS) intrinsics dicts."""
+    pinhole [B,3,3] tensors or FisheyeCamera (VADAS) intrinsics dicts.
+
+    `kink_flip_eps` (test instrument, not the reference): sample with `bilinear_other_cell`, which
+    puts every coordinate within eps of an integer into the OTHER bilinear cell — the same value,
+    the other one-sided derivative: the second legitimate fp32 outcome at a kink."""
     if isinstance(K_tgt, dict):
         grid = fisheye_project_to_grid(fisheye_lift(depth, K_tgt), K_ref, T)
     else:
         grid = project_to_grid(lift(depth, K_tgt), K_ref, T)
+    if kink_flip_eps > 0.0:
+        return bilinear_other_cell(ref, grid, kink_flip_eps)
     return F.grid_sample(ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+
+
+def bilinear_other_cell(ref, grid, eps):
+    """grid_sample(bilinear, zeros, align_corners=True) written out, with the tap cell of every
+    coordinate within `eps` of an integer n moved to the other side of n (x0 = n - 1 when the
+    coordinate is >= n, x0 = n when below): continuous value, the other cell's slope."""
+    B, C, H, W = ref.shape
+    ix = (grid[..., 0] + 1) / 2 * (W - 1)
+    iy = (grid[..., 1] + 1) / 2 * (H - 1)
+
+    def cell(i):
+        f = torch.floor(i.detach())
+        r = torch.round(i.detach())
+        near = (i.detach() - r).abs() < eps
+        other = torch.where(i.detach() >= r, r - 1, r)
+        return torch.where(near, other, f)
+
+    x0, y0 = cell(ix), cell(iy)
+    wx, wy = ix - x0, iy - y0
+    flat = ref.reshape(B, C, H * W)
+    out = 0.0
+    for dy, wyk in ((0, 1 - wy), (1, wy)):
+        for dx, wxk in ((0, 1 - wx), (1, wx)):
+            xx, yy = x0 + dx, y0 + dy
+            ok = (xx >= 0) & (xx <= W - 1) & (yy >= 0) & (yy <= H - 1)
+            idx = (yy.clamp(0, H - 1) * W + xx.clamp(0, W - 1)).long().view(B, 1, -1).expand(B, C, -1)
+            v = flat.gather(2, idx).view(B, C, *ix.shape[1:]) * ok.unsqueeze(1).to(ref.dtype)
+            out = out + v * (wxk * wyk).unsqueeze(1)
+    return out
 
 
 # ---------------------------------------------------------------------------------------------------------------------
@@ -210,17 +245,19 @@ def num_scales(progressive_scaling, num, progress):
 def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_scales_=4,
                      ssim_loss_weight=0.85, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
                      photometric_reduce_op="min", clip_loss=0.0, automask_loss=True,
-                     min_depth=0.5, max_depth=80.0, progressive_scaling=0.0, progress=0.0, tie_flip=None):
+                     min_depth=0.5, max_depth=80.0, progressive_scaling=0.0, progress=0.0, tie_flip=None,
+                     kink_flip_eps=0.0):
     """MultiViewPhotometricLoss.forward restated.  losses/multiview_photometric_loss.py:331-410.
 
     sigs: list of [B,1,h,w] sigmoid maps (the fork feeds sigmoid outputs, :362-369);
     pose_mats: list of [B,4,4] target->context transforms.  Pinhole cameras.
     Returns (loss[1], photometric metric, smoothness, per-scale reduced maps).
 
-    `tie_flip` (test instrument, not the reference): per-scale boolean maps [B,1,h,w]; at those
-    pixels the min-reprojection selects the SECOND-smallest candidate instead of the smallest —
-    the other legitimate fp32 outcome at a near-tie (tests bound the gradient at
-    `sensitive_pixels` by "matches either selection").
+    Test instruments (not the reference), for bounding the gradient at `sensitive_pixels`:
+    `tie_flip`: per-scale boolean maps [B,1,h,w]; at those pixels the min-reprojection selects the
+    SECOND-smallest candidate — the other legitimate fp32 outcome at a near-tie;
+    `kink_flip_eps`: every warp coordinate within eps of an integer takes the other bilinear cell
+    (synthesize) — the other legitimate one-sided derivative at a kink.
 
     Note the reference's metric aliasing: `add_metric` stores `photometric_loss.detach()`
     (:296, loss_base.py:73-81) and `loss += smoothness` (:405) then adds IN PLACE into that
@@ -252,9 +289,10 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
             depth = 1.0 / inv[i].clamp(min=1e-6)          # utils/depth.py:103-120
             if isinstance(K, dict):
                 sh = inv[i].shape[-2] / float(H)
-                warped.append(synthesize(refs[i], depth, fisheye_scale(K, s, sh), fisheye_scale(ref_K, s, sh), T))
+                warped.append(synthesize(refs[i], depth, fisheye_scale(K, s, sh), fisheye_scale(ref_K, s, sh), T,
+                                         kink_flip_eps))
             else:
-                warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T))
+                warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T, kink_flip_eps))
         for i, p in enumerate(photo(warped, images)):
             cands[i].append(p)
         if automask_loss:

@@ -110,29 +110,56 @@ def grad_check(got, ref, sensitive=None, tol=1e-3):
     return n == 0, f"{n} pixels over {tol:g}*max (max err {d.max():.3e}, lim {lim:.3e})"
 
 
-def grad_check_bounded(got, ref, ref_alt, sensitive, tol=1e-3, cap=5e-2, max_frac=0.05):
+def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=5e-2, max_frac=0.05):
     """Per-pixel gradient parity with a BOUNDED exclusion set.
 
     Every pixel must be within tol*max|ref| of the oracle gradient `ref`, except pixels that
     oracle.sensitive_pixels flags (bilinear kinks / min near-ties: fp32-ambiguous).  A flagged
-    pixel passes when it is within tol*max of `ref` OR of `ref_alt` (the oracle with the other
-    selection at every near-tie, photometric_loss(tie_flip=...)), or — a kink, where the two
-    bilinear cells give different slopes, or interacting ties — within cap*max.  At most
-    `max_frac` of the pixels may be flagged.  Returns (ok, stats dict)."""
+    pixel passes when it is within tol*max of `ref` OR of one of `ref_alts` — the oracle with the
+    other legitimate fp32 outcome taken at every flagged place (oracle_alternatives: the other
+    min selection at near-ties, the other bilinear cell at kinks, both) — and otherwise must stay
+    within cap*max (interacting flips in one 3x3 window).  At most `max_frac` of the pixels may be
+    flagged.  Returns (ok, stats dict)."""
     got = np.asarray(got, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
-    alt = np.asarray(ref_alt, dtype=np.float64) if ref_alt is not None else ref
+    if ref_alts is None:
+        alts = []
+    elif isinstance(ref_alts, (list, tuple)):
+        alts = [np.asarray(a, dtype=np.float64) for a in ref_alts if a is not None]
+    else:
+        alts = [np.asarray(ref_alts, dtype=np.float64)]
     sens = np.zeros(got.shape, bool) if sensitive is None else np.asarray(sensitive, dtype=bool)
     scale = max(np.abs(ref).max(), 1e-20)
     lim, lim_cap = tol * scale, cap * scale
-    da, db = np.abs(got - ref), np.abs(got - alt)
+    da = np.abs(got - ref)
+    dmin = da.copy()
+    for a in alts:
+        dmin = np.minimum(dmin, np.abs(got - a))
     plain_bad = (da > lim) & ~sens
-    ok_a, ok_b = (da <= lim) & sens, (db <= lim) & sens & ~((da <= lim) & sens)
-    capped = sens & (da > lim) & (db > lim)
-    cap_bad = capped & (np.minimum(da, db) > lim_cap)
+    ok_ref = (da <= lim) & sens
+    ok_alt = (dmin <= lim) & sens & ~ok_ref
+    capped = sens & (dmin > lim)
+    cap_bad = capped & (dmin > lim_cap)
     stats = {"pixels": int(got.size), "excluded": int(sens.sum()), "excluded_frac": float(sens.mean()),
-             "match_ref": int(ok_a.sum()), "match_alt": int(ok_b.sum()), "capped": int(capped.sum()),
-             "max_capped_err_over_tol": float(np.minimum(da, db)[capped].max() / lim) if capped.any() else 0.0,
+             "match_ref": int(ok_ref.sum()), "match_alt": int(ok_alt.sum()), "capped": int(capped.sum()),
+             "max_capped_err_over_tol": float(dmin[capped].max() / lim) if capped.any() else 0.0,
              "bad": int(plain_bad.sum() + cap_bad.sum())}
     ok = stats["bad"] == 0 and stats["excluded_frac"] <= max_frac
     return ok, stats
+
+
+def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-5, **kw):
+    """dL/dsig of the oracle with the other fp32 outcome at every ambiguous place: (ties flipped),
+    (kinks on the other bilinear cell), (both).  `kw`: oracle.photometric_loss keyword arguments."""
+    import torch
+    from oracle import photometric_oracle as O
+    out = []
+    for tie, kink in ((True, False), (False, True), (True, True)):
+        if tie and (ties is None or not any(bool(t.any()) for t in ties)):
+            continue
+        s_a = [s.detach().clone().requires_grad_(True) for s in sigs]
+        loss = O.photometric_loss(image, contexts, s_a, K, K, mats, mask, tie_flip=ties if tie else None,
+                                  kink_flip_eps=coord_eps if kink else 0.0, **kw)[0]
+        loss.sum().backward()
+        out.append([x.grad.numpy() if x.grad is not None else np.zeros(tuple(x.shape), np.float32) for x in s_a])
+    return [list(a) for a in zip(*out)] if out else [[] for _ in sigs]

@@ -59,6 +59,7 @@ def spread(tag, **kw):
     amp = kw.pop("amp", True)
     m.overlap_pose_net = kw.pop("overlap", True)
     det = kw.pop("det", False)
+    torch.backends.cudnn.deterministic = kw.pop("cudnn_det", False)
     torch.use_deterministic_algorithms(det, warn_only=True)
     g1, g2 = step(m, amp), step(m, amp)
     rel = sorted(float((g1[k] - g2[k]).norm() / g2[k].norm().clamp_min(1e-30)) for k in g1)
@@ -66,6 +67,8 @@ def spread(tag, **kw):
 
 
 spread("bf16 default")
+spread("bf16 cudnn.deterministic", cudnn_det=True)
+spread("fp32 cudnn.deterministic", cudnn_det=True, amp=False)
 spread("bf16 pose net on the current stream", overlap=False)
 spread("bf16 deterministic algorithms", det=True)
 spread("bf16 deterministic + current stream", det=True, overlap=False)
