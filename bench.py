@@ -98,9 +98,11 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=20, help="timed photometric fwd+bwd launches")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="torch.backends.cudnn.benchmark = False (MIOpen heuristics instead of find)")
-    ap.add_argument("--deterministic", default="cudnn", choices=["none", "cudnn", "all"],
+    ap.add_argument("--deterministic", default="none", choices=["none", "cudnn", "all"],
                     help="cudnn: torch.backends.cudnn.deterministic = True, as the reference trainer sets "
-                         "(horovod_trainer.py:23); all: torch.use_deterministic_algorithms(True)")
+                         "(horovod_trainer.py:23); all: torch.use_deterministic_algorithms(True).  Both "
+                         "restrict MIOpen to its deterministic solvers: 4.4 -> 1011 ms/step on MI355X "
+                         "(profiles/r02_determinism.json), so the bench uses MIOpen's fast solvers")
     ap.add_argument("--data-path", default="sampler", choices=["sampler", "resident", "gpu-augment"],
                     help="sampler: every step gathers the next batch of this rank's DistributedSampler "
                          "partition of a synthetic dataset resident in HBM; resident: one fixed batch; "

@@ -364,7 +364,8 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="garg", use_gt_scale=True
 # test helpers: where is a fp32 implementation allowed to disagree with the reference's gradient?
 # ---------------------------------------------------------------------------------------------------------------------
 def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, automask=True,
-                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-5, margin_eps=5e-5, return_ties=False):
+                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-5, margin_eps=5e-5, l1_eps=2e-6,
+                     return_ties=False):
     """Per-scale boolean maps [B,1,h,w] of pixels whose gradient is discontinuous at fp32 precision:
 
     * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer — d(warp)/d(ix)
@@ -374,6 +375,9 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
       carries ~1e-5 absolute error from the E[x^2]-mu^2 cancellation, so two fp32 implementations
       can order candidates differently below that) — the
       selected candidate (and so the gradient of the 3x3 SSIM window around it) can flip.
+    * L1 sign near-ties: a warped value within `l1_eps` of the target in some channel — the
+      derivative of |est - tgt| flips sign there (the selected candidate's 3x3 SSIM window aside,
+      only that pixel's gradient moves).
     Computed in float64 from the same inputs.  Full-resolution scales only.  With `return_ties`
     also the (undilated) near-tie maps, the `tie_flip` argument of photometric_loss.
     """
@@ -396,7 +400,9 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
             iy = (g[..., 1] + 1) / 2 * (H - 1)
             kink = ((ix - ix.round()).abs() < coord_eps) | ((iy - iy.round()).abs() < coord_eps)
             bad |= kink.unsqueeze(1)
-            cands.append(photometric_map(synthesize(c, depth, Kd, Kd, T), img, ssim_w, C1, C2))
+            warped = synthesize(c, depth, Kd, Kd, T)
+            bad |= ((warped - img).abs() < l1_eps).any(1, keepdim=True)
+            cands.append(photometric_map(warped, img, ssim_w, C1, C2))
             if automask:
                 cands.append(photometric_map(c, img, ssim_w, C1, C2))
         tie = torch.zeros_like(s, dtype=torch.bool)

@@ -21,11 +21,57 @@ def _build(dev, seed=0):
     return bench.to_channels_last(bench.build_model(A, dev))
 
 
-def test_graph_replayed_step_equals_eager_step():
-    """One replay == one eager step on the same batch: same loss, same gradients (bf16 nets;
-    MIOpen's weight-gradient kernels may reduce in a different order between calls, so the
-    gradients are compared by relative norm), same number of optimizer steps, and no
-    AccumulateGrad stream-mismatch warning (the pose net runs on a forked stream)."""
+def _grads(model):
+    return [(n, p.grad.float().clone() if p.grad is not None else None) for n, p in model.named_parameters()]
+
+
+def test_graph_replayed_step_equals_eager_step_exactly():
+    """fp32 nets with deterministic MIOpen algorithms (the reference trainer's
+    cudnn.deterministic = True, horovod_trainer.py:23): one HIP-graph replay is the same step as
+    the eager one — loss, every gradient and the updated parameters bit for bit over 3 steps —
+    and capturing emits no AccumulateGrad stream-mismatch warning (the pose net runs on a forked
+    stream)."""
+    import __graft_entry__
+    __graft_entry__.build()
+    import bench
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    dev = torch.device("cuda:0")
+    old = torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic
+    torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = False, True
+    try:
+        mg, me = _build(dev), _build(dev)
+        tg = DDPTrainer(mg, make_optimizer(mg, 1e-4, 1e-4, capturable=True), dev, amp_dtype=None, graph=True)
+        te = DDPTrainer(me, make_optimizer(me, 1e-4, 1e-4, capturable=True), dev, amp_dtype=None, graph=False,
+                        flat=True)
+        batches = [bench.synthetic_batch(2, 64, 192, dev, seed=s, channels_last=True) for s in range(3)]
+        static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in batches[0].items()}
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            for i, b in enumerate(batches):
+                og = tg.train_step(static if i == 0 else b)
+                oe = te.train_step(b)
+                torch.cuda.synchronize()
+                assert torch.equal(og["loss"], oe["loss"]), (i, float(og["loss"]), float(oe["loss"]))
+                for (n, gg), (_, ge) in zip(_grads(mg), _grads(me)):
+                    assert (gg is None) == (ge is None), n
+                    if ge is not None:
+                        assert torch.equal(gg, ge), (i, n, float((gg - ge).abs().max()))
+        for (n, pg), pe in zip(mg.named_parameters(), me.parameters()):
+            assert torch.equal(pg, pe), n
+        msgs = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
+        assert not msgs, msgs[0]
+        # per-step outputs are this step's own values, not views of the graph's static output
+        assert og["loss"].data_ptr() != tg.static_output["loss"].data_ptr()
+    finally:
+        torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = old
+
+
+def test_graph_replayed_bf16_step_within_eager_noise():
+    """The production path (bf16 nets, fused Adam on fp32 masters, MIOpen's fast solvers, which
+    are not bitwise reproducible in bf16: two identical eager steps give gradients ~5 % apart,
+    tools/diag_cycles.py): the replayed step's loss equals the eager one's, and its gradients are
+    as close to the eager step's as two eager steps are to each other; one optimizer step per
+    train_step."""
     import __graft_entry__
     __graft_entry__.build()
     import bench
@@ -37,29 +83,30 @@ def test_graph_replayed_step_equals_eager_step():
                     amp_dtype=torch.bfloat16, graph=True, bf16_weights=True)
     te = DDPTrainer(me, make_optimizer(me, 1e-4, 1e-4), dev, amp_dtype=torch.bfloat16, graph=False, flat=True,
                     bf16_weights=True, fused_optim=True)
-    batches = [bench.synthetic_batch(2, 64, 192, dev, seed=s, channels_last=True) for s in range(3)]
-    static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in batches[0].items()}
-    with warnings.catch_warnings(record=True) as caught:
-        warnings.simplefilter("always")
-        for i, b in enumerate(batches):
-            og = tg.train_step(static if i == 0 else b)
-            oe = te.train_step(b)
-            torch.cuda.synchronize()
-            lg, le = float(og["loss"]), float(oe["loss"])
-            assert abs(lg - le) <= 1e-3 * abs(le), (i, lg, le)
-            for (n, pg), pe in zip(mg.named_parameters(), me.parameters()):
-                if pe.grad is None:
-                    assert pg.grad is None, n
-                    continue
-                d = (pg.grad.float() - pe.grad.float()).norm() / pe.grad.float().norm().clamp_min(1e-20)
-                assert float(d) < 2e-2, (i, n, float(d))
-    msgs = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
-    assert not msgs, msgs[0]
-    assert int(tg.fused.step_count) == int(te.fused.step_count) == 3
-    # per-step outputs are this step's own values, not views of the graph's static output
-    assert og["loss"].data_ptr() != tg.static_output["loss"].data_ptr()
-    dm = (tg.fused.master - te.fused.master).abs().mean()
-    assert float(dm) < 0.05 * 1e-4, float(dm)
+    b = bench.synthetic_batch(2, 64, 192, dev, seed=0, channels_last=True)
+    static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in b.items()}
+    og = tg.train_step(static)
+    g_graph = _grads(mg)
+    # two eager evaluations of the same first step (the second one without its optimizer update)
+    te._zero_grad()
+    oe1 = te._forward_backward(b, 0.0)
+    g_e1 = _grads(me)
+    te._zero_grad()
+    te._forward_backward(b, 0.0)
+    g_e2 = _grads(me)
+    torch.cuda.synchronize()
+    assert abs(float(og["loss"]) - float(oe1["loss"])) <= 1e-5 * abs(float(oe1["loss"]))
+
+    def med(a, b_):
+        r = sorted(float((x - y).norm() / y.norm().clamp_min(1e-30)) for (_, x), (_, y) in zip(a, b_)
+                   if x is not None and y is not None)
+        return r[len(r) // 2]
+    noise, d = med(g_e2, g_e1), med(g_graph, g_e1)
+    print(f"median relative gradient difference: graph vs eager {d:.3e}, eager vs eager {noise:.3e}")
+    assert d <= 2.0 * noise + 1e-3, (d, noise)
+    for _ in range(2):
+        tg.train_step(b)
+    assert int(tg.fused.step_count) == 3
 
 
 def test_world2_flat_allreduce_algebra_on_fused_adam():
