@@ -364,11 +364,12 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="garg", use_gt_scale=True
 # test helpers: where is a fp32 implementation allowed to disagree with the reference's gradient?
 # ---------------------------------------------------------------------------------------------------------------------
 def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, automask=True,
-                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-5, margin_eps=5e-5, l1_eps=2e-6,
+                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-4, margin_eps=5e-5, l1_eps=2e-6,
                      return_ties=False):
     """Per-scale boolean maps [B,1,h,w] of pixels whose gradient is discontinuous at fp32 precision:
 
-    * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer — d(warp)/d(ix)
+    * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer (1e-4: an fp32
+      pixel coordinate in [512, 1024) has a 6.1e-5 ulp) — d(warp)/d(ix)
       jumps there (grid_sample's derivative is piecewise constant in the tap cell), so two fp32
       implementations that round ix to opposite sides get different gradients at that pixel;
     * min-reprojection near-ties: best and second-best candidate within `margin_eps` (fp32 SSIM

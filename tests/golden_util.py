@@ -152,18 +152,24 @@ def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_fr
     return ok, stats
 
 
-def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-5, **kw):
-    """dL/dsig of the oracle with the other fp32 outcome at every ambiguous place: (ties flipped),
-    (kinks on the other bilinear cell), (both).  `kw`: oracle.photometric_loss keyword arguments."""
-    import torch
+def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, **kw):
+    """dL/dsig of the oracle evaluated in float64 — as is, and with the other fp32 outcome at every
+    ambiguous place: (ties flipped), (kinks on the other bilinear cell), (both).  The float64
+    evaluation is the precision reference where the fp32 oracle itself rounds badly (a pixel of
+    the B=4 192x640 case: fp32 oracle -4.6e-5, fp64 oracle and HIP -6.98e-6; tools/debug_badpix.py).
+    `kw`: oracle.photometric_loss keyword arguments."""
     from oracle import photometric_oracle as O
+    d = lambda t: t.double() if t is not None else None  # noqa: E731
+    img, ctx = d(image), [d(c) for c in contexts]
+    Kd = {k: v.double() for k, v in K.items()} if isinstance(K, dict) else d(K)
+    md, mk = [d(m) for m in mats], d(mask)
     out = []
-    for tie, kink in ((True, False), (False, True), (True, True)):
+    for tie, kink in ((False, False), (True, False), (False, True), (True, True)):
         if tie and (ties is None or not any(bool(t.any()) for t in ties)):
             continue
-        s_a = [s.detach().clone().requires_grad_(True) for s in sigs]
-        loss = O.photometric_loss(image, contexts, s_a, K, K, mats, mask, tie_flip=ties if tie else None,
+        s_a = [s.detach().double().requires_grad_(True) for s in sigs]
+        loss = O.photometric_loss(img, ctx, s_a, Kd, Kd, md, mk, tie_flip=ties if tie else None,
                                   kink_flip_eps=coord_eps if kink else 0.0, **kw)[0]
         loss.sum().backward()
-        out.append([x.grad.numpy() if x.grad is not None else np.zeros(tuple(x.shape), np.float32) for x in s_a])
-    return [list(a) for a in zip(*out)] if out else [[] for _ in sigs]
+        out.append([x.grad.numpy() if x.grad is not None else np.zeros(tuple(x.shape)) for x in s_a])
+    return [list(a) for a in zip(*out)]

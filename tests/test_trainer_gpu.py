@@ -45,17 +45,20 @@ def test_graph_replayed_step_equals_eager_step_exactly():
                         flat=True)
         batches = [bench.synthetic_batch(2, 64, 192, dev, seed=s, channels_last=True) for s in range(3)]
         static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in batches[0].items()}
-        with warnings.catch_warnings(record=True) as caught:
-            warnings.simplefilter("always")
-            for i, b in enumerate(batches):
+        caught = []
+        for i, b in enumerate(batches):
+            with warnings.catch_warnings(record=True) as w:   # the graph trainer's capture / replays
+                warnings.simplefilter("always")
                 og = tg.train_step(static if i == 0 else b)
-                oe = te.train_step(b)
-                torch.cuda.synchronize()
-                assert torch.equal(og["loss"], oe["loss"]), (i, float(og["loss"]), float(oe["loss"]))
-                for (n, gg), (_, ge) in zip(_grads(mg), _grads(me)):
-                    assert (gg is None) == (ge is None), n
-                    if ge is not None:
-                        assert torch.equal(gg, ge), (i, n, float((gg - ge).abs().max()))
+            caught += w
+            oe = te.train_step(b)
+            torch.cuda.synchronize()
+            assert torch.equal(og["loss"], oe["loss"]), (i, float(og["loss"]), float(oe["loss"]))
+            del oe
+            for (n, gg), (_, ge) in zip(_grads(mg), _grads(me)):
+                assert (gg is None) == (ge is None), n
+                if ge is not None:
+                    assert torch.equal(gg, ge), (i, n, float((gg - ge).abs().max()))
         for (n, pg), pe in zip(mg.named_parameters(), me.parameters()):
             assert torch.equal(pg, pe), n
         msgs = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
