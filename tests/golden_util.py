@@ -113,7 +113,8 @@ def grad_check(got, ref, sensitive=None, tol=1e-3):
 def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_frac=0.05, max_capped=2e-5):
     """Per-pixel gradient parity with a BOUNDED exclusion set.
 
-    Every pixel must be within tol*max|ref| of the oracle gradient `ref`, except pixels that
+    Every pixel must be within tol*max|ref| of the oracle gradient `ref` (or of ref_alts[0], the
+    oracle evaluated in float64, where the fp32 oracle itself rounds badly), except pixels that
     oracle.sensitive_pixels flags (bilinear kinks / min near-ties: fp32-ambiguous).  A flagged
     pixel passes when it is within tol*max of `ref` OR of one of `ref_alts` — the oracle with the
     other legitimate fp32 outcome taken at every flagged place (oracle_alternatives: the other
@@ -136,6 +137,8 @@ def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_fr
     dmin = da.copy()
     for a in alts:
         dmin = np.minimum(dmin, np.abs(got - a))
+    if alts:   # alts[0] is the same oracle in float64: a precision reference for unflagged pixels too
+        da = np.minimum(da, np.abs(got - alts[0]))
     plain_bad = (da > lim) & ~sens
     ok_ref = (da <= lim) & sens
     ok_alt = (dmin <= lim) & sens & ~ok_ref
@@ -152,24 +155,32 @@ def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_fr
     return ok, stats
 
 
-def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, **kw):
+def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, pose_vec=None, **kw):
     """dL/dsig of the oracle evaluated in float64 — as is, and with the other fp32 outcome at every
     ambiguous place: (ties flipped), (kinks on the other bilinear cell), (both).  The float64
     evaluation is the precision reference where the fp32 oracle itself rounds badly (a pixel of
     the B=4 192x640 case: fp32 oracle -4.6e-5, fp64 oracle and HIP -6.98e-6; tools/debug_badpix.py).
+    With `pose_vec` [B,N,6] the poses are built from it (float64) and the return value is
+    (dL/dsig alternatives, [dL/dpose_vec per alternative]).
     `kw`: oracle.photometric_loss keyword arguments."""
     from oracle import photometric_oracle as O
     d = lambda t: t.double() if t is not None else None  # noqa: E731
     img, ctx = d(image), [d(c) for c in contexts]
     Kd = {k: v.double() for k, v in K.items()} if isinstance(K, dict) else d(K)
     md, mk = [d(m) for m in mats], d(mask)
-    out = []
+    out, pose = [], []
     for tie, kink in ((False, False), (True, False), (False, True), (True, True)):
         if tie and (ties is None or not any(bool(t.any()) for t in ties)):
             continue
         s_a = [s.detach().double().requires_grad_(True) for s in sigs]
+        if pose_vec is not None:
+            v = pose_vec.detach().double().requires_grad_(True)
+            md = [O.pose_vec_to_mat(v[:, j]) for j in range(v.shape[1])]
         loss = O.photometric_loss(img, ctx, s_a, Kd, Kd, md, mk, tie_flip=ties if tie else None,
                                   kink_flip_eps=coord_eps if kink else 0.0, **kw)[0]
         loss.sum().backward()
         out.append([x.grad.numpy() if x.grad is not None else np.zeros(tuple(x.shape)) for x in s_a])
-    return [list(a) for a in zip(*out)]
+        if pose_vec is not None:
+            pose.append(v.grad.numpy())
+    alts = [list(a) for a in zip(*out)]
+    return (alts, pose) if pose_vec is not None else alts

@@ -304,7 +304,7 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
     ref = O.photometric_loss(image, ctx, s_c, K, K, [O.pose_vec_to_mat(v_c[:, j]) for j in range(2)], None)
     ref[0].sum().backward()
     sens, ties = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0, return_ties=True)
-    alt = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties)
+    alt, alt_pose = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties, pose_vec=vec)
     s_d = [s.to(dev).requires_grad_(True) for s in sigs]
     v_d = vec.to(dev).requires_grad_(True)
     fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
@@ -320,8 +320,9 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
         ok, st = gu.grad_check_bounded(s_d[i].grad.cpu(), s_c[i].grad, alt[i], sens[i], GRAD_TOL)
         print(f"B={B} {H}x{W} dL/dsig{i}: {st}")
         assert ok, f"dL/dsig{i}: {st}"
-    # ~10^6 warps per image: kinks and near-ties always exist at these sizes (5e-3 as the
-    # full-resolution golden test; ATen-GPU vs ATen-CPU differ by 2.8e-3, tools/debug_grads.py)
-    e = gu.rel_err(v_d.grad.cpu(), v_c.grad)
-    print(f"B={B} {H}x{W} dL/dpose rel err {e:.2e}")
-    assert e < 5e-3
+    # the pose gradient sums ~10^6 warps, among them kinks and near-ties: within 5e-3 (max-norm
+    # relative) of the fp32 oracle or of one of its float64 evaluations (as is / ties flipped /
+    # kinks flipped / both); ATen-GPU vs ATen-CPU differ by 2.8e-3 (tools/debug_grads.py)
+    errs = [gu.rel_err(v_d.grad.cpu(), v_c.grad)] + [gu.rel_err(v_d.grad.cpu(), a) for a in alt_pose]
+    print(f"B={B} {H}x{W} dL/dpose rel err vs fp32 oracle / fp64 alternatives {[f'{e:.2e}' for e in errs]}")
+    assert min(errs) < 5e-3
