@@ -125,17 +125,22 @@ def fisheye_project_to_grid(X, cam, T):
     return torch.stack([2 * u / (W - 1) - 1.0, 2 * v / (H - 1) - 1.0], -1).view(B, H, W, 2)
 
 
-def synthesize(ref, depth, K_tgt, K_ref, T, kink_flip_eps=0.0):
+def synthesize(ref, depth, K_tgt, K_ref, T, kink_flip_eps=0.0, grid_mask=None):
     """Inverse warp of `ref` into the target view.  geometry/camera_utils.py:27-59.  K_* are
     pinhole [B,3,3] tensors or FisheyeCamera (VADAS) intrinsics dicts.
 
     `kink_flip_eps` (test instrument, not the reference): sample with `bilinear_other_cell`, which
     puts every coordinate within eps of an integer into the OTHER bilinear cell — the same value,
-    the other one-sided derivative: the second legitimate fp32 outcome at a kink."""
+    the other one-sided derivative: the second legitimate fp32 outcome at a kink.
+    `grid_mask` (test instrument): [B,1,H,W] bool; those pixels' warp coordinates pass no gradient
+    (their contribution to dL/dpose and dL/ddepth is dropped)."""
     if isinstance(K_tgt, dict):
         grid = fisheye_project_to_grid(fisheye_lift(depth, K_tgt), K_ref, T)
     else:
         grid = project_to_grid(lift(depth, K_tgt), K_ref, T)
+    if grid_mask is not None:
+        keep = (~grid_mask[:, 0]).unsqueeze(-1).to(grid.dtype)
+        grid = grid * keep + (grid * (1 - keep)).detach()
     if kink_flip_eps > 0.0:
         return bilinear_other_cell(ref, grid, kink_flip_eps)
     return F.grid_sample(ref, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
@@ -246,7 +251,7 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
                      ssim_loss_weight=0.85, smooth_loss_weight=0.001, C1=1e-4, C2=9e-4,
                      photometric_reduce_op="min", clip_loss=0.0, automask_loss=True,
                      min_depth=0.5, max_depth=80.0, progressive_scaling=0.0, progress=0.0, tie_flip=None,
-                     kink_flip_eps=0.0):
+                     kink_flip_eps=0.0, grid_mask=None):
     """MultiViewPhotometricLoss.forward restated.  losses/multiview_photometric_loss.py:331-410.
 
     sigs: list of [B,1,h,w] sigmoid maps (the fork feeds sigmoid outputs, :362-369);
@@ -257,7 +262,8 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
     `tie_flip`: per-scale boolean maps [B,1,h,w]; at those pixels the min-reprojection selects the
     SECOND-smallest candidate — the other legitimate fp32 outcome at a near-tie;
     `kink_flip_eps`: every warp coordinate within eps of an integer takes the other bilinear cell
-    (synthesize) — the other legitimate one-sided derivative at a kink.
+    (synthesize) — the other legitimate one-sided derivative at a kink;
+    `grid_mask`: per-scale [B,1,h,w] bool, pixels whose warp passes no gradient (synthesize).
 
     Note the reference's metric aliasing: `add_metric` stores `photometric_loss.detach()`
     (:296, loss_base.py:73-81) and `loss += smoothness` (:405) then adds IN PLACE into that
@@ -290,9 +296,10 @@ def photometric_loss(image, contexts, sigs, K, ref_K, pose_mats, mask=None, num_
             if isinstance(K, dict):
                 sh = inv[i].shape[-2] / float(H)
                 warped.append(synthesize(refs[i], depth, fisheye_scale(K, s, sh), fisheye_scale(ref_K, s, sh), T,
-                                         kink_flip_eps))
+                                         kink_flip_eps, None if grid_mask is None else grid_mask[i]))
             else:
-                warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T, kink_flip_eps))
+                warped.append(synthesize(refs[i], depth, scale_K(K, s), scale_K(ref_K, s), T, kink_flip_eps,
+                                         None if grid_mask is None else grid_mask[i]))
         for i, p in enumerate(photo(warped, images)):
             cands[i].append(p)
         if automask_loss:
@@ -364,7 +371,7 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="garg", use_gt_scale=True
 # test helpers: where is a fp32 implementation allowed to disagree with the reference's gradient?
 # ---------------------------------------------------------------------------------------------------------------------
 def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, automask=True,
-                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-4, margin_eps=5e-5, l1_eps=2e-6,
+                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-4, margin_eps=5e-5, l1_eps=1e-5,
                      return_ties=False):
     """Per-scale boolean maps [B,1,h,w] of pixels whose gradient is discontinuous at fp32 precision:
 
@@ -376,7 +383,8 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
       carries ~1e-5 absolute error from the E[x^2]-mu^2 cancellation, so two fp32 implementations
       can order candidates differently below that) — the
       selected candidate (and so the gradient of the 3x3 SSIM window around it) can flip.
-    * L1 sign near-ties: a warped value within `l1_eps` of the target in some channel — the
+    * L1 sign near-ties: a warped value within `l1_eps` of the target in some channel (1e-5: a
+      1e-4 px coordinate difference on a steep texture moves the warped value that much) — the
       derivative of |est - tgt| flips sign there (the selected candidate's 3x3 SSIM window aside,
       only that pixel's gradient moves).
     Computed in float64 from the same inputs.  Full-resolution scales only.  With `return_ties`

@@ -155,13 +155,16 @@ def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_fr
     return ok, stats
 
 
-def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, pose_vec=None, **kw):
+def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, pose_vec=None,
+                        sensitive=None, **kw):
     """dL/dsig of the oracle evaluated in float64 — as is, and with the other fp32 outcome at every
     ambiguous place: (ties flipped), (kinks on the other bilinear cell), (both).  The float64
     evaluation is the precision reference where the fp32 oracle itself rounds badly (a pixel of
     the B=4 192x640 case: fp32 oracle -4.6e-5, fp64 oracle and HIP -6.98e-6; tools/debug_badpix.py).
     With `pose_vec` [B,N,6] the poses are built from it (float64) and the return value is
-    (dL/dsig alternatives, [dL/dpose_vec per alternative]).
+    (dL/dsig alternatives, [dL/dpose_vec per alternative], pose bound): the pose bound is
+    |dL/dpose - dL/dpose with the `sensitive` pixels' warp gradients dropped| in float64 — how much
+    the flagged pixels contribute to the pose gradient.
     `kw`: oracle.photometric_loss keyword arguments."""
     from oracle import photometric_oracle as O
     d = lambda t: t.double() if t is not None else None  # noqa: E731
@@ -183,4 +186,13 @@ def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e
         if pose_vec is not None:
             pose.append(v.grad.numpy())
     alts = [list(a) for a in zip(*out)]
-    return (alts, pose) if pose_vec is not None else alts
+    if pose_vec is None:
+        return alts
+    bound = None
+    if sensitive is not None:
+        v = pose_vec.detach().double().requires_grad_(True)
+        md = [O.pose_vec_to_mat(v[:, j]) for j in range(v.shape[1])]
+        s_a = [s.detach().double() for s in sigs]
+        O.photometric_loss(img, ctx, s_a, Kd, Kd, md, mk, grid_mask=sensitive, **kw)[0].sum().backward()
+        bound = np.abs(pose[0] - v.grad.numpy())
+    return alts, pose, bound

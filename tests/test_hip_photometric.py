@@ -304,7 +304,8 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
     ref = O.photometric_loss(image, ctx, s_c, K, K, [O.pose_vec_to_mat(v_c[:, j]) for j in range(2)], None)
     ref[0].sum().backward()
     sens, ties = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0, return_ties=True)
-    alt, alt_pose = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties, pose_vec=vec)
+    alt, alt_pose, pose_bound = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties, pose_vec=vec,
+                                                       sensitive=sens)
     s_d = [s.to(dev).requires_grad_(True) for s in sigs]
     v_d = vec.to(dev).requires_grad_(True)
     fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
@@ -320,9 +321,12 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
         ok, st = gu.grad_check_bounded(s_d[i].grad.cpu(), s_c[i].grad, alt[i], sens[i], GRAD_TOL)
         print(f"B={B} {H}x{W} dL/dsig{i}: {st}")
         assert ok, f"dL/dsig{i}: {st}"
-    # the pose gradient sums ~10^6 warps, among them kinks and near-ties: within 5e-3 (max-norm
-    # relative) of the fp32 oracle or of one of its float64 evaluations (as is / ties flipped /
-    # kinks flipped / both); ATen-GPU vs ATen-CPU differ by 2.8e-3 (tools/debug_grads.py)
-    errs = [gu.rel_err(v_d.grad.cpu(), v_c.grad)] + [gu.rel_err(v_d.grad.cpu(), a) for a in alt_pose]
-    print(f"B={B} {H}x{W} dL/dpose rel err vs fp32 oracle / fp64 alternatives {[f'{e:.2e}' for e in errs]}")
-    assert min(errs) < 5e-3
+    # the pose gradient sums ~10^6 warps, among them the flagged pixels: every entry within
+    # 1e-3 * max|g| + 2 x the flagged pixels' own contribution to that entry (float64 oracle with
+    # their warp gradients dropped, golden_util.oracle_alternatives) of the float64 oracle
+    got_v, ref_v = v_d.grad.cpu().double().numpy(), alt_pose[0]
+    slack = 1e-3 * np.abs(ref_v).max() + 2.0 * pose_bound
+    ratio = float((np.abs(got_v - ref_v) / slack).max())
+    print(f"B={B} {H}x{W} dL/dpose: rel err vs fp64 oracle {gu.rel_err(got_v, ref_v):.2e}, flagged-pixel share "
+          f"{float((pose_bound / np.abs(ref_v).max()).max()):.2e} of max, worst |err| / allowance {ratio:.2f}")
+    assert ratio <= 1.0
