@@ -19,6 +19,9 @@ from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometr
 torch.set_num_threads(16)
 dev = torch.device("cuda:0")
 B, H, W = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (4, 192, 640)
+if len(sys.argv) > 4 and sys.argv[4] == "k1k2":   # the unfused K1 forward / K2 + K3 backward
+    from packnet_sfm_amd.losses import _hip_photometric as HP
+    HP.FUSED_GRAD = False
 g = torch.Generator().manual_seed(4000 + B * 7 + H)
 image = gu.smooth_texture(g, B, 3, H, W)
 ctx = [gu.smooth_texture(g, B, 3, H, W) for _ in range(2)]
