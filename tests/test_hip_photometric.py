@@ -125,13 +125,15 @@ def _seeded_inputs(seed, B, H, W, nctx=2):
     return image, ctx, gu.kitti_K(B, H, W), gu.pose_vecs(g, B, nctx), [gu.sigmoid_maps(g, B, H, W) for _ in range(4)]
 
 
-@pytest.mark.parametrize("B,H,W", [(1, 24, 80), (1, 13, 70), (2, 12, 64), (1, 16, 130), (1, 10, 200)])
+# shapes small enough that a seed with no flagged pixel exists (1e-4 px kink band, 5e-5 min / L1
+# near-ties over 4 scales x 2 contexts): partial band (H < RB), one / two / three stripes
+@pytest.mark.parametrize("B,H,W", [(1, 8, 40), (1, 6, 70), (1, 5, 130)])
 def test_kink_free_inputs_match_oracle_tightly(dev, B, H, W):
     """Seeded inputs with NO kink / near-tie pixel: every gradient entry within 1e-3 of the oracle."""
     from oracle import photometric_oracle as O
     from packnet_sfm_amd.geometry.pose import Pose
     from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
-    for seed in range(100, 400):
+    for seed in range(100, 1100):
         image, ctx, K, vec, sigs = _seeded_inputs(seed, B, H, W)
         mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
         sens = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0)

@@ -7,7 +7,10 @@ import sys
 trace, out = sys.argv[1], sys.argv[2]
 rows = list(csv.DictReader(open(trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-key = "k12_fwd_grad" if any("k12_fwd_grad" in r["Kernel_Name"] for r in rows) else "k1_forward"
+# steps are delimited by the fused Adam launch (once per training step; bench.py's photometric
+# kernel timing replays after the timed steps launch K12 but never Adam)
+names = {r["Kernel_Name"] for r in rows}
+key = next(k for k in ("k_adam", "k12_fwd_grad", "k1_forward") if any(k in n for n in names))
 k1 = [i for i, r in enumerate(rows) if key in r["Kernel_Name"]]
 lines = [f"rows {len(rows)}  k1 launches {len(k1)}"]
 if len(k1) >= 3:
