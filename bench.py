@@ -42,7 +42,7 @@ N_CTX, N_SCALES = 2, 4
 # BASELINE.json configs -> bench presets (reference YAML in parentheses)
 CONFIGS = {
     "overfit": dict(depth_net="DepthResNet", pose_net="PoseResNet", batch=6, height=192, width=640, cameras=1,
-                    amp="fp32", min_depth=0.5, max_depth=80.0,
+                    amp="fp32", min_depth=0.0, max_depth=80.0,
                     yaml="configs/overfit_kitti.yaml (DepthResNet 18pt + PoseResNet 18pt, fp32)"),
     "kitti-resnet-san": dict(depth_net="ResNetSAN01", pose_net="PoseNet", batch=4, height=192, width=640,
                              cameras=1, amp="bf16", min_depth=0.5, max_depth=80.0,
@@ -108,8 +108,12 @@ def parse(argv=None):
                          "partition of a synthetic dataset resident in HBM; resident: one fixed batch; "
                          "gpu-augment: the reference's train_transforms on the GPU from raw 375x1242 uint8 "
                          "frames inside every timed step")
-    ap.add_argument("--fused-nets", action="store_true",
-                    help="run the nets' BN/GN/bias+activation epilogues as fused HIP kernels (psfm_netops)")
+    ap.add_argument("--fused-nets", default="bias,gn",
+                    help="net epilogues as fused HIP kernels (psfm_netops): none | all | a comma list of "
+                         "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU), gn (GroupNorm + ReLU); "
+                         "default: the measured winners (networks/layers/fused.py FUSE)")
+    ap.add_argument("--no-upcat", action="store_true",
+                    help="DepthDecoder upsample + cat as the torch op chain instead of psfm_upcat")
     args = ap.parse_args(argv)
     preset = CONFIGS[args.config]
     for k in ("batch", "cameras", "height", "width", "depth_net", "pose_net", "amp"):
@@ -392,7 +396,9 @@ def main():
     from packnet_sfm_amd.datasets.synthetic import ResidentLoader, SyntheticSfmDataset, get_datasampler
 
     from packnet_sfm_amd.networks.layers import fused
-    fused.ENABLED = bool(args.fused_nets)
+    kinds = {"none": set(), "all": {"bias", "bn", "gn"}}.get(args.fused_nets, set(args.fused_nets.split(",")))
+    fused.FUSE.update(bias="bias" in kinds, bn="bn" in kinds, gn="gn" in kinds)
+    fused.UPCAT = not args.no_upcat
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     torch.backends.cudnn.deterministic = args.deterministic != "none"
@@ -486,7 +492,9 @@ def main():
                           "deterministic": args.deterministic,
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
-                          "net_epilogues": "fused HIP (psfm_netops)" if args.fused_nets else "reference op chain",
+                          "net_epilogues": (f"fused HIP (psfm_netops: {args.fused_nets}), the rest the reference "
+                                            f"op chain (MIOpen BN)" if args.fused_nets != "none" else "reference op chain"),
+                          "decoder_upcat": "torch op chain" if args.no_upcat else "HIP (psfm_upcat)",
                           "weights": "random init (no network / checkpoints)", "config_key": config_key(args)}}
         if ktimes:
             out["roofline"] = roofline(args, ktimes)

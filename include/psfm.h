@@ -61,6 +61,12 @@ typedef struct psfm_params {
                                psfm_photometric_fwd_grad (its partial sums use that kernel's
                                unit grid: psfm_finalize / psfm_photometric_grad_finish read it) */
     int cam_model;          /* psfm_cam_model; fisheye: K1 / K12 paths only, N <= 2          */
+    int sig_shift[PSFM_MAX_SCALES]; /* sigmoid map s is stored at (H >> k, W >> k), k = sig_shift[s]:
+                               the depth net's coarse output, nearest-upsampled to H x W on the
+                               fly (models/model_utils.py:152-196 upsample_output; 2^k x 2^k
+                               blocks, exact).  0 = stored at H x W.  k > 0: K12 training path
+                               (prepass / fwd_grad / grad_finish, grad_sig then at the coarse
+                               size) and the K1 forward / clip-stats path; H, W multiples of 2^k */
 } psfm_params;
 
 /* Device inputs of one call. `cam` holds one record per (scale, context, batch):

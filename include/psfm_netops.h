@@ -85,6 +85,18 @@ int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bi
 
 const char* psfm_netops_last_error(void);
 
+/* Decoder up-stage input: out = cat([nearest_up2(x), skip], channels)  (the reference's
+ * upsample(convs[("upconv", i, 0)](x)) then torch.cat with the encoder skip,
+ * packnet_sfm/networks/layers/resnet/depth_decoder.py:48-57, layers.py:60-64).
+ * x bf16 NHWC [N, h, w, C1]; skip bf16 NHWC [N, 2h, 2w, C2] or NULL with C2 = 0; out bf16 NHWC
+ * [N, 2h, 2w, C1 + C2].  C1 >= 8, C1 and C2 multiples of 8 (16-byte vectors). */
+int psfm_upcat_fwd(const void* x, const void* skip, int N, int h, int w, int C1, int C2, void* out, void* stream);
+
+/* Its backward: dx[n, y, x, c] = the sum of dout[n, 2y + i, 2x + j, c] over the 2x2 block (fp32,
+ * fixed order, one bf16 rounding: deterministic, unlike ATen's atomic upsample backward),
+ * dskip = dout[..., C1:] (NULL when C2 = 0). */
+int psfm_upcat_bwd(const void* dout, int N, int h, int w, int C1, int C2, void* dx, void* dskip, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

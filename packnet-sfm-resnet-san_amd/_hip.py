@@ -29,7 +29,8 @@ class Params(ctypes.Structure):
                 ("scale0", c_int), ("n_scales", c_int), ("automask", c_int), ("reduce_op", c_int),
                 ("l1_only", c_int), ("ssim_w", c_float), ("C1", c_float), ("C2", c_float),
                 ("min_depth", c_float), ("max_depth", c_float), ("clip_loss", c_float),
-                ("smooth_w", c_float), ("grad_fused", c_int), ("cam_model", c_int)]
+                ("smooth_w", c_float), ("grad_fused", c_int), ("cam_model", c_int),
+                ("sig_shift", c_int * MAX_SCALES)]
 
 
 class Inputs(ctypes.Structure):
@@ -115,6 +116,8 @@ def lib():
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V, V],
                             c_int),
         "psfm_netops_last_error": ([], ctypes.c_char_p),
+        "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
+        "psfm_upcat_bwd": ([V, c_int, c_int, c_int, c_int, c_int, V, V, V], c_int),
         # include/psfm_pack3d.h
         "psfm_p3d_fwd": ([V, V, V, V, V, V], c_int),
         "psfm_p3d_ws_floats": ([V], ctypes.c_int64),
@@ -144,6 +147,7 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
+            "psfm_upcat_fwd", "psfm_upcat_bwd",
             "psfm_depth_metrics", "psfm_metrics_last_error",
             "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
             "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error")
@@ -153,7 +157,7 @@ def check(rc, what):
     if rc != 0:
         if what.startswith(("psfm_optim", "psfm_grad", "psfm_adam")):
             err = lib().psfm_optim_last_error
-        elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops")):
+        elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops", "psfm_upcat")):
             err = lib().psfm_netops_last_error
         elif what.startswith("psfm_depth_metrics"):
             err = lib().psfm_metrics_last_error

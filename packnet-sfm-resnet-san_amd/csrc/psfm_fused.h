@@ -244,6 +244,7 @@ struct K12 {
     const psfm_params& p;
     Cfg<FAST> cfg;
     int H, W, B, b, s, unit, y0, col, colr, lane;
+    int sh, Ws, colc;  // sigmoid storage: (H >> sh, W >> sh), this lane's stored column
     uint32_t plane, pb;
     bool pcol, qcol, border;
     DepthChain dc;
@@ -303,7 +304,10 @@ struct K12 {
         cx = (float)(base / ((double)B * H * (W - 1)));
         cy = (float)(base / ((double)B * (H - 1) * W));
         tgt = a.in.tgt + (size_t)b * 3 * plane;
-        sig = pick4(a.in.sig, s) + (size_t)b * plane;
+        sh = pick4(p.sig_shift, s);
+        Ws = W >> sh;
+        colc = colr >> sh;
+        sig = pick4(a.in.sig, s) + (size_t)b * (plane >> (2 * sh));
 #pragma unroll
         for (int j = 0; j < NC; ++j) ctx[j] = pick4(a.in.ctx, j) + (size_t)b * 3 * plane;
         thr = (cfg.clip()) ? a.ws.clip_thr + (size_t)s * (cfg.automask() ? 2 * NC : NC) : nullptr;
@@ -364,7 +368,11 @@ struct K12 {
 #endif
     }
 
-    __device__ __forceinline__ float load_sig(int v) const { return sig[(uint32_t)(reflect1(v, H) * W + colr)]; }
+    // the sigmoid at full-resolution row v, this lane's column: nearest upsampling of the stored
+    // (H >> sh, W >> sh) map by 2^sh (upsample_output, model_utils.py:152-196)
+    __device__ __forceinline__ float load_sig(int v) const {
+        return sig[(uint32_t)((reflect1(v, H) >> sh) * Ws + colc)];
+    }
 
     template <int I, bool LOAD, bool PEVAL, bool QEVAL>
     __device__ __forceinline__ void step(State<NC>& S, int k) const {

@@ -964,9 +964,113 @@ inline Geo gn_geometry(int N, int HW, int C) {
     return g;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Decoder up-stage input: out = cat([nearest_up2(x), skip], channels), NHWC bf16, 16-byte
+// vectors (depth_decoder.py:48-57).  One launch each way instead of the upsample, cat and the
+// backward's strided copy + two-pass block-sum reduction.
+// ---------------------------------------------------------------------------------------------
+struct UpcatArgs {
+    const uint4* x;     // [N, h, w, C1/8]
+    const uint4* skip;  // [N, 2h, 2w, C2/8] or null
+    uint4* out;         // [N, 2h, 2w, (C1+C2)/8]
+    const uint4* dout;
+    uint4* dx;
+    uint4* dskip;
+    int N, h, w, V1, V2;  // V = channels / 8
+    uint32_t nfwd, ndx, ndskip;
+};
+
+__global__ __launch_bounds__(256) void k_upcat_fwd(UpcatArgs a) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= a.nfwd) return;
+    const uint32_t Vt = (uint32_t)(a.V1 + a.V2);
+    const uint32_t pix = i / Vt, v = i - pix * Vt;   // output pixel (n, Y, X), vector in the row
+    const uint32_t W2 = 2u * (uint32_t)a.w, H2 = 2u * (uint32_t)a.h;
+    const uint32_t X = pix % W2, nY = pix / W2, Y = nY % H2, n = nY / H2;
+    if (v < (uint32_t)a.V1)
+        a.out[i] = a.x[(((size_t)n * a.h + (Y >> 1)) * a.w + (X >> 1)) * a.V1 + v];
+    else
+        a.out[i] = a.skip[(size_t)pix * a.V2 + (v - a.V1)];
+}
+
+__device__ __forceinline__ void add8(float (&acc)[8], uint4 q) {
+    const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(u[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(u[k] & 0xffff0000u);
+    }
+}
+
+// threads [0, ndx): one 8-channel vector of dx (sum of its 2x2 block, rows then columns, fp32,
+// one bf16 rounding); threads [ndx, ndx + ndskip): one vector of dskip (copy)
+__global__ __launch_bounds__(256) void k_upcat_bwd(UpcatArgs a) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t Vt = (uint32_t)(a.V1 + a.V2);
+    if (i < a.ndx) {
+        const uint32_t pix = i / (uint32_t)a.V1, v = i - pix * (uint32_t)a.V1;  // input pixel (n, y, x)
+        const uint32_t x = pix % (uint32_t)a.w, ny = pix / (uint32_t)a.w;
+        const uint32_t y = ny % (uint32_t)a.h, n = ny / (uint32_t)a.h;
+        const uint32_t W2 = 2u * (uint32_t)a.w;
+        const size_t r0 = ((size_t)n * 2u * a.h + 2u * y) * W2 + 2u * x;  // top-left output pixel
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        add8(acc, a.dout[r0 * Vt + v]);
+        add8(acc, a.dout[(r0 + 1) * Vt + v]);
+        add8(acc, a.dout[(r0 + W2) * Vt + v]);
+        add8(acc, a.dout[(r0 + W2 + 1) * Vt + v]);
+        uint4 o;
+        o.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
+        o.y = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
+        o.z = (uint32_t)f2bf(acc[4]) | ((uint32_t)f2bf(acc[5]) << 16);
+        o.w = (uint32_t)f2bf(acc[6]) | ((uint32_t)f2bf(acc[7]) << 16);
+        a.dx[i] = o;
+        return;
+    }
+    const uint32_t j = i - a.ndx;
+    if (j >= a.ndskip) return;
+    const uint32_t pix = j / (uint32_t)a.V2, v = j - pix * (uint32_t)a.V2;
+    a.dskip[j] = a.dout[(size_t)pix * Vt + a.V1 + v];
+}
+
 }  // namespace
 
 extern "C" {
+
+static int upcat_check(int N, int h, int w, int C1, int C2, const char* who) {
+    if (N < 1 || h < 1 || w < 1 || C1 < 8 || C2 < 0 || (C1 % 8) || (C2 % 8)) return fail(-1, who);
+    if ((long long)N * 4 * h * w * (C1 + C2) / 8 >= (1LL << 32)) return fail(-1, who);
+    return 0;
+}
+
+int psfm_upcat_fwd(const void* x, const void* skip, int N, int h, int w, int C1, int C2, void* out, void* stream) {
+    if (int e = upcat_check(N, h, w, C1, C2, "upcat_fwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)")) return e;
+    if (!x || !out || (C2 > 0 && !skip)) return fail(-1, "upcat_fwd: null pointer");
+    UpcatArgs a{};
+    a.x = static_cast<const uint4*>(x);
+    a.skip = static_cast<const uint4*>(skip);
+    a.out = static_cast<uint4*>(out);
+    a.N = N, a.h = h, a.w = w, a.V1 = C1 / 8, a.V2 = C2 / 8;
+    a.nfwd = (uint32_t)((size_t)N * 4 * h * w * (a.V1 + a.V2));
+    hipLaunchKernelGGL(k_upcat_fwd, dim3((a.nfwd + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_upcat_bwd(const void* dout, int N, int h, int w, int C1, int C2, void* dx, void* dskip, void* stream) {
+    if (int e = upcat_check(N, h, w, C1, C2, "upcat_bwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)")) return e;
+    if (!dout || !dx || (C2 > 0 && !dskip)) return fail(-1, "upcat_bwd: null pointer");
+    UpcatArgs a{};
+    a.dout = static_cast<const uint4*>(dout);
+    a.dx = static_cast<uint4*>(dx);
+    a.dskip = static_cast<uint4*>(dskip);
+    a.N = N, a.h = h, a.w = w, a.V1 = C1 / 8, a.V2 = C2 / 8;
+    a.ndx = (uint32_t)((size_t)N * h * w * a.V1);
+    a.ndskip = (uint32_t)((size_t)N * 4 * h * w * a.V2);
+    const uint32_t n = a.ndx + a.ndskip;
+    hipLaunchKernelGGL(k_upcat_bwd, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
 
 size_t psfm_netops_ws_floats(int M, int C) {
     const Geo g = geometry(M, C, pick_vec(C));

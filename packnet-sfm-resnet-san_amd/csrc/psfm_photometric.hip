@@ -765,19 +765,32 @@ __global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
 // ---------------------------------------------------------------------------------------------
 struct SigSumArgs {
     const float* sig[MAXS];
+    int shift[MAXS];
     float* part;  // [S][B][SIGCH]
-    int B;
+    int B, W;
     uint32_t plane;
 };
 
+// fixed-order sums over the FULL-resolution plane (the upsampled map's mean, utils/depth.py:183),
+// a stored coarse map read through the nearest 2^shift mapping: the same values in the same
+// order as summing the materialised upsample
 __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
     __shared__ float red[NWAVE];
     const int ch = blockIdx.x, b = blockIdx.y, s = blockIdx.z;
+    const int sh = pick4(a.shift, s);
     const uint32_t per = (a.plane + fused::SIGCH - 1) / fused::SIGCH;
     const uint32_t lo = ch * per, hi = min(a.plane, lo + per);
-    const float* x = pick4(a.sig, s) + (size_t)b * a.plane;
+    const float* x = pick4(a.sig, s) + (size_t)b * (a.plane >> (2 * sh));
+    const uint32_t W = (uint32_t)a.W, Ws = W >> sh;
     float v[1] = {0.0f};
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) v[0] += x[i];
+    if (sh == 0) {
+        for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) v[0] += x[i];
+    } else {
+        for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) {
+            const uint32_t y = i / W, c = i - y * W;
+            v[0] += x[(y >> sh) * Ws + (c >> sh)];
+        }
+    }
     block_sum<1>(v, red);
     if (threadIdx.x == 0) a.part[((size_t)s * a.B + b) * fused::SIGCH + ch] = v[0];
 }
@@ -785,6 +798,7 @@ __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
 struct GradFinishArgs {
     const float* gin[MAXS];
     float* g[MAXS];
+    int shift[MAXS];
     const float* smooth_stats;  // [n][B][4] = Ax, Ay, m, max(m, 1e-6)   (finalize)
     const float* grad_out;
     int B, H, W, scale0, n_scales, has_smooth;
@@ -808,12 +822,32 @@ __global__ __launch_bounds__(NT) void k_grad_finish(GradFinishArgs a) {
     }
     const float go = *a.grad_out;
     const float* gi = pick4(a.gin, s) + (size_t)b * plane;
-    float* g = pick4(a.g, s) + (size_t)b * plane;
+    const int sh = pick4(a.shift, s);
+    const uint32_t cplane = plane >> (2 * sh);
+    float* g = pick4(a.g, s) + (size_t)b * cplane;
     const uint32_t i0 = blockIdx.x * (NT * 4) + threadIdx.x;
+    if (sh == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + u * NT;
+            if (i < plane) g[i] = go * (gi[i] + c);
+        }
+        return;
+    }
+    // stored coarse map: the adjoint of the nearest 2^sh upsampling sums each 2^sh x 2^sh block of
+    // the full-resolution gradient (row-major, fixed order: deterministic, no atomics)
+    const int f = 1 << sh;
+    const uint32_t Ws = (uint32_t)(a.W >> sh);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint32_t i = i0 + u * NT;
-        if (i < plane) g[i] = go * (gi[i] + c);
+        if (i >= cplane) break;
+        const uint32_t Y = i / Ws, X = i - Y * Ws;
+        const float* r = gi + ((size_t)Y * f) * a.W + (size_t)X * f;
+        float acc = 0.0f;
+        for (int dy = 0; dy < f; ++dy)
+            for (int dx = 0; dx < f; ++dx) acc += go * (r[(size_t)dy * a.W + dx] + c);
+        g[i] = acc;
     }
 }
 
@@ -885,6 +919,7 @@ __global__ __launch_bounds__(NT) void k_vs_bwd(VSArgs v) {
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
+int validate_shift(const psfm_params* p);
 int validate(const psfm_params* p, const psfm_inputs* in) {
     if (!p || !in) return fail(-1, "null params/inputs");
     if (p->B < 1 || p->H < 2 || p->W < 2) return fail(-2, "bad B/H/W (need B>=1, H>=2, W>=2)");
@@ -905,6 +940,24 @@ int validate(const psfm_params* p, const psfm_inputs* in) {
     if (p->cam_model != PSFM_CAM_PINHOLE && p->cam_model != PSFM_CAM_FISHEYE) return fail(-16, "unknown cam_model");
     if (p->cam_model == PSFM_CAM_FISHEYE && (p->N > 2 || p->l1_only))
         return fail(-16, "fisheye calls: N <= 2 and SSIM candidates (ssim_loss_weight > 0)");
+    if (int e = validate_shift(p)) return e;
+    return 0;
+}
+
+// stored-resolution shifts of the sigmoid maps (psfm_params.sig_shift)
+bool any_shift(const psfm_params* p) {
+    for (int s = 0; s < p->S; ++s)
+        if (p->sig_shift[s]) return true;
+    return false;
+}
+int validate_shift(const psfm_params* p) {
+    for (int s = 0; s < p->S; ++s) {
+        const int k = p->sig_shift[s];
+        if (k < 0 || k > 8) return fail(-17, "sig_shift must be in [0, 8]");
+        if (k && ((p->H & ((1 << k) - 1)) || (p->W & ((1 << k) - 1))))
+            return fail(-17, "sig_shift: H and W must be multiples of 2^sig_shift");
+    }
+    if (any_shift(p) && p->l1_only) return fail(-17, "sig_shift > 0: SSIM candidates only (the K1 / K12 sweeps)");
     return 0;
 }
 
@@ -1102,6 +1155,7 @@ int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm
                          const float* grad_out, float* const* grad_sig, void* stream) {
     if (int e = validate(p, in)) return e;
     if (p->cam_model != PSFM_CAM_PINHOLE) return fail(-16, "K2 backward is pinhole-only: use psfm_photometric_fwd_grad");
+    if (any_shift(p)) return fail(-17, "sig_shift > 0: use psfm_photometric_fwd_grad (K12) for the gradient");
     if (!ws || !ws->pose_part || (p->reduce_op == PSFM_REDUCE_MIN && !ws->argmin))
         return fail(-12, "null workspace");
     if (!grad_out || !grad_sig) return fail(-14, "null grad buffers");
@@ -1132,6 +1186,7 @@ int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float
                         const float* grad_out, float* const* grad_sig, void* stream) {
     if (int e = validate(p, in)) return e;
     if (!smooth_stats || !grad_out || !grad_sig) return fail(-14, "null smoothness grad buffers");
+    if (any_shift(p)) return fail(-17, "sig_shift > 0: use psfm_photometric_fwd_grad (K12) for the gradient");
     KArgs a{};
     a.p = *p;
     a.in = *in;
@@ -1211,9 +1266,13 @@ int psfm_photometric_prepass(const psfm_params* p, const psfm_inputs* in, const 
     if (p->automask && !(p->clip_loss > 0.0f)) launch_k0(p, sweep_args(p, in, ws), st);  // clip: clip_stats did
     if (p->smooth_w > 0.0f) {
         SigSumArgs sa{};
-        for (int s = 0; s < p->S; ++s) sa.sig[s] = in->sig[s];
+        for (int s = 0; s < p->S; ++s) {
+            sa.sig[s] = in->sig[s];
+            sa.shift[s] = p->sig_shift[s];
+        }
         sa.part = ws->sig_part;
         sa.B = p->B;
+        sa.W = p->W;
         sa.plane = (uint32_t)(p->H * p->W);
         hipLaunchKernelGGL(k_sig_sum, dim3(fused::SIGCH, p->B, p->S), dim3(NT), 0, st, sa);
     }
@@ -1270,10 +1329,14 @@ int psfm_photometric_grad_finish(const psfm_params* p, const float* smooth_stats
     const bool sm = p->smooth_w > 0.0f;
     if (sm && !smooth_stats) return fail(-14, "null smooth_stats");
     GradFinishArgs a{};
+    if (int e = validate_shift(p)) return e;
     for (int s = 0; s < p->S; ++s) {
         if (!grad_sig[s] || !grad_k12[s]) return fail(-14, "null grad_sig");
+        if (p->sig_shift[s] && grad_sig[s] == grad_k12[s])
+            return fail(-14, "grad_finish with sig_shift > 0 cannot run in place");
         a.gin[s] = grad_k12[s];
         a.g[s] = grad_sig[s];
+        a.shift[s] = p->sig_shift[s];
     }
     a.smooth_stats = smooth_stats;
     a.grad_out = grad_out;

@@ -360,6 +360,7 @@ struct K1 {
     const psfm_params& p;
     Cfg<FAST> cfg;
     int H, W, b, s, unit, y0, col, colr, B;
+    int sh, Ws, colc;  // sigmoid storage: (H >> sh, W >> sh) (psfm_params.sig_shift)
     uint32_t plane;
     bool pcol;
     DepthChain dc;
@@ -387,15 +388,18 @@ struct K1 {
         dc = depth_chain(p);
         l1w = 1.0f - p.ssim_w;
         tgt = a.in.tgt + (size_t)b * 3 * plane;
-        sig = pick4(a.in.sig, s) + (size_t)b * plane;
+        sh = pick4(p.sig_shift, s);
+        Ws = W >> sh;
+        colc = colr >> sh;
+        sig = pick4(a.in.sig, s) + (size_t)b * (plane >> (2 * sh));
 #pragma unroll
         for (int j = 0; j < NC; ++j) ctx[j] = pick4(a.in.ctx, j) + (size_t)b * 3 * plane;
         cams.load(as_const(a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC), B, H, W);
         thr = (cfg.clip() && !STATS) ? a.ws.clip_thr + (size_t)s * (cfg.automask() ? 2 * NC : NC) : nullptr;
     }
 
-    __device__ __forceinline__ float load_sig(int v) const {
-        return sig[(uint32_t)(reflect1(v, H) * W + colr)];
+    __device__ __forceinline__ float load_sig(int v) const {  // nearest 2^sh upsampling (K12 load_sig)
+        return sig[(uint32_t)((reflect1(v, H) >> sh) * Ws + colc)];
     }
 
     // issue row v: target, warped contexts (from the prefetched sigmoid sg)

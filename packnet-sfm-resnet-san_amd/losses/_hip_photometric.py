@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from .. import _hip
 from ..geometry.camera_utils import scale_intrinsics, pinhole_inverse
+from ..utils.image import NearestScales
 
 
 # Optional live kernel timing (bench.py roofline): HIP events recorded on the stream the kernels
@@ -91,7 +92,7 @@ def kernel_times_ms():
 class _Call:
     """One ABI call: scales that share an image size (one call for the full-res case)."""
 
-    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask, fused=False, cam_model=0):
+    def __init__(self, cfg, scale0, S, image, contexts, sigs, cam, mask, fused=False, cam_model=0, shifts=None):
         B, _, H, W = image.shape
         p = _hip.Params()
         p.B, p.H, p.W, p.N, p.S = B, H, W, len(contexts), S
@@ -103,6 +104,8 @@ class _Call:
         p.clip_loss, p.smooth_w = cfg["clip"], cfg["smooth_w"]
         p.grad_fused = int(fused)
         p.cam_model = cam_model
+        for i, k in enumerate(shifts or ()):
+            p.sig_shift[i] = int(k)
         self.params = p
         self.image, self.contexts, self.sigs, self.cam, self.mask = image, contexts, sigs, cam, mask
         inp = _hip.Inputs()
@@ -179,11 +182,14 @@ class PhotometricLossFn(torch.autograd.Function):
         N, n = len(contexts), len(sigs)
         Tf = T.detach().reshape(N, B, 12).float()
 
-        # group consecutive scales of equal size into one call (full-res: one call for all)
+        # group consecutive scales of equal size into one call (full-res: one call for all);
+        # stored coarse maps with a nearest 2^k mapping count as full size (cfg["shifts"])
+        shifts = cfg.get("shifts")
+        size = (lambda i: tuple(cfg["full_hw"])) if shifts else (lambda i: tuple(sigs[i].shape[-2:]))
         groups, s0 = [], 0
         while s0 < n:
             s1 = s0 + 1
-            while s1 < n and sigs[s1].shape[-2:] == sigs[s0].shape[-2:] and s1 - s0 < _hip.MAX_SCALES:
+            while s1 < n and size(s1) == size(s0) and s1 - s0 < _hip.MAX_SCALES:
                 s1 += 1
             groups.append((s0, s1))
             s0 = s1
@@ -197,7 +203,7 @@ class PhotometricLossFn(torch.autograd.Function):
                                       "gradient path (FUSED_GRAD)")
         calls = []
         for (a, b) in groups:
-            hw = sigs[a].shape[-2:]
+            hw = size(a)
             scale = hw[1] / float(W)  # Camera.scaled(DW/W) (camera.py:84-108)
             if fish:
                 cam = _fisheye_records(K, ref_K, Tf, scale, hw[0] / float(H), b - a, N, B, dev)
@@ -213,7 +219,8 @@ class PhotometricLossFn(torch.autograd.Function):
             cx = [_to_size(c, hw, "bilinear") for c in contexts]
             mk = _to_size(mask, hw, "nearest").contiguous() if mask is not None else None
             calls.append(_Call(cfg, a, b - a, im, cx, sigs[a:b], cam, mk, fused,
-                               _hip.CAM_FISHEYE if fish else _hip.CAM_PINHOLE))
+                               _hip.CAM_FISHEYE if fish else _hip.CAM_PINHOLE,
+                               shifts[a:b] if shifts else None))
 
         L = _hip.lib()
         st = _hip.stream(dev)
@@ -221,8 +228,8 @@ class PhotometricLossFn(torch.autograd.Function):
             if cfg["clip"] > 0.0:
                 _run("clip_stats", L.psfm_photometric_clip_stats, ctypes.byref(c.params),
                      ctypes.byref(c.inputs), ctypes.byref(c.ws), st, keep=(c,))
-            if fused:
-                c.gsig = [torch.empty_like(t) for t in c.sigs]
+            if fused:   # K12's dL/dsig planes at the call's full size (grad_finish maps them to the stored size)
+                c.gsig = [torch.empty(B, 1, c.params.H, c.params.W, device=dev, dtype=torch.float32) for _ in c.sigs]
                 _run("prepass", L.psfm_photometric_prepass, ctypes.byref(c.params), ctypes.byref(c.inputs),
                      ctypes.byref(c.ws), st, keep=(c,))
                 _run("K12_photometric_fwd_grad", L.psfm_photometric_fwd_grad, ctypes.byref(c.params),
@@ -260,7 +267,7 @@ class PhotometricLossFn(torch.autograd.Function):
         if ctx.fused:  # gradient already computed by K12 for dL/dloss = 1: scale + normaliser term
             grads = []
             for c in calls:
-                gsig = [torch.empty_like(g) for g in c.gsig]
+                gsig = [torch.empty(t.shape, device=dev, dtype=torch.float32) for t in c.sigs]
                 _run("grad_finish", L.psfm_photometric_grad_finish, ctypes.byref(c.params),
                      _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), _sig_array(c.gsig), _sig_array(gsig), st,
                      keep=(c, ctx.smooth_stats, gout, gsig))
@@ -285,7 +292,20 @@ class PhotometricLossFn(torch.autograd.Function):
 
 
 def photometric_loss_hip(image, contexts, sigs, K, ref_K, T, mask, cfg):
-    """Returns (loss[1], metrics.photometric_loss, metrics.smoothness_loss)."""
+    """Returns (loss[1], metrics.photometric_loss, metrics.smoothness_loss).
+
+    `sigs` a list of maps, or a NearestScales (utils/image.py): the stored maps and their 2^k
+    nearest factors go to the kernels as psfm_params.sig_shift, gradients come back at the stored
+    size.  The in-kernel mapping serves the K12 training path and the K1 forward path; the unfused
+    backward (FUSED_GRAD off, N > 2, L1-only) gets the materialised upsample instead."""
+    shifts = None
+    if isinstance(sigs, NearestScales):
+        wants_grad = torch.is_grad_enabled() and (T.requires_grad or any(s.requires_grad for s in sigs.stored))
+        in_kernel = cfg["ssim_w"] > 0.0 and (not wants_grad or (FUSED_GRAD and len(contexts) <= 2))
+        if in_kernel:
+            shifts = tuple(sigs.shifts)
+            cfg = dict(cfg, full_hw=tuple(sigs.shape), shifts=shifts)
+        sigs = sigs.stored if in_kernel else sigs.materialize()
     return PhotometricLossFn.apply(cfg, image, mask, K, ref_K, T, len(contexts), *contexts, *sigs)
 
 

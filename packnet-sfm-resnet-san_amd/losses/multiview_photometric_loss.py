@@ -17,6 +17,7 @@ import torch
 from .loss_base import LossBase, ProgressiveScaling
 from ._hip_photometric import photometric_loss_hip
 from .. import _hip
+from ..utils.image import NearestScales
 
 
 def SSIM(x, y, C1=1e-4, C2=9e-4, kernel_size=3, stride=1):
@@ -64,7 +65,10 @@ class MultiViewPhotometricLoss(LossBase):
         if isinstance(intrinsics, dict) != isinstance(ref_intrinsics, dict):
             raise ValueError("intrinsics and ref_intrinsics must be both pinhole K or both fisheye dicts")
         self.n = self.progressive_scaling(progress)
-        sigs = [s.float() for s in inv_depths[:self.n]]  # nets may run under bf16 autocast
+        if isinstance(inv_depths, NearestScales):   # stored maps + 2^k nearest mapping (no full-size copies)
+            sigs = NearestScales([s.float() for s in inv_depths.stored[:self.n]], inv_depths.shape)
+        else:
+            sigs = [s.float() for s in inv_depths[:self.n]]  # nets may run under bf16 autocast
         T = torch.stack([p.mat[:, :3, :] for p in poses], 0)  # [N,B,3,4], differentiable
         cfg = dict(n=self.n, automask=bool(self.automask_loss),
                    reduce_op=_hip.REDUCE_MIN if self.photometric_reduce_op == "min" else _hip.REDUCE_MEAN,

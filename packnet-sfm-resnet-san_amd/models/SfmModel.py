@@ -18,8 +18,11 @@ class SfmModel(BaseModel):
     parallel branch.  Numerically identical to the serial order."""
 
     def __init__(self, depth_net=None, pose_net=None, rotation_mode="euler", flip_lr_prob=0.0,
-                 upsample_depth_maps=False, overlap_pose_net=True, **kwargs):
+                 upsample_depth_maps=False, overlap_pose_net=True, lazy_upsample=True, **kwargs):
         super().__init__()
+        # lazy_upsample: the training-mode upsampled 'inv_depths' are NearestScales (the loss reads
+        # the depth net's stored maps; models/model_utils.upsample_output)
+        self.lazy_upsample = lazy_upsample
         self.overlap_pose_net = overlap_pose_net
         self._side_streams = {}
         self.depth_net = depth_net
@@ -45,7 +48,7 @@ class SfmModel(BaseModel):
         flag = random.random() < self.flip_lr_prob if self.training else force_flip
         output = self.depth_net_flipping(batch, flag, **kwargs)
         if self.training and self.upsample_depth_maps:
-            output = upsample_output(output, mode="nearest", align_corners=None)
+            output = upsample_output(output, mode="nearest", align_corners=None, lazy=self.lazy_upsample)
         return output
 
     def compute_pose_net(self, image, contexts):

@@ -3,7 +3,7 @@
 `upsample_output` (:152-196)."""
 import torch
 
-from ..utils.image import flip_lr, interpolate_scales
+from ..utils.image import NearestScales, flip_lr, interpolate_scales
 from ..utils.misc import filter_dict
 
 
@@ -60,9 +60,16 @@ def flip_output(output):
     return output
 
 
-def upsample_output(output, mode="nearest", align_corners=None):
+def upsample_output(output, mode="nearest", align_corners=None, lazy=False):
+    """`lazy` (the training step, SfmModel.compute_depth_net): 'inv_depths' reaching full size by
+    exact 2^k nearest factors become a NearestScales sequence — the loss reads the stored maps
+    through the index mapping and nothing full-size is written (utils/image.py)."""
     for key in filter_dict(output, ["inv_depths", "uncertainty"]):
-        output[key] = interpolate_scales(output[key], mode=mode, align_corners=align_corners)
+        v = output[key]
+        if lazy and key == "inv_depths" and mode == "nearest" and NearestScales.exact(v, v[0].shape[-2:]):
+            output[key] = NearestScales(v, v[0].shape[-2:])
+            continue
+        output[key] = interpolate_scales(v, mode=mode, align_corners=align_corners)
     for key in filter_dict(output, ["inv_depths_context"]):
         output[key] = [interpolate_scales(v, mode=mode, align_corners=align_corners) for v in output[key]]
     return output

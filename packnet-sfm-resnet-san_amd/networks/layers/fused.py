@@ -22,11 +22,15 @@ import torch.nn.functional as F
 from ... import _hip
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
-ENABLED = False  # opt-in until the fused reductions beat MIOpen (bench.py --fused-nets)
+# Which layer kinds run fused, from the A/B of the ResNetSAN01 + PoseNet step on MI355X
+# (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
+# chain (972 -> 1025 img/s together); BatchNorm + ReLU loses to MIOpen's BN kernels (-> 981), so
+# BN stays on MIOpen.  bench.py --fused-nets overrides.
+FUSE = {"bias": True, "gn": True, "bn": False}
 
 
-def _fusable(x):
-    return ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+def _fusable(x, kind):
+    return FUSE[kind] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
 
 
 def _rows(t):
@@ -87,7 +91,7 @@ class _BiasAct(torch.autograd.Function):
 def bias_act(x, bias, act, module):
     """act(x + bias): x = conv output WITHOUT its bias (F.conv2d(..., None)); `module` owns the
     reduction counter.  Sigmoid outputs are fp32 (they feed the fp32 photometric loss)."""
-    if _fusable(x) and bias is not None:
+    if _fusable(x, "bias") and bias is not None:
         return _BiasAct.apply(x, bias, act, _counter(module, x.device))
     y = x if bias is None else x + bias.to(x.dtype).view(1, -1, 1, 1)
     if act == ACT_RELU:
@@ -147,7 +151,7 @@ class _BNAct(torch.autograd.Function):
 
 def bn_act(x, bn, relu=True, residual=None):
     """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn`."""
-    if (_fusable(x) and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
+    if (_fusable(x, "bn") and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
             and bn.running_mean is not None):
         if bn.num_batches_tracked is not None:  # the graph trainer keeps these off the step
             bn.num_batches_tracked.add_(1)
@@ -204,10 +208,57 @@ class _GNAct(torch.autograd.Function):
 
 def gn_act(x, bias, gn, relu=True):
     """act(groupnorm(x + bias)) with the reference's nn.GroupNorm module `gn`."""
-    if _fusable(x) and bias is not None and gn.affine and x.shape[1] % gn.num_groups == 0:
+    if _fusable(x, "gn") and bias is not None and gn.affine and x.shape[1] % gn.num_groups == 0:
         return _GNAct.apply(x, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), bool(relu),
                             _counter(gn, x.device))
     if bias is not None:
         x = x + bias.to(x.dtype).view(1, -1, 1, 1)
     y = gn(x)
     return torch.relu(y) if relu else y
+
+
+# ----------------------------------------------------------------------------------------------
+UPCAT = True  # decoder up-stage input on HIP
+
+
+class _UpCat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, skip):
+        N, C1, h, w = x.shape
+        C2 = skip.shape[1] if skip is not None else 0
+        out = torch.empty((N, C1 + C2, 2 * h, 2 * w), device=x.device, dtype=x.dtype,
+                          memory_format=torch.channels_last)
+        _hip.check(_hip.lib().psfm_upcat_fwd(_hip.ptr(x), _hip.ptr(skip), N, h, w, C1, C2, _hip.ptr(out),
+                                             _hip.stream(x.device)), "psfm_upcat_fwd")
+        ctx.dims, ctx.has_skip = (N, C1, C2, h, w), skip is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        N, C1, C2, h, w = ctx.dims
+        dout = _rows(dout)
+        dx = torch.empty((N, C1, h, w), device=dout.device, dtype=dout.dtype, memory_format=torch.channels_last)
+        dskip = torch.empty((N, C2, 2 * h, 2 * w), device=dout.device, dtype=dout.dtype,
+                            memory_format=torch.channels_last) if ctx.has_skip else None
+        _hip.check(_hip.lib().psfm_upcat_bwd(_hip.ptr(dout), N, h, w, C1, C2, _hip.ptr(dx), _hip.ptr(dskip),
+                                             _hip.stream(dout.device)), "psfm_upcat_bwd")
+        return dx, dskip
+
+
+def _nhwc_bf16(t):
+    return t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def up_cat(x, skip=None):
+    """torch.cat([F.interpolate(x, scale_factor=2, mode='nearest'), skip], 1) — the DepthDecoder
+    up-stage input (depth_decoder.py:48-57) — as ONE HIP kernel each way on bf16 channels_last
+    activations (include/psfm_netops.h psfm_upcat_*).  Other layouts / dtypes / devices run the
+    reference's op chain (upsample with the deterministic block-sum backward, then cat)."""
+    from ...utils.image import upsample_nearest
+    if (UPCAT and _nhwc_bf16(x) and x.shape[1] % 8 == 0 and
+            (skip is None or (_nhwc_bf16(skip) and skip.shape[1] % 8 == 0 and skip.device == x.device
+                              and tuple(skip.shape[-2:]) == (2 * x.shape[2], 2 * x.shape[3])
+                              and skip.shape[0] == x.shape[0]))):
+        return _UpCat.apply(x, skip)
+    up = upsample_nearest(x, 2)
+    return up if skip is None else torch.cat([up, skip.to(up.dtype)], 1)

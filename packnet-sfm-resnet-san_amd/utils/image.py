@@ -1,6 +1,7 @@
 """Image helpers with the reference API (packnet_sfm/utils/image.py:85-282):
 `gradient_x/y`, `interpolate_image`, `interpolate_scales`, `match_scales`, `meshgrid`,
 `image_grid`, `flip_lr`."""
+from collections.abc import Sequence
 from functools import lru_cache
 
 import torch
@@ -65,6 +66,48 @@ class UpsampleNearest(torch.nn.Module):
 
     def forward(self, x):
         return upsample_nearest(x, self.scale_factor)
+
+
+class NearestScales(Sequence):
+    """Inverse-depth scales nearest-upsampled to one size (`upsample_output(mode='nearest')`,
+    models/model_utils.py:152-196) WITHOUT materialising the upsampled maps.
+
+    The photometric loss reads the stored maps through the 2^k index mapping
+    (psfm_params.sig_shift, include/psfm.h) and returns their gradient at the stored size, so
+    the training step never writes the 4 full-resolution copies nor runs their backward
+    reductions.  Indexing / iterating yields the upsampled tensors (differentiable, deterministic
+    backward), so callers that read `output['inv_depths'][i]` see the reference's values."""
+
+    def __init__(self, stored, shape):
+        self.stored = list(stored)
+        self.shape = tuple(shape[-2:])
+        self.shifts = []
+        for t in self.stored:
+            f = self.shape[0] // t.shape[-2]
+            k = f.bit_length() - 1
+            if f != (1 << k) or t.shape[-2] * f != self.shape[0] or t.shape[-1] * f != self.shape[1]:
+                raise ValueError(f"NearestScales: {tuple(t.shape[-2:])} -> {self.shape} is not a 2^k upsampling")
+            self.shifts.append(k)
+
+    @staticmethod
+    def exact(images, shape):
+        """True when every image reaches `shape` by an exact power-of-two factor."""
+        for t in images:
+            f = shape[0] // t.shape[-2]
+            if f < 1 or f & (f - 1) or t.shape[-2] * f != shape[0] or t.shape[-1] * f != shape[1]:
+                return False
+        return True
+
+    def __len__(self):
+        return len(self.stored)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return NearestScales(self.stored[i], self.shape)
+        return upsample_nearest(self.stored[i], 1 << self.shifts[i])
+
+    def materialize(self):
+        return [self[i] for i in range(len(self))]
 
 
 def interpolate_scales(images, shape=None, mode="bilinear", align_corners=False):

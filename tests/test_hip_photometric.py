@@ -332,3 +332,49 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
     print(f"B={B} {H}x{W} dL/dpose: rel err vs fp64 oracle {gu.rel_err(got_v, ref_v):.2e}, flagged-pixel share "
           f"{float((pose_bound / np.abs(ref_v).max()).max()):.2e} of max, worst |err| / allowance {ratio:.2f}")
     assert ratio <= 1.0
+
+
+@pytest.mark.parametrize("B,H,W,clip", [(2, 32, 96, 0.0), (4, 192, 640, 0.0), (1, 64, 128, 0.5)])
+def test_nearest_scales_fold_matches_materialized(dev, B, H, W, clip):
+    """upsample_output's lazy NearestScales (the training default): the kernels read the depth
+    net's stored maps through the 2^k nearest mapping (psfm_params.sig_shift) instead of 4
+    materialised full-size copies.  Same values in the same order -> loss, metrics and dL/dpose
+    bitwise equal to the materialised path; the stored-size dL/dsig = the block sums of the
+    materialised full-size gradient (fp32 sums of 4^k terms in another order: 1e-6 * max|g|).
+    Also the forward-only (no_grad, K1) path, bitwise."""
+    from packnet_sfm_amd.geometry.pose import Pose
+    from packnet_sfm_amd.losses.multiview_photometric_loss import MultiViewPhotometricLoss
+    from packnet_sfm_amd.utils.image import NearestScales, upsample_nearest
+    image, ctx, K, vec, _ = _seeded_inputs(11, B, H, W)
+    g = torch.Generator().manual_seed(7)
+    stored = [gu.sigmoid_maps(g, B, H >> k, W >> k) for k in range(4)]
+    fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
+                                  photometric_reduce_op="min", automask_loss=True, clip_loss=clip,
+                                  min_depth=0.5, max_depth=80.0)
+    args = (image.to(dev), [c.to(dev) for c in ctx])
+
+    def run(lazy, grad=True):
+        st = [c.to(dev).requires_grad_(grad) for c in stored]
+        v = vec.to(dev).requires_grad_(grad)
+        sig = NearestScales(st, (H, W)) if lazy else [upsample_nearest(s, 1 << k) for k, s in enumerate(st)]
+        out = fn(*args, sig, K.to(dev), K.to(dev), [Pose.from_vec(v[:, j], "euler") for j in range(2)])
+        if grad:
+            out["loss"].sum().backward()
+        torch.cuda.synchronize()
+        return out, st, v
+
+    a, sa, va = run(True)
+    b, sb, vb = run(False)
+    assert torch.equal(a["loss"], b["loss"])
+    for k in ("photometric_loss", "smoothness_loss"):
+        assert torch.equal(a["metrics"][k], b["metrics"][k])
+    assert torch.equal(va.grad, vb.grad)
+    for k in range(4):
+        assert sa[k].grad.shape == stored[k].shape
+        tol = 1e-6 * float(sb[k].grad.abs().max())
+        err = float((sa[k].grad - sb[k].grad).abs().max())
+        assert err <= tol, f"scale {k}: {err} > {tol}"
+    with torch.no_grad():
+        c, _, _ = run(True, grad=False)
+        d, _, _ = run(False, grad=False)
+    assert torch.equal(c["loss"], d["loss"])

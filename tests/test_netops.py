@@ -38,11 +38,11 @@ def dev():
 
 @pytest.fixture(autouse=True)
 def fused_on():
-    """The fused path is opt-in in the product (fused.ENABLED); these tests exercise it."""
-    prev = FU.ENABLED
-    FU.ENABLED = True
+    """Every fused kind on (the product enables the measured winners, fused.FUSE)."""
+    prev = dict(FU.FUSE)
+    FU.FUSE.update(bias=True, gn=True, bn=True)
     yield
-    FU.ENABLED = prev
+    FU.FUSE.update(prev)
 
 
 @gpu
@@ -188,7 +188,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
     x = _cl(torch.rand(2, 3, 96, 320)).to(dev)
 
     def run(enabled, amp):
-        FU.ENABLED = enabled
+        FU.FUSE.update(bias=enabled, gn=enabled, bn=enabled)
         try:
             net.zero_grad(set_to_none=True)
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -200,7 +200,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
                      net.encoder.encoder.conv1.weight.grad.detach().float().clone(),
                      net.encoder.encoder.layer4[1].bn2.weight.grad.detach().float().clone()])
         finally:
-            FU.ENABLED = True
+            FU.FUSE.update(bias=True, gn=True, bn=True)
 
     ref = run(False, False)
     fused, plain = run(True, True), run(False, True)
@@ -228,3 +228,32 @@ def test_cpu_path_is_the_reference_op_chain():
     b = torch.randn(8)
     assert torch.equal(FU.gn_act(x, b, gn, True), torch.relu(gn(x + b.view(1, -1, 1, 1))))
     assert torch.equal(FU.bias_act(x, b, FU.ACT_SIGMOID, nn.Module()), torch.sigmoid(x + b.view(1, -1, 1, 1)))
+
+
+@gpu
+@pytest.mark.parametrize("N,C1,C2,h,w", [(4, 256, 256, 6, 20), (4, 16, 0, 96, 320), (2, 32, 64, 48, 160),
+                                         (1, 8, 24, 3, 5)])
+def test_upcat_matches_torch(dev, N, C1, C2, h, w):
+    """psfm_upcat vs the reference's op chain cat([F.interpolate(x, 2, 'nearest'), skip]):
+    forward and dskip bitwise; dx = the 2x2 block sums of dout, fp32 accumulation with one bf16
+    rounding (1 bf16 ulp of the fp32 sum); the kernel actually runs (no op-chain fallback)."""
+    torch.manual_seed(1)
+    x = _cl(torch.randn(N, C1, h, w)).to(dev).bfloat16().requires_grad_(True)
+    skip = _cl(torch.randn(N, C2, 2 * h, 2 * w)).to(dev).bfloat16().requires_grad_(True) if C2 else None
+    calls = []
+    orig = FU._UpCat.apply
+    FU._UpCat.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        out = FU.up_cat(x, skip)
+    finally:
+        FU._UpCat.apply = orig
+    assert calls and out.is_contiguous(memory_format=torch.channels_last)
+    up = torch.nn.functional.interpolate(x.detach(), scale_factor=2, mode="nearest")
+    ref = up if skip is None else torch.cat([up, skip.detach()], 1)
+    assert torch.equal(out, ref)
+    dout = _cl(torch.randn(out.shape)).to(dev).bfloat16()
+    out.backward(dout)
+    blk = dout[:, :C1].float().reshape(N, C1, h, 2, w, 2).sum((3, 5))
+    assert (x.grad.float() - blk).abs().max() <= (blk.abs() * 2.0 ** -8).max() + 1e-30
+    if skip is not None:
+        assert torch.equal(skip.grad, dout[:, C1:])

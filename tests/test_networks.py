@@ -207,3 +207,51 @@ def test_upsample_nearest_equals_interpolate(f, cl):
     ups = interpolate_scales([x, x[..., :3, :4]], shape=(5 * f, 7 * f), mode="nearest", align_corners=None)
     assert torch.equal(ups[0], yb)    # exact multiple -> the deterministic op
     assert ups[1].shape[-2:] == (5 * f, 7 * f)   # not a multiple -> F.interpolate
+
+
+def test_config1_depthresnet_poseresnet_step_on_gpu_matches_cpu_oracle():
+    """BASELINE config 1 (configs/overfit_kitti.yaml): SelfSupModel(DepthResNet 18pt + PoseResNet
+    18pt), fp32, B=6, 192x640, min_depth 0 / max_depth 80.  The GPU step (MIOpen nets + HIP loss
+    through the lazy upsample fold) vs the same weights on CPU with the oracle loss: loss 1e-4
+    relative, every parameter-gradient norm 2e-2 (fp32 MIOpen vs CPU convolutions re-round the
+    activations, which moves min-reprojection near-ties / bilinear kinks of the photometric
+    gradient — the same tolerance as the reference-golden step tests)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import __graft_entry__
+    __graft_entry__.build()
+    from oracle import photometric_oracle as O
+    from packnet_sfm_amd.models.SelfSupModel import SelfSupModel
+    from packnet_sfm_amd.networks.depth.DepthResNet import DepthResNet
+    from packnet_sfm_amd.networks.pose.PoseResNet import PoseResNet
+    torch.manual_seed(3)
+    kw = dict(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001, photometric_reduce_op="min",
+              automask_loss=True, clip_loss=0.0, min_depth=0.0, max_depth=80.0)
+    model = SelfSupModel(**kw, upsample_depth_maps=True, rotation_mode="euler")
+    model.add_depth_net(DepthResNet(version="18pt"))
+    model.add_pose_net(PoseResNet(version="18pt"))
+    model.train()
+    B, H, W = 6, 192, 640
+    rgb, ctx, K = _batch(B, H, W)
+    # CPU: the same nets, upsample_output materialised, oracle loss (tests-only checker)
+    inv = model.depth_net(rgb)["inv_depths"]
+    inv = [torch.nn.functional.interpolate(i, size=(H, W), mode="nearest") for i in inv]
+    vec = model.pose_net(rgb, ctx)
+    ref = O.photometric_loss(rgb, ctx, inv, K, K, [O.pose_vec_to_mat(vec[:, j]) for j in range(2)], None,
+                             num_scales_=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
+                             photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
+                             min_depth=0.0, max_depth=80.0)[0]
+    ref.sum().backward()
+    ref_norms = {n: float(p.grad.double().norm()) for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    dev = torch.device("cuda:0")
+    model = model.to(dev)
+    batch = dict(rgb=rgb.to(dev), rgb_context=[c.to(dev) for c in ctx], rgb_original=rgb.to(dev),
+                 rgb_context_original=[c.to(dev) for c in ctx], intrinsics=K.to(dev))
+    out = model(batch, progress=0.0)
+    out["loss"].sum().backward()
+    assert gu.rel_err(out["loss"].detach().cpu(), ref.detach()) < 1e-4
+    got = {n: float(p.grad.double().norm()) for n, p in model.named_parameters() if p.grad is not None}
+    assert set(got) == set(ref_norms)
+    bad = {n: (got[n], r) for n, r in ref_norms.items() if abs(got[n] - r) > 2e-2 * r + 1e-12}
+    assert not bad, bad

@@ -23,7 +23,7 @@ if args.lib:
     _hip.LIB_PATH = args.lib
 from packnet_sfm_amd.networks.layers import fused as FU  # noqa: E402
 
-FU.ENABLED = args.mode == "fused"
+FU.FUSE.update(bias=args.mode == "fused", gn=args.mode == "fused", bn=args.mode == "fused")
 dev = torch.device("cuda:0")
 BN_SHAPES = [(4, 64, 96, 320), (4, 64, 48, 160), (4, 128, 24, 80), (4, 256, 12, 40), (4, 512, 6, 20)]
 GN_SHAPES = [(4, 16, 96, 320), (4, 32, 48, 160), (4, 64, 24, 80), (4, 128, 12, 40), (4, 256, 6, 20)]
