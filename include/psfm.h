@@ -96,12 +96,16 @@ typedef struct psfm_workspace {
                                                     UN-warped context (scale independent)  */
     float* sig_part;     /* [S][B][16]              chunk sums of each sigmoid map (the
                                                     smoothness normaliser, fwd_grad only)  */
+    float* cam_pairs;    /* [S][B][PSFM_CAMREC][2]  the camera records of contexts 0 and 1
+                                                    interleaved (written by the prepass): K12
+                                                    projects both contexts with packed f32
+                                                    pairs, one 8-byte scalar load per entry  */
 } psfm_workspace;
 
 /* number of floats (and argmin bytes) the workspace of this call needs */
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
                           size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp,
-                          size_t* sig_part);
+                          size_t* sig_part, size_t* cam_pairs);
 
 /* Clip statistics pass (only when clip_loss > 0): per-candidate-map sum / sum of squares
  * (calc_photometric_loss :249-253), then thresholds mean + clip*std (unbiased). */

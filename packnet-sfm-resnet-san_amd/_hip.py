@@ -43,7 +43,7 @@ class Workspace(ctypes.Structure):
     """psfm_workspace."""
     _fields_ = [("photo_part", c_void_p), ("smooth_part", c_void_p), ("clip_part", c_void_p),
                 ("clip_thr", c_void_p), ("pose_part", c_void_p), ("argmin", c_void_p),
-                ("unwarp", c_void_p), ("sig_part", c_void_p)]
+                ("unwarp", c_void_p), ("sig_part", c_void_p), ("cam_pairs", c_void_p)]
 
 
 class MetricsParams(ctypes.Structure):
@@ -81,7 +81,7 @@ def lib():
     WS, WSP, IN = ctypes.POINTER(Workspace), ctypes.POINTER(ctypes.POINTER(Workspace)), ctypes.POINTER(Inputs)
     sz = ctypes.POINTER(c_size_t)
     sig = {
-        "psfm_workspace_floats": ([P, sz, sz, sz, sz, sz, sz, sz, sz], c_int),
+        "psfm_workspace_floats": ([P, sz, sz, sz, sz, sz, sz, sz, sz, sz], c_int),
         "psfm_photometric_clip_stats": ([P, IN, WS, V], c_int),
         "psfm_photometric_fwd": ([P, IN, WS, V], c_int),
         "psfm_smoothness_fwd": ([P, IN, WS, V], c_int),

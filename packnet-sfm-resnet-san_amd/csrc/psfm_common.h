@@ -177,6 +177,7 @@ __device__ __forceinline__ float ldg(const float* __restrict__ base, uint32_t by
 struct TapAddr {
     uint32_t nw, ne, sw, se;  // BYTE offsets within one channel plane
     bool vnw, vne, vsw, vse;
+    bool xw, xe, yn, ys;      // column x0 / x0+1, row y0 / y0+1 in bounds (tap valid = row && column)
     float ax, bx, ay, by;  // (x0+1-ix), (ix-x0), (y0+1-iy), (iy-y0)
 };
 
@@ -192,6 +193,10 @@ __device__ __forceinline__ TapAddr tap_addr(float ix, float iy, int H, int W) {
     a.ne = a.nw + (uint32_t)(cx1 - cx0) * 4u;
     a.sw = (uint32_t)(cy1 * W + cx0) * 4u;
     a.se = a.sw + (uint32_t)(cx1 - cx0) * 4u;
+    a.xw = xw;
+    a.xe = xe;
+    a.yn = yn;
+    a.ys = ys;
     a.vnw = yn && xw;
     a.vne = yn && xe;
     a.vsw = ys && xw;

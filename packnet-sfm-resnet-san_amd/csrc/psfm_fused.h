@@ -8,24 +8,28 @@
 // for dL/dloss = 1 and scaled later by psfm_photometric_grad_finish (which also adds the one
 // per-image term that needs whole-image sums: d/ds of the 1/mean(s) smoothness normaliser).
 //
-// One wave per (60-column stripe, RB-row band, image, scale), both contexts of a target packed
-// in the two halves of 64-bit register pairs (v_pk_* arithmetic).  Lanes = columns c0-2..c0+61;
-// the 60 inner lanes are outputs (a 3x3 SSIM window of a 3x3 neighbourhood: halo 2).  Step k
-// of the sweep:
-//   issue   row v = y0-2+k: target, sigmoid (prefetched one step earlier), lift/project per
-//           context and the 12 bilinear gathers per context (results consumed at the END of
-//           the step, so their latency hides under the two evaluations below);
-//   p-eval  row v-2: SSIM + L1 of every warped context (forward value AND the SSIM adjoint
+// One wave per (60-column stripe, RB-row band, image, scale).  The (at most two) contexts of a
+// target live in the two halves of 64-bit register pairs end to end: projection (pinhole: the
+// camera records of both contexts interleaved by the prepass, ws.cam_pairs, so every camera
+// entry is one SGPR pair operand of a v_pk_fma_f32), bilinear resolve, SSIM / L1, the SSIM
+// adjoint, the bilinear and projection adjoints and the dL/d[R|t] accumulation are v_pk_*
+// instructions for both contexts at once.  Lanes = columns c0-2..c0+61; the 60 inner lanes are
+// outputs (a 3x3 SSIM window of a 3x3 neighbourhood: halo 2).  Step k of the sweep:
+//   issue   row v = y0-2+k: target, sigmoid (prefetched one step earlier), lift/project and the
+//           12 bilinear gathers per context (results consumed at the END of the step, so their
+//           latency hides under the two evaluations below);
+//   p-eval  row v-2: SSIM + L1 of both warped contexts (forward value AND the SSIM adjoint
 //           coefficients d/d(mean x, E[x^2], E[xy])), automask candidates (K0 maps), min /
 //           argmin (or mean), clip / mask, forward partial sums, smoothness forward terms; the
 //           coefficients of the SELECTED candidate (G = 0 for the others) are accumulated
 //           vertically into the three q-rows they touch (reflect weights at the image edge);
 //   q-eval  row v-3 (its three p-rows are now complete): horizontal 3-sum of the accumulated
 //           coefficients (DPP), adjoint through the bilinear sample (d warp / d(ix,iy) stashed
-//           in wave-private LDS at issue time) and the projection, dL/d[R|t] per context, plus
-//           the per-pixel smoothness gradient -> dL/dsig written once (contexts summed in
-//           order in registers: deterministic, no LDS ring, no barrier);
-//   resolve the bilinear samples of row v (x and d x/d(ix,iy)).
+//           in wave-private LDS at issue time) and the projection, dL/d[R|t] of both contexts,
+//           plus the per-pixel smoothness gradient -> dL/dsig written once (no LDS ring, no
+//           barrier, no atomics: deterministic);
+//   resolve the bilinear samples of row v (x and d x/d(ix,iy)) with validity-masked tap and
+//           derivative coefficients (grid_sample's zero padding: an out-of-bounds tap adds 0).
 // Reference: losses/multiview_photometric_loss.py:15-54, :199-297, :301-327,
 // utils/depth.py:146-198, geometry/camera.py:111-190, geometry/camera_utils.py:27-59.
 #pragma once
@@ -49,50 +53,28 @@ using sweep::TWin;
 using sweep::wave_sum64;
 using sweep::work_item;
 
-#ifndef PSFM_K12_WAVES
-#define PSFM_K12_WAVES 2
-#endif
-#ifndef PSFM_K12_CAM_RELOAD
-#define PSFM_K12_CAM_RELOAD 1
-#endif
-#ifndef PSFM_K12_DI_B128
-#define PSFM_K12_DI_B128 0
-#endif
-#ifndef PSFM_K12_GT_REG
-#define PSFM_K12_GT_REG 0
-#endif
-#ifndef PSFM_K12_RB
-#define PSFM_K12_RB 20
-#endif
 // Phase boundaries of a sweep step (issue | p-eval | q-eval | resolve): the scheduler may not
 // interleave the phases, so the register peak is the largest phase's, not their sum (the
 // gathers issued in the first phase still fly under the next two: loads are asynchronous).
-#ifndef PSFM_K12_NO_PHASES
 #define PSFM_PHASE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define PSFM_PHASE() ((void)0)
-#endif
 // channel boundaries inside the SSIM phases: three unrolled channels interleaved by the
 // scheduler triple the live temporaries (~40 VGPRs each)
-#ifndef PSFM_K12_NO_CHAN
 #define PSFM_CHAN() __builtin_amdgcn_sched_barrier(0)
-#else
-#define PSFM_CHAN() ((void)0)
-#endif
-constexpr int RB = PSFM_K12_RB;  // q (output) rows per band
+constexpr int WAVES = 2;         // waves per SIMD the register budget is sized for (<= 256 VGPRs)
+constexpr int RB = 20;           // q (output) rows per band (20 beats 16 / 24: 1760 waves on 2048 slots)
 constexpr int OW = 60;           // output columns per stripe
 constexpr int SIGCH = 16;        // chunks of the per-(scale, image) sigmoid sum pre-pass
+constexpr int GTS = 28;          // per-lane dL/dT row: 12 entries x 2 contexts, padded to 28 dwords
+                                 // (the 16 lanes of a b128 access start on distinct bank groups)
 static_assert(RB % 4 == 0, "K12 band height must be a multiple of 4 (4-slot pipeline)");
 
 __host__ __device__ inline int stripes(int W) { return (W + OW - 1) / OW; }
 __host__ __device__ inline int units(int H, int W) { return stripes(W) * ((H + RB - 1) / RB); }
 // wave-private LDS (each lane touches only its own column: no barriers):
-//   [3 row slots][6 NC] d warp / d(ix, iy) | [12 NC] per-lane dL/d[R|t] accumulators
-// per-lane dL/dT row stride: 12 NC floats padded to 16 NC + ... (28 dwords at NC = 2: the 16
-// lanes of a b128 access start on distinct 4-bank groups -> no bank conflicts)
-__host__ __device__ constexpr int gt_stride(int NC) { return NC == 1 ? 12 : 28; }
+//   [3 row slots][6][64] f2  d warp / d(ix, iy) of both contexts | [64][GTS] dL/dT accumulators
 __host__ __device__ inline size_t lds_bytes(int NC) {
-    return ((size_t)3 * 6 * NC * 64 + (size_t)gt_stride(NC) * 64) * sizeof(float);
+    (void)NC;
+    return ((size_t)3 * 6 * 64 * 2 + (size_t)GTS * 64) * sizeof(float);
 }
 
 struct Args {
@@ -102,11 +84,14 @@ struct Args {
     float* grad_sig[PSFM_MAX_SCALES];
 };
 
+__device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }   // both halves (op_sel broadcast)
+__device__ __forceinline__ f2 mask01(bool a, bool b) { return f2{a ? 1.0f : 0.0f, b ? 1.0f : 0.0f}; }
+
 // Bilinear gathers in flight for one context (issued at the top of a step, resolved at its end).
 struct Pend {
     float q[3][4];
     float ax, bx, ay, by;
-    bool vnw, vne, vsw, vse;
+    bool xw, xe, yn, ys;
 };
 
 __device__ __forceinline__ void gather(const float* __restrict__ img, uint32_t pb, float ix, float iy, int H,
@@ -123,19 +108,24 @@ __device__ __forceinline__ void gather(const float* __restrict__ img, uint32_t p
     g.bx = t.bx;
     g.ay = t.ay;
     g.by = t.by;
-    g.vnw = t.vnw;
-    g.vne = t.vne;
-    g.vsw = t.vsw;
-    g.vse = t.vse;
+    g.xw = t.xw;
+    g.xe = t.xe;
+    g.yn = t.yn;
+    g.ys = t.ys;
 }
 
-// grid_sample value and d/d(ix), d/d(iy) (same arithmetic as sweep::bilinear3_vd)
-__device__ __forceinline__ void resolve(const Pend& g, float v[3], float dix[3], float diy[3]) {
+// grid_sample value and d/d(ix), d/d(iy) of the two contexts of a pair (same arithmetic as
+// sweep::bilinear3_vd).  A tap is valid when its row and its column are: the taps are multiplied
+// by 0/1 masks (out-of-bounds taps read a clamped valid address), which is grid_sample's zero
+// padding (padding_mode='zeros') without per-channel selects — every channel is v_pk_* work for
+// both contexts.
+__device__ __forceinline__ void resolve1(const Pend& g, float v[3], float dix[3], float diy[3]) {
     const float wnw = g.ax * g.ay, wne = g.bx * g.ay, wsw = g.ax * g.by, wse = g.bx * g.by;
+    const bool vnw = g.yn && g.xw, vne = g.yn && g.xe, vsw = g.ys && g.xw, vse = g.ys && g.xe;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float nw = g.vnw ? g.q[c][0] : 0.0f, ne = g.vne ? g.q[c][1] : 0.0f;
-        const float sw = g.vsw ? g.q[c][2] : 0.0f, se = g.vse ? g.q[c][3] : 0.0f;
+        const float nw = vnw ? g.q[c][0] : 0.0f, ne = vne ? g.q[c][1] : 0.0f;
+        const float sw = vsw ? g.q[c][2] : 0.0f, se = vse ? g.q[c][3] : 0.0f;
         float acc = 0.0f;
         acc += nw * wnw;
         acc += ne * wne;
@@ -146,20 +136,94 @@ __device__ __forceinline__ void resolve(const Pend& g, float v[3], float dix[3],
         diy[c] = (sw - nw) * g.ax + (se - ne) * g.bx;
     }
 }
-
-// Adjoint of project_lifted for one context: (gix, giy) -> dL/d(warp depth), dL/dT += ...
-// (same arithmetic as psfm::project_grad)
-// dL/dT += gc (X, 1)^T into 12 accumulators (registers, or a lane-private LDS row)
-template <typename P>
-__device__ __forceinline__ void acc_gT(float* g, const float (&gc)[3], const P& r) {
+__device__ __forceinline__ void resolve_pair(const Pend& a, const Pend& b, f2 (&v)[3], f2 (&dix)[3],
+                                             f2 (&diy)[3]) {
+    float va[3], xa[3], ya[3], vb[3], xb[3], yb[3];
+    resolve1(a, va, xa, ya);
+    resolve1(b, vb, xb, yb);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        g[4 * i + 0] += gc[i] * r.X0;
-        g[4 * i + 1] += gc[i] * r.X1;
-        g[4 * i + 2] += gc[i] * r.X2;
-        g[4 * i + 3] += gc[i];
+    for (int c = 0; c < 3; ++c) {
+        v[c] = f2{va[c], vb[c]};
+        dix[c] = f2{xa[c], xb[c]};
+        diy[c] = f2{ya[c], yb[c]};
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Pinhole projection of both contexts at once (Camera.reconstruct -> Pose -> Camera.project ->
+// grid_sample's normalise / unnormalise round trip, geometry/camera.py:111-190), from the
+// context-paired record of (s, b): entry k = (context 0, context 1) floats 2k, 2k+1.
+// ---------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(4))) const f2 cf2;
+
+struct PairProj {
+    f2 p0, p1, p2;  // K_ref (R X + t)
+    f2 iz;          // 1 / clamp(p2, 1e-5)
+    f2 ix, iy;      // sampling position in pixels
+};
+
+struct CamPair {
+    float Ki[9];   // K^-1 of the target (both halves of the record hold it)
+    f2 Kr[9], T[12];
+    float wm1, rwm1, hm1, rhm1;
+
+    __device__ __forceinline__ void load(cf2* rec, int H, int W) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Ki[i] = rec[i].x;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Kr[i] = rec[9 + i];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) T[i] = rec[18 + i];
+        wm1 = (float)(W - 1);
+        hm1 = (float)(H - 1);
+        rwm1 = rcp_nr(wm1);
+        rhm1 = rcp_nr(hm1);
+    }
+    __device__ __forceinline__ Lift lift(float u, float v, float d) const { return psfm::lift(Ki, u, v, d); }
+    // p = K_ref (R X + t), z = clamp(p2, 1e-5), iz = 1/z (rcp + one Newton step)
+    __device__ __forceinline__ void transform(const Lift& l, PairProj& r) const {
+        const f2 X0 = bc(l.X0), X1 = bc(l.X1), X2 = bc(l.X2);
+        const f2 c0 = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[3];
+        const f2 c1 = T[4] * X0 + T[5] * X1 + T[6] * X2 + T[7];
+        const f2 c2 = T[8] * X0 + T[9] * X1 + T[10] * X2 + T[11];
+        r.p0 = Kr[0] * c0 + Kr[1] * c1 + Kr[2] * c2;
+        r.p1 = Kr[3] * c0 + Kr[4] * c1 + Kr[5] * c2;
+        r.p2 = Kr[6] * c0 + Kr[7] * c1 + Kr[8] * c2;
+        const f2 z = f2{fmaxf(r.p2.x, 1e-5f), fmaxf(r.p2.y, 1e-5f)};
+        const f2 r0 = f2{__builtin_amdgcn_rcpf(z.x), __builtin_amdgcn_rcpf(z.y)};
+        r.iz = (f2{1.0f, 1.0f} - z * r0) * r0 + r0;
+    }
+    // + the sampling position: u = p0 / z (rcp-refined quotient), then ((2u/(W-1) - 1) + 1)/2 (W-1)
+    __device__ __forceinline__ void project(const Lift& l, PairProj& r) const {
+        transform(l, r);
+        const f2 z = f2{fmaxf(r.p2.x, 1e-5f), fmaxf(r.p2.y, 1e-5f)};
+        f2 u = r.p0 * r.iz, w = r.p1 * r.iz;
+        u = (r.p0 - u * z) * r.iz + u;
+        w = (r.p1 - w * z) * r.iz + w;
+        r.ix = roundtrip(u, wm1, rwm1);
+        r.iy = roundtrip(w, hm1, rhm1);
+    }
+    __device__ __forceinline__ static f2 roundtrip(f2 pz, float sm1, float rsm1) {
+        const f2 t = pz + pz;
+        f2 q = t * bc(rsm1);
+        q = (t - q * bc(sm1)) * bc(rsm1) + q;
+        const f2 n = q - f2{1.0f, 1.0f};
+        return ((n + f2{1.0f, 1.0f}) * f2{0.5f, 0.5f}) * bc(sm1);
+    }
+    // adjoint: (dL/dix, dL/diy) -> dL/dc (gc) and dL/d(depth) (returned), both contexts
+    __device__ __forceinline__ f2 grad(const PairProj& r, const Lift& l, f2 gix, f2 giy, f2 (&gc)[3]) const {
+        const f2 gp0 = gix * r.iz, gp1 = giy * r.iz;
+        const f2 t = -(gix * r.p0 + giy * r.p1) * (r.iz * r.iz);
+        const f2 gp2 = f2{r.p2.x >= 1e-5f ? t.x : 0.0f, r.p2.y >= 1e-5f ? t.y : 0.0f};
+        gc[0] = Kr[0] * gp0 + Kr[3] * gp1 + Kr[6] * gp2;
+        gc[1] = Kr[1] * gp0 + Kr[4] * gp1 + Kr[7] * gp2;
+        gc[2] = Kr[2] * gp0 + Kr[5] * gp1 + Kr[8] * gp2;
+        const f2 gX0 = T[0] * gc[0] + T[4] * gc[1] + T[8] * gc[2];
+        const f2 gX1 = T[1] * gc[0] + T[5] * gc[1] + T[9] * gc[2];
+        const f2 gX2 = T[2] * gc[0] + T[6] * gc[1] + T[10] * gc[2];
+        return gX0 * bc(l.xn0) + gX1 * bc(l.xn1) + gX2 * bc(l.xn2);
+    }
+};
 
 __device__ __forceinline__ f2 pk_rcp(f2 v) { return f2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)}; }
 __device__ __forceinline__ f2 pk_sel01(f2 l) {  // 1 where 0 <= l <= 1 (clamp pass-through), else 0
@@ -208,7 +272,7 @@ __device__ __forceinline__ f2 photo_grad_pair(const f2 (&xa)[3], const f2 (&xb)[
 
 template <int NC>
 struct State {
-    static constexpr int NP = (NC + 1) / 2;
+    static constexpr int NP = 1;
     // four row slots as separate members (compile-time slot selection; no indexed aggregate
     // that could be demoted to scratch)
     float Y0[3], Y1[3], Y2[3], Y3[3];
@@ -225,21 +289,20 @@ struct State {
     template <int I> __device__ __forceinline__ f2 (&X())[NP][3] {
         if constexpr (I == 0) return X0; else if constexpr (I == 1) return X1; else if constexpr (I == 2) return X2; else return X3;
     }
-    // dL/d(warped sample) per channel (context pairs packed) of the q-rows a p-row touches:
+    // dL/d(warped sample) per channel (the contexts packed) of the q-rows a p-row touches:
     // D0 = row p-1 (completed by this p-row), D1 = row p, D2 = row p+1
     f2 D0[NP][3], D1[NP][3], D2[NP][3];
     float h_p, h_n;           // smoothness x-term sgn(s - s_right) w of p-row q / this p-row
     float t_pp, t_p, t_n;     // y-term sgn(s - s_below) w of p-rows q-1, q, this p-row
     float acc_photo, acc_ax, acc_ay, acc_m;
-#if PSFM_K12_GT_REG
-    float gT[NC][12];
-#endif
 };
 
 template <int NC, bool FAST, int MODEL>
 struct K12 {
+    static_assert(NC == 1 || NC == 2, "K12: one context pair (N <= 2, fused_ok)");
+    static constexpr bool PAIR_CAM = MODEL == PSFM_CAM_PINHOLE;  // packed pinhole projection
     using CM = Cams<NC, MODEL>;
-    static constexpr int NP = (NC + 1) / 2;
+    static constexpr int NP = 1;
     const Args& a;
     const psfm_params& p;
     Cfg<FAST> cfg;
@@ -255,20 +318,26 @@ struct K12 {
     const float* thr;
     const float* mask;
     float* gsig;
-    float* di;  // wave-private LDS [3][NC*6][64]
-    float* gt;  // (PSFM_K12_GT_REG=0) this lane's dL/dT accumulators: gt[j*12 + m], 16-B aligned
-    const float* camrec;  // record of (s, context 0, b); context j is j*B records further
+    f2* di;      // wave-private LDS [3][6][64] f2
+    float* gt;   // this lane's dL/dT accumulators: gt[2 m + j] (entry m, context j), 16-B aligned
+    const float* camrec;   // record of (s, context 0, b); context j is j*B records further
+    const float* campair;  // context-paired record of (s, b) (ws.cam_pairs)
 
-    // The 51 camera scalars are re-loaded at each use (s_load through the constant address
-    // space: scalar cache, no VGPRs) instead of being held in SGPRs for the whole sweep; the
-    // laundered pointer stops the compiler from keeping them live across the SSIM phase.
+    // Camera scalars are re-loaded at each use (s_load through the constant address space:
+    // scalar cache, no VGPRs) instead of being held in SGPRs for the whole sweep; the laundered
+    // pointer stops the compiler from keeping them live across the SSIM phase.
     __device__ __forceinline__ CM load_cams() const {
         uint64_t rp = reinterpret_cast<uint64_t>(camrec);
-#if PSFM_K12_CAM_RELOAD
         asm volatile("" : "+s"(rp));
-#endif
         CM c;
         c.load(reinterpret_cast<cfloat*>(rp), B, H, W);
+        return c;
+    }
+    __device__ __forceinline__ CamPair load_pair() const {
+        uint64_t rp = reinterpret_cast<uint64_t>(campair);
+        asm volatile("" : "+s"(rp));
+        CamPair c;
+        c.load(reinterpret_cast<cf2*>(rp), H, W);
         return c;
     }
 
@@ -313,15 +382,15 @@ struct K12 {
         thr = (cfg.clip()) ? a.ws.clip_thr + (size_t)s * (cfg.automask() ? 2 * NC : NC) : nullptr;
         mask = (!FAST && a.in.mask) ? a.in.mask + (size_t)b * plane : nullptr;
         gsig = pick4(a.grad_sig, s) + (size_t)b * plane;
-        di = lds;
-        gt = lds + 3 * 6 * NC * 64 + lane * gt_stride(NC);
+        di = reinterpret_cast<f2*>(lds);
+        gt = lds + 3 * 6 * 64 * 2 + lane * GTS;
         camrec = a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC;
+        campair = a.ws.cam_pairs + ((size_t)s * B + b) * 2 * PSFM_CAMREC;
         // per-image mean of the sigmoid map (smoothness normaliser, utils/depth.py:183-185),
         // from the SIGCH chunk sums of the pre-pass, summed in chunk order in fp64 (wave-uniform
         // scalar loads: written by the previous launch, read-only here)
         mc = 1.0f;
         if (cfg.smooth()) {
-            typedef __attribute__((address_space(4))) const float cfloat;
             cfloat* sp = reinterpret_cast<cfloat*>(reinterpret_cast<uint64_t>(a.ws.sig_part) +
                                                    (((size_t)s * B + b) * SIGCH) * sizeof(float));
             double v = 0.0;
@@ -331,41 +400,16 @@ struct K12 {
         }
     }
 
-    // d warp / d(ix, iy) of a row slot: [slot][m][64] (b32, conflict-free) or, with
-    // PSFM_K12_DI_B128, [slot][lane][6 NC] (b128: a quarter of the LDS instructions)
-    __device__ __forceinline__ void di_store(int slot, const float (&dv)[NC * 6]) const {
-#if PSFM_K12_DI_B128
-        float4* d4 = reinterpret_cast<float4*>(di + (slot * 64 + lane) * (NC * 6));
+    // d warp / d(ix, iy) of a row slot, both contexts: [slot][m][64] f2 (b64, conflict-free)
+    __device__ __forceinline__ void di_store(int slot, const f2 (&dv)[6]) const {
+        f2* ds = di + slot * (6 * 64);
 #pragma unroll
-        for (int i = 0; i < NC * 6 / 4; ++i) d4[i] = make_float4(dv[4 * i], dv[4 * i + 1], dv[4 * i + 2], dv[4 * i + 3]);
-        if ((NC * 6) % 4) {
-            float2* d2 = reinterpret_cast<float2*>(di + (slot * 64 + lane) * (NC * 6) + (NC * 6 / 4) * 4);
-            d2[0] = make_float2(dv[NC * 6 - 2], dv[NC * 6 - 1]);
-        }
-#else
-        float* ds = di + slot * (NC * 6 * 64);
-#pragma unroll
-        for (int m = 0; m < NC * 6; ++m) ds[m * 64 + lane] = dv[m];
-#endif
+        for (int m = 0; m < 6; ++m) ds[m * 64 + lane] = dv[m];
     }
-    __device__ __forceinline__ void di_load(int slot, float (&dv)[NC * 6]) const {
-#if PSFM_K12_DI_B128
-        const float4* d4 = reinterpret_cast<const float4*>(di + (slot * 64 + lane) * (NC * 6));
+    __device__ __forceinline__ void di_load(int slot, f2 (&dv)[6]) const {
+        const f2* ds = di + slot * (6 * 64);
 #pragma unroll
-        for (int i = 0; i < NC * 6 / 4; ++i) {
-            const float4 t = d4[i];
-            dv[4 * i] = t.x; dv[4 * i + 1] = t.y; dv[4 * i + 2] = t.z; dv[4 * i + 3] = t.w;
-        }
-        if ((NC * 6) % 4) {
-            const float2 t = reinterpret_cast<const float2*>(di + (slot * 64 + lane) * (NC * 6) + (NC * 6 / 4) * 4)[0];
-            dv[NC * 6 - 2] = t.x;
-            dv[NC * 6 - 1] = t.y;
-        }
-#else
-        const float* ds = di + slot * (NC * 6 * 64);
-#pragma unroll
-        for (int m = 0; m < NC * 6; ++m) dv[m] = ds[m * 64 + lane];
-#endif
+        for (int m = 0; m < 6; ++m) dv[m] = ds[m * 64 + lane];
     }
 
     // the sigmoid at full-resolution row v, this lane's column: nearest upsampling of the stored
@@ -398,20 +442,25 @@ struct K12 {
             const uint32_t pix = (uint32_t)(r * W + colr);
 #pragma unroll
             for (int c = 0; c < 3; ++c) S.template Y<I>()[c] = tgt[c * plane + pix];
-            const CM cams = load_cams();
             float d1, inv;
             const float d = dc.warp_depth(sg, d1, inv);
-            const Lift l = cams.lift((float)colr, (float)r, d);
+            if constexpr (PAIR_CAM) {
+                const CamPair cams = load_pair();
+                PairProj pr;
+                cams.project(cams.lift((float)colr, (float)r, d), pr);
+                gather(ctx[0], pb, pr.ix.x, pr.iy.x, H, W, pd[0]);
+                if (NC == 2) gather(ctx[NC - 1], pb, pr.ix.y, pr.iy.y, H, W, pd[NC - 1]);
+            } else {
+                const CM cams = load_cams();
+                const Lift l = cams.lift((float)colr, (float)r, d);
 #pragma unroll
-            for (int j = 0; j < NC; ++j) {
-                typename CM::P pr;
-                cams.project(j, l, pr);
-                gather(ctx[j], pb, pr.ix, pr.iy, H, W, pd[j]);
+                for (int j = 0; j < NC; ++j) {
+                    typename CM::P pr;
+                    cams.project(j, l, pr);
+                    gather(ctx[j], pb, pr.ix, pr.iy, H, W, pd[j]);
+                }
             }
         }
-#ifdef PSFM_K12_NOPIPE
-        if (LOAD) resolve_row<I>(S, k, pd);
-#endif
         PSFM_PHASE();
         if (PEVAL) peval<IA, IB, IC>(S, v - 2);
         PSFM_PHASE();
@@ -422,39 +471,28 @@ struct K12 {
             S.t_p = S.t_n;
             S.h_p = S.h_n;
 #pragma unroll
-            for (int q = 0; q < NP; ++q)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    S.D0[q][c] = S.D1[q][c];
-                    S.D1[q][c] = S.D2[q][c];
-                }
+            for (int c = 0; c < 3; ++c) {
+                S.D0[0][c] = S.D1[0][c];
+                S.D1[0][c] = S.D2[0][c];
+            }
         }
-#ifndef PSFM_K12_NOPIPE
         if (LOAD) resolve_row<I>(S, k, pd);
-#endif
     }
 
+    // the bilinear samples of the issued row (the duplicate context of NC = 1 is computed in the
+    // high half and never read)
     template <int I>
     __device__ __forceinline__ void resolve_row(State<NC>& S, int k, const Pend (&pd)[NC]) const {
-        {
-            float dv[NC * 6];
+        f2 x[3], dix[3], diy[3];
+        resolve_pair(pd[0], pd[NC - 1], x, dix, diy);
+        f2 dv[6];
 #pragma unroll
-            for (int j = 0; j < NC; ++j) {
-                float x[3], dix[3], diy[3];
-                resolve(pd[j], x, dix, diy);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    S.template X<I>()[j >> 1][c][j & 1] = x[c];
-                    dv[j * 6 + c] = dix[c];
-                    dv[j * 6 + 3 + c] = diy[c];
-                }
-            }
-            di_store(k % 3, dv);
-            if (NC & 1) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) S.template X<I>()[NP - 1][c].y = S.template X<I>()[NP - 1][c].x;
-            }
+        for (int c = 0; c < 3; ++c) {
+            S.template X<I>()[0][c] = x[c];
+            dv[c] = dix[c];
+            dv[3 + c] = diy[c];
         }
+        di_store(k % 3, dv);
     }
 
     // p-row pv from slots IA (pv-1), IB (pv), IC (pv+1)
@@ -586,71 +624,78 @@ struct K12 {
     __device__ __forceinline__ void qeval(State<NC>& S, int qv, int k) const {
         const float h_left = cfg.smooth() ? from_prev(S.h_p) : 0.0f;  // cross-lane
         if (qv >= H || qv >= y0 + RB || !qcol) return;
-        float dv[NC * 6];
+        f2 dv[6];
         di_load(k % 3, dv);
-        const CM cams = load_cams();
+        // dL/d(ix, iy) of both contexts: the channels' dL/dx through d warp / d(ix, iy)
+        f2 gix = S.D0[0][0] * dv[0], giy = S.D0[0][0] * dv[3];
+#pragma unroll
+        for (int c = 1; c < 3; ++c) {
+            gix += S.D0[0][c] * dv[c];
+            giy += S.D0[0][c] * dv[3 + c];
+        }
         float d1, inv;
         const float d = dc.warp_depth(S.template SG<IQ>(), d1, inv);
         const float dw = dc.dwarp_ds(d, d1, inv);
-        const Lift l = cams.lift((float)col, (float)qv, d);
-        float gs = 0.0f;
+        float gs;
+        f2* g2 = reinterpret_cast<f2*>(gt);   // entry m of both contexts
+        if constexpr (PAIR_CAM) {
+            const CamPair cams = load_pair();
+            const Lift l = cams.lift((float)col, (float)qv, d);
+            PairProj pr;
+            cams.transform(l, pr);
+            f2 gc[3];
+            const f2 gd = cams.grad(pr, l, gix, giy, gc);
+            gs = (NC == 2 ? gd.x + gd.y : gd.x) * dw;
+            // dL/dT += gc (X, 1)^T for both contexts: lane-private LDS row, b128 read-modify-write
+            float4* g4 = reinterpret_cast<float4*>(gt);
+            const f2 X0 = bc(l.X0), X1 = bc(l.X1), X2 = bc(l.X2);
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const int q = j >> 1;
-            float gix = 0.0f, giy = 0.0f;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float dx = (j & 1) ? S.D0[q][c].y : S.D0[q][c].x;
-                gix += dx * dv[j * 6 + c];
-                giy += dx * dv[j * 6 + 3 + c];
+            for (int i = 0; i < 3; ++i) {
+                const float4 ta = g4[2 * i], tb = g4[2 * i + 1];
+                f2 e0 = f2{ta.x, ta.y}, e1 = f2{ta.z, ta.w}, e2 = f2{tb.x, tb.y}, e3 = f2{tb.z, tb.w};
+                e0 += gc[i] * X0;
+                e1 += gc[i] * X1;
+                e2 += gc[i] * X2;
+                e3 += gc[i];
+                g4[2 * i] = make_float4(e0.x, e0.y, e1.x, e1.y);
+                g4[2 * i + 1] = make_float4(e2.x, e2.y, e3.x, e3.y);
             }
-            typename CM::P pr;
-            cams.project(j, l, pr);
-            float gc[3];
-            gs += cams.grad(j, pr, gix, giy, gc) * dw;
-#if PSFM_K12_GT_REG
-            acc_gT(S.gT[j], gc, pr);
-#else
-            {  // lane-private LDS row: 3 x b128 read-modify-write
-                float4* g4 = reinterpret_cast<float4*>(gt + j * 12);
-                float g[12];
+        } else {
+            const CM cams = load_cams();
+            const Lift l = cams.lift((float)col, (float)qv, d);
+            gs = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                typename CM::P pr;
+                cams.project(j, l, pr);
+                float gc[3];
+                gs += cams.grad(j, pr, j ? gix.y : gix.x, j ? giy.y : giy.x, gc) * dw;
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    const float4 t = g4[i];
-                    g[4 * i] = t.x; g[4 * i + 1] = t.y; g[4 * i + 2] = t.z; g[4 * i + 3] = t.w;
+                    gt[2 * (4 * i + 0) + j] += gc[i] * pr.X0;
+                    gt[2 * (4 * i + 1) + j] += gc[i] * pr.X1;
+                    gt[2 * (4 * i + 2) + j] += gc[i] * pr.X2;
+                    gt[2 * (4 * i + 3) + j] += gc[i];
                 }
-                acc_gT(g, gc, pr);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) g4[i] = make_float4(g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]);
             }
-#endif
         }
+        (void)g2;
         if (cfg.smooth()) gs += (cx * (S.h_p - h_left) + cy * (S.t_p - S.t_pp)) / mc;
         gsig[(uint32_t)(qv * W + col)] = gs;
     }
 };
 
 template <int NC, bool FAST, int MODEL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSFM_K12_WAVES))) void k12_fwd_grad(Args a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) void k12_fwd_grad(Args a) {
     extern __shared__ __attribute__((aligned(16))) float k12_lds[];
     const K12<NC, FAST, MODEL> K(a, k12_lds);
-    constexpr int NP = (NC + 1) / 2;
     State<NC> S;
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;
     S.h_p = S.h_n = S.t_pp = S.t_p = S.t_n = 0.0f;
 #pragma unroll
-    for (int q = 0; q < NP; ++q)
+    for (int c = 0; c < 3; ++c) S.D0[0][c] = S.D1[0][c] = S.D2[0][c] = f2{0.0f, 0.0f};
 #pragma unroll
-        for (int c = 0; c < 3; ++c) S.D0[q][c] = S.D1[q][c] = S.D2[q][c] = f2{0.0f, 0.0f};
-#if PSFM_K12_GT_REG
-#pragma unroll
-    for (int j = 0; j < NC; ++j)
-#pragma unroll
-        for (int m = 0; m < 12; ++m) S.gT[j][m] = 0.0f;
-#else
-#pragma unroll
-    for (int m = 0; m < 12 * NC; ++m) K.gt[m] = 0.0f;
-#endif
+    for (int m = 0; m < 24; ++m) K.gt[m] = 0.0f;
     // rows y0-2 .. y0+RB+1 issued at k = 0 .. RB+3; p-rows y0-1 .. y0+RB at k = 3 .. RB+4;
     // q-rows y0 .. y0+RB-1 at k = 5 .. RB+4 (the last step's issue is a harmless extra row)
     S.sg_next = K.load_sig(K.y0 - 2);
@@ -686,11 +731,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PSFM_K12_WAV
         float* o = a.ws.pose_part + ((((size_t)K.s * NC + j) * p.B + K.b) * nu + K.unit) * 12;
 #pragma unroll
         for (int mm = 0; mm < 12; ++mm) {
-#if PSFM_K12_GT_REG
-            const float t = wave_sum64(S.gT[j][mm]);
-#else
-            const float t = wave_sum64(K.gt[j * 12 + mm]);
-#endif
+            const float t = wave_sum64(K.gt[2 * mm + j]);
             if (threadIdx.x == 0) o[mm] = t;
         }
     }

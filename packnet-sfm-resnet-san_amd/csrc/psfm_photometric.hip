@@ -767,7 +767,9 @@ struct SigSumArgs {
     const float* sig[MAXS];
     int shift[MAXS];
     float* part;  // [S][B][SIGCH]
-    int B, W;
+    const float* cam;  // [S][N][B][CAMREC]
+    float* cam_pairs;  // [S][B][CAMREC][2]
+    int B, W, N, smooth;
     uint32_t plane;
 };
 
@@ -777,6 +779,12 @@ struct SigSumArgs {
 __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
     __shared__ float red[NWAVE];
     const int ch = blockIdx.x, b = blockIdx.y, s = blockIdx.z;
+    if (ch == 0 && threadIdx.x < 2 * PSFM_CAMREC) {  // K12's context-paired camera record of (s, b)
+        const int k = threadIdx.x >> 1, j = min((int)(threadIdx.x & 1), a.N - 1);
+        a.cam_pairs[((size_t)s * a.B + b) * 2 * PSFM_CAMREC + threadIdx.x] =
+            a.cam[(((size_t)s * a.N + j) * a.B + b) * PSFM_CAMREC + k];
+    }
+    if (!a.smooth) return;
     const int sh = pick4(a.shift, s);
     const uint32_t per = (a.plane + fused::SIGCH - 1) / fused::SIGCH;
     const uint32_t lo = ch * per, hi = min(a.plane, lo + per);
@@ -1036,7 +1044,7 @@ int psfm_tiles_per_image(int H, int W) { return tiles_img(H, W); }
 
 int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, size_t* clip,
                           size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp,
-                          size_t* sig_part) {
+                          size_t* sig_part, size_t* cam_pairs) {
     if (!p) return fail(-1, "null params");
     const int u = std::max(std::max(tiles_img(p->H, p->W), fused::units(p->H, p->W)),
                            std::max(sweep::k1_units(p->H, p->W), sweep::k2_units(p->H, p->W)));
@@ -1050,6 +1058,7 @@ int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, s
     if (argmin_bytes) *argmin_bytes = (size_t)p->S * p->B * p->H * p->W;
     if (unwarp) *unwarp = (p->automask && !p->l1_only) ? (size_t)p->N * p->B * p->H * p->W : 0;
     if (sig_part) *sig_part = (size_t)p->S * p->B * fused::SIGCH;
+    if (cam_pairs) *cam_pairs = (size_t)p->S * p->B * PSFM_CAMREC * 2;
     return 0;
 }
 
@@ -1261,20 +1270,25 @@ int psfm_photometric_prepass(const psfm_params* p, const psfm_inputs* in, const 
     if (!fused_ok(p)) return fail(-15, "prepass/fwd_grad need ssim_loss_weight > 0 and N <= 2 (use fwd + bwd)");
     if (!ws) return fail(-12, "null workspace");
     if (p->smooth_w > 0.0f && !ws->sig_part) return fail(-12, "null sig_part workspace");
+    if (!ws->cam_pairs) return fail(-12, "null cam_pairs workspace");
     if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
     hipStream_t st = (hipStream_t)stream;
     if (p->automask && !(p->clip_loss > 0.0f)) launch_k0(p, sweep_args(p, in, ws), st);  // clip: clip_stats did
-    if (p->smooth_w > 0.0f) {
+    {  // sigmoid chunk sums (smoothness normaliser) + the context-paired camera records
         SigSumArgs sa{};
         for (int s = 0; s < p->S; ++s) {
             sa.sig[s] = in->sig[s];
             sa.shift[s] = p->sig_shift[s];
         }
         sa.part = ws->sig_part;
+        sa.cam = in->cam;
+        sa.cam_pairs = ws->cam_pairs;
         sa.B = p->B;
         sa.W = p->W;
+        sa.N = p->N;
+        sa.smooth = p->smooth_w > 0.0f;
         sa.plane = (uint32_t)(p->H * p->W);
-        hipLaunchKernelGGL(k_sig_sum, dim3(fused::SIGCH, p->B, p->S), dim3(NT), 0, st, sa);
+        hipLaunchKernelGGL(k_sig_sum, dim3(sa.smooth ? fused::SIGCH : 1, p->B, p->S), dim3(NT), 0, st, sa);
     }
     PSFM_LAUNCH_CHECK();
     return 0;
@@ -1287,6 +1301,7 @@ int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const
     if (!p->grad_fused) return fail(-15, "fwd_grad needs p->grad_fused = 1 (finalize reads its unit grid)");
     if (!ws || !ws->photo_part || !ws->pose_part) return fail(-12, "null workspace");
     if (p->smooth_w > 0.0f && (!ws->smooth_part || !ws->sig_part)) return fail(-12, "null smoothness workspace");
+    if (!ws->cam_pairs) return fail(-12, "null cam_pairs workspace (written by psfm_photometric_prepass)");
     if (p->automask && !ws->unwarp) return fail(-12, "automask needs ws->unwarp");
     if (p->clip_loss > 0.0f && !ws->clip_thr) return fail(-12, "clip needs clip_thr");
     if (!grad_sig) return fail(-14, "null grad_sig");

@@ -118,10 +118,10 @@ class _Call:
         inp.mask = mask.data_ptr() if mask is not None else None
         self.inputs = inp
         # workspace (caller-owned; sized by the library)
-        n = [ctypes.c_size_t() for _ in range(8)]
+        n = [ctypes.c_size_t() for _ in range(9)]
         _hip.check(_hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]),
                    "psfm_workspace_floats")
-        sizes = [x.value for x in n[:5]] + [n[6].value, n[7].value]
+        sizes = [x.value for x in n[:5]] + [n[6].value, n[7].value, n[8].value]
         total = sum(sizes)
         self.fbuf = torch.empty(total, device=image.device, dtype=torch.float32)
         self.abuf = torch.empty(max(n[5].value, 1), device=image.device, dtype=torch.uint8)
@@ -129,7 +129,7 @@ class _Call:
         off = 0
         base = self.fbuf.data_ptr()
         for name, sz in zip(("photo_part", "smooth_part", "clip_part", "clip_thr", "pose_part", "unwarp",
-                             "sig_part"), sizes):
+                             "sig_part", "cam_pairs"), sizes):
             setattr(ws, name, base + 4 * off if sz else None)
             off += sz
         ws.argmin = self.abuf.data_ptr()

@@ -37,7 +37,7 @@ def test_every_declared_symbol_is_exported(hip):
 
 def test_workspace_sizes(hip):
     p = hip.Params(B=4, H=192, W=640, N=2, S=4, scale0=0, n_scales=4, automask=1, reduce_op=0)
-    n = [ctypes.c_size_t() for _ in range(8)]
+    n = [ctypes.c_size_t() for _ in range(9)]
     assert hip.lib().psfm_workspace_floats(ctypes.byref(p), *[ctypes.byref(x) for x in n]) == 0
     tiles = hip.tiles_per_image(192, 640)
     assert tiles == 10 * 48
@@ -46,6 +46,7 @@ def test_workspace_sizes(hip):
     assert n[5].value == 4 * 4 * 192 * 640
     assert n[6].value == 2 * 4 * 192 * 640
     assert n[7].value == 4 * 4 * 16   # sigmoid chunk sums of the K12 pre-pass
+    assert n[8].value == 4 * 4 * 32 * 2   # context-paired camera records (K12)
 
 
 def test_fused_path_argument_checks(hip):
