@@ -41,6 +41,7 @@ extern "C" {
 #define PSFM_ACT_NONE 0
 #define PSFM_ACT_RELU 1
 #define PSFM_ACT_SIGMOID 2
+#define PSFM_ACT_ELU 3     /* ELU(alpha = 1): GroupNorm only (PackNet Conv2D / ResidualConv) */
 
 /* fp32 workspace floats needed by a reduction over an [M, C] activation (bias_act_bwd,
  * bn_act_fwd / bn_act_bwd), and for groupnorm over [N, HW, C] with G groups. */
@@ -70,18 +71,22 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, int* counter, void* stream);
 
-/* GroupNorm(G) over (x + bias) (+ ReLU) per sample: x bf16 [N, HW, C], conv bias bf16/fp32 [C],
- * gamma/beta fp32 [C] (PoseNet.py:15-19 conv_gn).  save_mean / save_invstd [N*G]. */
-int psfm_gn_act_fwd(const void* x, const void* bias, int bias_bf16, const float* gamma, const float* beta,
-                    float eps, int N, int HW, int C, int G, int relu, void* y, float* save_mean,
+/* y = act(GroupNorm(G)(x [+ res] + bias)) per sample: x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
+ * or NULL, gamma/beta fp32 [C], act PSFM_ACT_NONE / RELU / ELU.  PoseNet conv_gn (conv + GN + ReLU,
+ * PoseNet.py:15-19); PackNet Conv2D (conv + GN(16) + ELU, layers01.py:10-37) and ResidualConv's
+ * GN(conv2 + shortcut) + ELU (res = the conv2 branch, layers01.py:40-61).  save_mean / save_invstd
+ * [N*G]. */
+int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
+                    const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
                     float* save_invstd, float* ws, int* counter, void* stream);
 
-/* Backward of psfm_gn_act_fwd: dx (bf16), dbias (bias dtype; the column sum of the stored dx, as
- * autograd forms a conv bias gradient), dgamma / dbeta (fp32 [C]).  `counter` spans two slots. */
-int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bias, int bias_bf16,
+/* Backward of psfm_gn_act_fwd: dx (bf16) and, with res, dres (a second copy: both inputs are summed),
+ * dbias (bias dtype; the column sum of the stored dx, as autograd forms a conv bias gradient; NULL
+ * with bias NULL), dgamma / dbeta (fp32 [C]).  `counter` spans two slots. */
+int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* res, const void* bias, int bias_bf16,
                     const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C,
-                    int G, int relu, void* dx, void* dbias, float* dgamma, float* dbeta, float* ws, int* counter,
-                    void* stream);
+                    int G, int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta, float* ws,
+                    int* counter, void* stream);
 
 const char* psfm_netops_last_error(void);
 

@@ -38,19 +38,10 @@ int fail(int code, const char* msg) {
         }                                                            \
     } while (0)
 
-#ifndef NETOPS_U
-#define NETOPS_U 4
-#endif
-#ifndef NETOPS_TARGET_BLOCKS
-#define NETOPS_TARGET_BLOCKS 512
-#endif
-#ifndef NETOPS_GS
-#define NETOPS_GS 16
-#endif
 constexpr int NT = 256;           // threads per workgroup
-constexpr int U = NETOPS_U;       // row steps unrolled (independent loads in flight per thread)
-constexpr int TARGET_BLOCKS = NETOPS_TARGET_BLOCKS;
-constexpr int GS = NETOPS_GS;     // workgroups per reduction group (ngroups)
+constexpr int U = 4;              // row steps unrolled (independent loads in flight per thread)
+constexpr int TARGET_BLOCKS = 512;
+constexpr int GS = 16;     // workgroups per reduction group (ngroups)
 constexpr int MAX_KC = 1024;      // widest partial row (BN: 2*C, C <= 512)
 constexpr int CTR = PSFM_NETOPS_COUNTER_INTS;
 
@@ -106,6 +97,14 @@ __device__ __forceinline__ void st_bf(uint16_t* __restrict__ p, const Vec<VEC>& 
 #pragma unroll
         for (int i = 0; i < VEC; ++i) p[i] = f2bf(a.v[i]);
     }
+}
+
+// v += the bf16 vector at p (the residual input of a fused GroupNorm)
+template <int VEC>
+__device__ __forceinline__ void add_bf(Vec<VEC>& v, const uint16_t* __restrict__ p) {
+    const Vec<VEC> r = ld_bf<VEC>(p);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v.v[i] += r.v[i];
 }
 
 template <int VEC>
@@ -306,9 +305,6 @@ __device__ void sum_rows(const T* src, int nrows, int KC, double* fin, double* s
 // Returns true in the single workgroup that finishes the segment; fin = column totals.
 __device__ bool tree_reduce(float* rows, double* grp, int* ctr, int b, int nblk, int KC, double* fin,
                             double* scratch) {
-#ifdef NETOPS_NO_TREE  // timing experiment only: the streaming cost without the reduction tail
-    return false;
-#endif
     const int g = b / GS, ng = ngroups(nblk);
     const int n_in = min(GS, nblk - g * GS);
     if (!arrive(ctr + 1 + g, n_in)) return false;
@@ -654,12 +650,26 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// GroupNorm(NG) of (x + bias) + ReLU, per sample n over rows [n*HW, (n+1)*HW).  Each sample is
+// GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW).  Each sample is
 // its own reduction segment (bpn workgroups, counters at counter + n*(1+ngroups(bpn))).
 // ------------------------------------------------------------------------------------------
+// GroupNorm activations: ReLU (PoseNet conv_gn) or ELU(alpha = 1) (PackNet Conv2D / ResidualConv,
+// layers01.py:10-37, :40-61: x > 0 ? x : expm1(x); backward from the result: y > 0 ? g : g (y + 1))
+__device__ __forceinline__ float gn_act_f(float w, int act) {
+    if (act == PSFM_ACT_RELU) return fmaxf(w, 0.0f);
+    if (act == PSFM_ACT_ELU) return w > 0.0f ? w : expm1f(w);
+    return w;
+}
+__device__ __forceinline__ float gn_act_g(float g, float y, int act) {
+    if (act == PSFM_ACT_RELU) return y > 0.0f ? g : 0.0f;
+    if (act == PSFM_ACT_ELU) return y > 0.0f ? g : g * (y + 1.0f);
+    return g;
+}
+
 struct GNArgs {
     const uint16_t* x;
-    const void* bias;
+    const uint16_t* res;  // optional second input summed with x (PackNet ResidualConv)
+    const void* bias;     // optional (null = 0)
     const uint16_t* dy;
     const uint16_t* y;
     const float* gamma;
@@ -667,13 +677,14 @@ struct GNArgs {
     float* save_mean;    // [N*NG]
     float* save_invstd;  // [N*NG]
     uint16_t* out;
+    uint16_t* out2;       // backward: dres (a second copy of dx) when res is given
     void* dbias;
     float* dgamma;
     float* dbeta;
     float* ws;
     int* counter;
     float eps;
-    int N, HW, C, NG, relu, bias_bf16, G, TR, rpb, bpn;  // bpn: workgroups per sample
+    int N, HW, C, NG, act, bias_bf16, G, TR, rpb, bpn;  // act: PSFM_ACT_*; bpn: workgroups per sample
 };
 
 // workspace: stats tree [N segs][2C] | coef [N][3][C] | per-sample bwd rows [N][2C] fp64 |
@@ -704,8 +715,9 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
     if (r < a.TR) {
-        const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+        const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         const uint16_t* xs = a.x + (size_t)n * a.HW * a.C;
+        const uint16_t* rs = a.res ? a.res + (size_t)n * a.HW * a.C : nullptr;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
         ROW_LOOP_BEGIN(row0, row1, r, a.TR)
         Vec<VEC> v[U];
@@ -715,6 +727,7 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
             const int row = base_ + u * a.TR;
             in[u] = row < row1;
             v[u] = in[u] ? ld_bf<VEC>(xs + (size_t)row * a.C + c0) : zero<VEC>();
+            if (rs && in[u]) add_bf<VEC>(v[u], rs + (size_t)row * a.C + c0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -760,7 +773,7 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_apply(GNArgs a) {
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
     const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
     const Vec<VEC> sc = ld_f<VEC>(coef + c0), sh = ld_f<VEC>(coef + a.C + c0);
-    const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+    const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
     const size_t so = (size_t)n * a.HW * a.C;
     const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
     ROW_LOOP_BEGIN(row0, row1, r, a.TR)
@@ -769,6 +782,7 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_apply(GNArgs a) {
     for (int u = 0; u < U; ++u) {
         const int row = base_ + u * a.TR;
         v[u] = row < row1 ? ld_bf<VEC>(a.x + so + (size_t)row * a.C + c0) : zero<VEC>();
+        if (a.res && row < row1) add_bf<VEC>(v[u], a.res + so + (size_t)row * a.C + c0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -776,9 +790,7 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_apply(GNArgs a) {
         if (row >= row1) break;
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
-            float w = (v[u].v[i] + b.v[i]) * sc.v[i] + sh.v[i];
-            if (a.relu) w = fmaxf(w, 0.0f);
-            v[u].v[i] = w;
+            v[u].v[i] = gn_act_f((v[u].v[i] + b.v[i]) * sc.v[i] + sh.v[i], a.act);
         }
         st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, v[u]);
     }
@@ -802,7 +814,7 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
     if (r < a.TR) {
-        const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+        const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         float mu[VEC], is[VEC];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
@@ -819,14 +831,15 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
             const size_t o = so + (size_t)row * a.C + c0;
             const bool in = row < row1;
             g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+            if (a.act) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
             x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+            if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
+                const float gg = gn_act_g(g[u].v[i], y[u].v[i], a.act);
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
                 acc[0][i] += gg;
                 acc[1][i] += gg * xh;
@@ -882,7 +895,7 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
     if (r < a.TR) {
         const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
         const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
-        const Vec<VEC> b = ld_param<VEC>(a.bias, a.bias_bf16, c0);
+        const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         float mu[VEC], is[VEC];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
@@ -899,8 +912,9 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
             const size_t o = so + (size_t)row * a.C + c0;
             const bool in = row < row1;
             g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
+            if (a.act) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
             x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
+            if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -909,11 +923,12 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
             Vec<VEC> d;
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
+                const float gg = gn_act_g(g[u].v[i], y[u].v[i], a.act);
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
                 d.v[i] = k1.v[i] * gg - k2.v[i] - xh * k3.v[i];
             }
             st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, d);
+            if (a.out2) st_bf<VEC>(a.out2 + so + (size_t)row * a.C + c0, d);
 #pragma unroll
             for (int i = 0; i < VEC; ++i) acc[0][i] += bfround(d.v[i]);
         }
@@ -925,6 +940,7 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
     store_row<VEC, 1>(rows + (size_t)blockIdx.x * a.C, acc, a.C, c0, r);
     double* grp = reinterpret_cast<double*>(rows + tree_grp_off(1, nb, a.C));
     if (!tree_reduce(rows, grp, a.counter + CTR, blockIdx.x, nb, a.C, fin, scratch)) return;
+    if (!a.dbias) return;
     for (int c = t; c < a.C; c += NT) {
         if (a.bias_bf16)
             static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)fin[c]);
@@ -1198,20 +1214,22 @@ static int gn_setup(GNArgs& a, int N, int HW, int C, int G, Geo& g, int& vec) {
     return 0;
 }
 
-int psfm_gn_act_fwd(const void* x, const void* bias, int bias_bf16, const float* gamma, const float* beta, float eps,
-                    int N, int HW, int C, int G, int relu, void* y, float* save_mean, float* save_invstd, float* ws,
-                    int* counter, void* stream) {
-    if (!x || !bias || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || !counter)
+int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
+                    const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
+                    float* save_invstd, float* ws, int* counter, void* stream) {
+    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || !counter ||
+        (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU))
         return fail(-1, "gn_act_fwd: bad arguments");
     GNArgs a{};
     Geo g;
     int vec;
     if (int e = gn_setup(a, N, HW, C, G, g, vec)) return e;
     a.x = static_cast<const uint16_t*>(x);
+    a.res = static_cast<const uint16_t*>(res);
     a.bias = bias, a.bias_bf16 = bias_bf16, a.gamma = gamma, a.beta = beta, a.eps = eps;
     a.save_mean = save_mean, a.save_invstd = save_invstd;
     a.out = static_cast<uint16_t*>(y);
-    a.ws = ws, a.counter = counter, a.relu = relu;
+    a.ws = ws, a.counter = counter, a.act = act;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(N * g.nblk);
     if (vec == 8) {
@@ -1225,11 +1243,13 @@ int psfm_gn_act_fwd(const void* x, const void* bias, int bias_bf16, const float*
     return 0;
 }
 
-int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bias, int bias_bf16, const float* gamma,
-                    const float* save_mean, const float* save_invstd, int N, int HW, int C, int G, int relu, void* dx,
-                    void* dbias, float* dgamma, float* dbeta, float* ws, int* counter, void* stream) {
-    if (!dy || !x || !bias || !gamma || !save_mean || !save_invstd || !dx || !dbias || !dgamma || !dbeta || !ws ||
-        !counter || (relu && !y))
+int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* res, const void* bias, int bias_bf16,
+                    const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C, int G,
+                    int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta, float* ws, int* counter,
+                    void* stream) {
+    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
+        (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU) || (act && !y) || (res && !dres) ||
+        (bias && !dbias))
         return fail(-1, "gn_act_bwd: bad arguments");
     GNArgs a{};
     Geo g;
@@ -1238,10 +1258,12 @@ int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* bi
     a.dy = static_cast<const uint16_t*>(dy);
     a.y = static_cast<const uint16_t*>(y);
     a.x = static_cast<const uint16_t*>(x);
+    a.res = static_cast<const uint16_t*>(res);
     a.bias = bias, a.bias_bf16 = bias_bf16, a.gamma = gamma;
     a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
     a.out = static_cast<uint16_t*>(dx);
-    a.dbias = dbias, a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws, a.counter = counter, a.relu = relu;
+    a.out2 = static_cast<uint16_t*>(dres);
+    a.dbias = dbias, a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws, a.counter = counter, a.act = act;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(N * g.nblk);
     if (vec == 8) {

@@ -27,17 +27,8 @@
 namespace psfm {
 namespace sweep {
 
-#ifndef PSFM_K1_RB
-#define PSFM_K1_RB 13
-#endif
-#ifndef PSFM_K2_RB
-#define PSFM_K2_RB 24
-#endif
-#ifndef PSFM_XCD_REMAP
-#define PSFM_XCD_REMAP 1
-#endif
-constexpr int K1RB = PSFM_K1_RB;  // output rows per K0/K1 band
-constexpr int K2RB = PSFM_K2_RB;  // output rows per K2 band
+constexpr int K1RB = 13;  // output rows per K1 band (4m+1: 4-slot pipeline)
+constexpr int K2RB = 24;  // output rows per K2 band
 constexpr int K1W = 62;           // output columns per K1 stripe (halo 1)
 constexpr int K2W = 60;           // output columns per K2 stripe (halo 2)
 
@@ -46,15 +37,14 @@ __host__ __device__ inline int k2_stripes(int W) { return (W + K2W - 1) / K2W; }
 __host__ __device__ inline int k1_units(int H, int W) { return k1_stripes(W) * ((H + K1RB - 1) / K1RB); }
 __host__ __device__ inline int k2_units(int H, int W) { return k2_stripes(W) * ((H + K2RB - 1) / K2RB); }
 
-// Which (unit, batch, scale) this workgroup sweeps.  Grid = (units, B, S).  With PSFM_XCD_REMAP
-// the linear block id is re-dealt so that the blocks one XCD receives (round-robin dealing:
-// blocks i and i+8 share an XCD) form one contiguous run of (b, s, unit) -> one image's context
-// frames stay in that XCD's L2 (speed only: any placement is correct).
+// Which (unit, batch, scale) this workgroup sweeps.  Grid = (units, B, S).  The linear block id
+// is re-dealt so that the blocks one XCD receives (round-robin dealing: blocks i and i+8 share an
+// XCD) form one contiguous run of (b, s, unit) -> one image's context frames stay in that XCD's
+// L2 (speed only: any placement is correct).
 struct WorkItem {
     int unit, b, s;
 };
 __device__ __forceinline__ WorkItem work_item() {
-#if PSFM_XCD_REMAP
     const int units = gridDim.x, B = gridDim.y, S = gridDim.z;
     const int T = units * B * S;
     const int L = blockIdx.x + units * (blockIdx.y + B * blockIdx.z);
@@ -62,9 +52,6 @@ __device__ __forceinline__ WorkItem work_item() {
     const int w = xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
     const int bs = w / units;
     return WorkItem{w - bs * units, bs / S, bs % S};
-#else
-    return WorkItem{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-#endif
 }
 
 template <int I>

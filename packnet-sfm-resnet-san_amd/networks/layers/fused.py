@@ -166,8 +166,9 @@ def bn_act(x, bn, relu=True, residual=None):
 # ----------------------------------------------------------------------------------------------
 class _GNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, weight, beta, G, eps, relu, counter):
+    def forward(ctx, x, res, bias, weight, beta, G, eps, act, counter):
         x = _rows(x)
+        res = _rows(res.to(x.dtype)) if res is not None else None
         N, C, H, W = x.shape
         HW = H * W
         dev = x.device
@@ -176,45 +177,59 @@ class _GNAct(torch.autograd.Function):
         invstd = torch.empty(N * G, device=dev, dtype=torch.float32)
         L = _hip.lib()
         ws = torch.empty(L.psfm_gn_ws_floats(N, HW, C, G), device=dev, dtype=torch.float32)
-        bf = int(bias.dtype == torch.bfloat16)
-        _hip.check(L.psfm_gn_act_fwd(_hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight), _hip.ptr(beta),
-                                     ctypes.c_float(eps), N, HW, C, G, int(relu), _hip.ptr(y), _hip.ptr(mean),
+        bf = int(bias is not None and bias.dtype == torch.bfloat16)
+        _hip.check(L.psfm_gn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf, _hip.ptr(weight), _hip.ptr(beta),
+                                     ctypes.c_float(eps), N, HW, C, G, int(act), _hip.ptr(y), _hip.ptr(mean),
                                      _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
                    "psfm_gn_act_fwd")
-        ctx.save_for_backward(x, y, bias, weight, mean, invstd)
-        ctx.G, ctx.relu, ctx.counter = G, relu, counter
+        ctx.save_for_backward(x, res, y, bias, weight, mean, invstd)
+        ctx.G, ctx.act, ctx.counter = G, act, counter
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, bias, weight, mean, invstd = ctx.saved_tensors
+        x, res, y, bias, weight, mean, invstd = ctx.saved_tensors
         dy = _rows(dy.to(x.dtype))
         N, C, H, W = x.shape
         HW, G = H * W, ctx.G
         dev = x.device
         L = _hip.lib()
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dbias = torch.empty(C, device=dev, dtype=bias.dtype)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if res is not None else None
+        dbias = torch.empty(C, device=dev, dtype=bias.dtype) if bias is not None else None
         dw = torch.empty(C, device=dev, dtype=torch.float32)
         db = torch.empty(C, device=dev, dtype=torch.float32)
         ws = torch.empty(L.psfm_gn_ws_floats(N, HW, C, G), device=dev, dtype=torch.float32)
-        bf = int(bias.dtype == torch.bfloat16)
-        _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(weight),
-                                     _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.relu), _hip.ptr(dx),
-                                     _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws),
-                                     _slot(ctx.counter, BWD), _hip.stream(dev)), "psfm_gn_act_bwd")
-        return dx, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None
+        bf = int(bias is not None and bias.dtype == torch.bfloat16)
+        _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf,
+                                     _hip.ptr(weight), _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.act),
+                                     _hip.ptr(dx), _hip.ptr(dres), _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db),
+                                     _hip.ptr(ws), _slot(ctx.counter, BWD), _hip.stream(dev)), "psfm_gn_act_bwd")
+        return dx, dres, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None
 
 
-def gn_act(x, bias, gn, relu=True):
-    """act(groupnorm(x + bias)) with the reference's nn.GroupNorm module `gn`."""
-    if _fusable(x, "gn") and bias is not None and gn.affine and x.shape[1] % gn.num_groups == 0:
-        return _GNAct.apply(x, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), bool(relu),
+ACT_ELU = 3  # PSFM_ACT_ELU (GroupNorm only)
+
+
+def gn_act(x, bias, gn, relu=True, act=None, residual=None):
+    """act(groupnorm(x [+ residual] + bias)) with the reference's nn.GroupNorm module `gn`; act is
+    ReLU (relu=True, PoseNet) / none, or `act=ACT_ELU` (PackNet Conv2D / ResidualConv).  `bias`
+    may be None."""
+    act = (ACT_RELU if relu else ACT_NONE) if act is None else act
+    if (_fusable(x, "gn") and gn.affine and x.shape[1] % gn.num_groups == 0
+            and (residual is None or (residual.shape == x.shape and residual.device == x.device))):
+        return _GNAct.apply(x, residual, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), act,
                             _counter(gn, x.device))
+    if residual is not None:
+        x = x + residual
     if bias is not None:
         x = x + bias.to(x.dtype).view(1, -1, 1, 1)
     y = gn(x)
-    return torch.relu(y) if relu else y
+    if act == ACT_RELU:
+        return torch.relu(y)
+    if act == ACT_ELU:
+        return F.elu(y)
+    return y
 
 
 # ----------------------------------------------------------------------------------------------

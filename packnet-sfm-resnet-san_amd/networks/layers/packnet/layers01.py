@@ -10,13 +10,16 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..fused import ACT_ELU, gn_act
 from .pack3d import conv3d_unpack, pack_conv3d
 
 
 class Conv2D(nn.Module):
     """zero-pad(k//2) -> Conv2d -> GroupNorm(16) -> ELU.  The zero padding is the convolution's
     own (`padding=k//2`, identical arithmetic to ConstantPad2d + unpadded conv, layers01.py:34-39)
-    instead of a padded copy of the input; `pad` is kept as the (parameter-free) module."""
+    instead of a padded copy of the input; `pad` is kept as the (parameter-free) module.  The conv
+    bias, GroupNorm and ELU run as one fused pass each way on bf16 channels_last activations
+    (fused.gn_act, include/psfm_netops.h) instead of autocast's fp32 GroupNorm round trip."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride):
         super().__init__()
@@ -28,7 +31,8 @@ class Conv2D(nn.Module):
 
     def forward(self, x):
         c = self.conv_base
-        return self.activ(self.normalize(F.conv2d(x, c.weight, c.bias, c.stride, self.kernel_size // 2)))
+        return gn_act(F.conv2d(x, c.weight, None, c.stride, self.kernel_size // 2), c.bias, self.normalize,
+                      act=ACT_ELU)
 
 
 class ResidualConv(nn.Module):
@@ -44,7 +48,12 @@ class ResidualConv(nn.Module):
         self.activ = nn.ELU(inplace=True)
 
     def forward(self, x):
-        return self.activ(self.normalize(self.conv2(self.conv1(x)) + self.conv3(x)))
+        # GN(conv2(conv1(x)) + shortcut(x)) + ELU: the sum, shortcut bias, GroupNorm and ELU fused
+        r = self.conv2(self.conv1(x))
+        if isinstance(self.conv3, nn.Conv2d):
+            c = self.conv3
+            return gn_act(F.conv2d(x, c.weight, None, c.stride), c.bias, self.normalize, act=ACT_ELU, residual=r)
+        return gn_act(self.conv3(x), None, self.normalize, act=ACT_ELU, residual=r)
 
 
 def ResidualBlock(in_channels, out_channels, num_blocks, stride, dropout=None):

@@ -257,3 +257,41 @@ def test_upcat_matches_torch(dev, N, C1, C2, h, w):
     assert (x.grad.float() - blk).abs().max() <= (blk.abs() * 2.0 ** -8).max() + 1e-30
     if skip is not None:
         assert torch.equal(skip.grad, dout[:, C1:])
+
+
+@gpu
+@pytest.mark.parametrize("shape,residual,bias", [((6, 64, 96, 320), True, True), ((6, 32, 48, 160), False, True),
+                                                 ((2, 256, 12, 40), True, False), ((2, 32, 5, 7), False, True)])
+def test_gn_elu_matches_torch(dev, shape, residual, bias):
+    """PackNet Conv2D / ResidualConv epilogue: ELU(GroupNorm(16)(x [+ res] + bias)) and its backward
+    (dx, dres, dbias, dgamma, dbeta) against the fp32 torch chain (layers01.py:10-61)."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    C = shape[1]
+    conv_b = torch.randn(C, generator=g).to(dev, torch.bfloat16).requires_grad_(True) if bias else None
+    gn = nn.GroupNorm(16, C).to(dev)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    x = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16).requires_grad_(True)
+    r = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16).requires_grad_(True) if residual else None
+    y = FU.gn_act(x, conv_b, gn, act=FU.ACT_ELU, residual=r)
+    assert y.grad_fn is not None and "GNAct" in type(y.grad_fn).__name__
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    br = conv_b.detach().float().requires_grad_(True) if bias else None
+    wr = gn.weight.detach().clone().requires_grad_(True)
+    betar = gn.bias.detach().clone().requires_grad_(True)
+    s = xr + (rr if residual else 0) + (br.view(1, -1, 1, 1) if bias else 0)
+    yr = torch.nn.functional.elu(torch.nn.functional.group_norm(s, 16, wr, betar, gn.eps))
+    _close(y, yr, 2e-2)
+    dy = torch.randn(shape, generator=g).to(dev, torch.bfloat16)
+    y.backward(_cl(dy))
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 2e-2)
+    if residual:
+        assert torch.equal(r.grad, x.grad)
+    if bias:
+        own = x.grad.double().sum((0, 2, 3))
+        assert torch.allclose(conv_b.grad.double(), own, rtol=1e-2, atol=1e-3 * own.abs().max().item() + 1e-6)
+    _close(gn.weight.grad, wr.grad, 2e-2)
+    _close(gn.bias.grad, betar.grad, 2e-2)

@@ -209,6 +209,7 @@ def test_upsample_nearest_equals_interpolate(f, cl):
     assert ups[1].shape[-2:] == (5 * f, 7 * f)   # not a multiple -> F.interpolate
 
 
+@pytest.mark.gpu
 def test_config1_depthresnet_poseresnet_step_on_gpu_matches_cpu_oracle():
     """BASELINE config 1 (configs/overfit_kitti.yaml): SelfSupModel(DepthResNet 18pt + PoseResNet
     18pt), fp32, B=6, 192x640, min_depth 0 / max_depth 80.  The GPU step (MIOpen nets + HIP loss
