@@ -11,7 +11,9 @@
 //   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: 4 x 16 pixels x 16 k,
 //                                            16-byte staged halo tile, 4 pixels per thread
 //   k_p3d_bwd_x    dV = conv3d^T(dy)         any other layout: 4 x 8 pixels x 16 k
-//   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (tap, o)), fixed-order fp64 reduce
+//   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (spatial shift, pixel group), ND x 3
+//                  register partials; 16-byte dy staging for channels_last pack layers), fixed-order
+//                  fp64 reduce
 // V is the virtual volume: pack = space-to-depth view of x (channel k = c r^2 + i r + j),
 // unpack = x itself; the output channel o K + k is folded (pack) or pixel-shuffled (unpack).
 #include <hip/hip_runtime.h>
@@ -301,18 +303,34 @@ __global__ __launch_bounds__(NTH, 2) void k_p3d_bwd_x_cl(P3 a) {
 }
 
 // --------------------------------------------------------------------------------------------
-// per-workgroup partials: thread t < 27 ND -> (tap = t / ND, o = t % ND) of dw; the next ND -> dbias[o]
-template <typename T, int MODE, int ND>
-__global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) {
+// dW[o][tap] = sum_{b,p,k} dy[o, k, p] V[k + dz - 1, p + (dy, dx) - 1], dbias[o] = sum dy[o, ., .]:
+// per-workgroup partials over a 4 x 16 pixel tile and its share of the channel chunks.
+// Thread t < 252: spatial shift s = t % 9 ((dy, dx) of the tap) and pixel group pg = t / 9
+// (pixels pg, pg + 28, pg + 56 of the tile); it keeps the ND x 3 (o, dz) partials of its shift in
+// registers: per pixel one 18-channel V run (shared by the three dz) and ND 16-channel dy runs
+// feed 48 ND FMAs (~10 FMAs per 16-byte LDS read; one thread per (tap, o) needed 2).  Shift-0
+// threads also sum dy for dbias.  The pixel groups are folded in a fixed order through LDS at the
+// end (deterministic), one partial row per workgroup as before.
+// Staging: dy of a pack layer in channels_last (CL): each (pixel, o) run of 16 channels is one
+// pair of 16-byte loads; otherwise element loads through yaddr.
+template <typename T, int MODE, int ND, bool CL>
+__device__ __forceinline__ void bwd_w_body(const P3& a) {
     constexpr int TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2, LK = DC + 2;
-    __shared__ float sv[LY * LX * LK];         // [yy][xx][kk] with halo
-    __shared__ float sg[TY * TX * ND * DC];    // [p][o][dl], zero where out of range
+    constexpr int NPG = 28, NACT = 9 * NPG, NP = TY * TX;
+    constexpr int GS = DC + 4;                  // per-(pixel, o) run stride in sg (16-B aligned, 4 mod 8)
+    __shared__ __attribute__((aligned(16))) float sv[LY * LX * LK + 2];  // [yy][xx][kk] with halo
+    __shared__ __attribute__((aligned(16))) float sg[NP * ND * GS];      // [p][o][kl]
     const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
     const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
     const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
     const int t = threadIdx.x;
-    const int o = t % ND, tap = t / ND, dz = tap / 9, dy = (tap / 3) % 3, dx = tap % 3;
-    float acc = 0.0f;
+    const int sft = t % 9, pg = t / 9, sdy = sft / 3, sdx = sft % 3;
+    float acc[ND][3], accb[ND];
+#pragma unroll
+    for (int o = 0; o < ND; ++o) {
+        acc[o][0] = acc[o][1] = acc[o][2] = 0.0f;
+        accb[o] = 0.0f;
+    }
     for (int ch = c_lo; ch < c_hi; ++ch) {
         const int k0 = ch * DC;
         __syncthreads();
@@ -322,34 +340,100 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) {
             const bool in = gk >= 0 && gk < a.K && gy >= 0 && gy < a.Hv && gx >= 0 && gx < a.Wv;
             sv[e] = in ? ld<T>(a.x, vaddr<MODE>(a, b, gk, gy, gx)) : 0.0f;
         }
-        for (int e = t; e < TY * TX * ND * DC; e += NTH) {
-            const int kl = e % DC, r1 = e / DC, oo = r1 % ND, p = r1 / ND, py = p / TX, px = p % TX;
-            const int gk = k0 + kl, gy = y0 + py, gx = x0 + px;
-            const bool in = gk < a.K && gy < a.Hv && gx < a.Wv;
-            sg[e] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, oo, gk, gy, gx)) : 0.0f;
+        if constexpr (CL) {   // (pixel, o) runs of 16 contiguous channels: 2 x 16-byte loads each
+            for (int u = t; u < NP * ND; u += NTH) {
+                const int oo = u % ND, p = u / ND, gy = y0 + p / TX, gx = x0 + p % TX;
+                float v[16];
+                if (gy < a.Hv && gx < a.Wv) {
+                    const T* src = static_cast<const T*>(a.dy) + yaddr<MODE>(a, b, oo, k0, gy, gx);
+                    if constexpr (sizeof(T) == 2) {
+                        const uint4 q0 = reinterpret_cast<const uint4*>(src)[0], q1 = reinterpret_cast<const uint4*>(src)[1];
+                        const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            v[2 * i] = __uint_as_float(w[i] << 16);
+                            v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const float4 q = reinterpret_cast<const float4*>(src)[i];
+                            v[4 * i] = q.x, v[4 * i + 1] = q.y, v[4 * i + 2] = q.z, v[4 * i + 3] = q.w;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v[i] = 0.0f;
+                }
+                float4* dst = reinterpret_cast<float4*>(sg + (p * ND + oo) * GS);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        } else {
+            for (int e = t; e < NP * ND * DC; e += NTH) {
+                const int kl = e % DC, r1 = e / DC, oo = r1 % ND, p = r1 / ND, py = p / TX, px = p % TX;
+                const int gk = k0 + kl, gy = y0 + py, gx = x0 + px;
+                const bool in = gk < a.K && gy < a.Hv && gx < a.Wv;
+                sg[(p * ND + oo) * GS + kl] = in ? ld<T>(a.dy, yaddr<MODE>(a, b, oo, gk, gy, gx)) : 0.0f;
+            }
         }
         __syncthreads();
-        if (t < 27 * ND) {
-#pragma unroll 4
-            for (int p = 0; p < TY * TX; ++p) {
+        if (t < NACT) {
+            for (int p = pg; p < NP; p += NPG) {
                 const int py = p / TX, px = p % TX;
-                const float* g = sg + (p * ND + o) * DC;
-                const float* v = sv + ((py + dy) * LX + (px + dx)) * LK + dz;
+                const float* vr = sv + ((py + sdy) * LX + (px + sdx)) * LK;   // kk = 0..17 <-> k0-1 .. k0+16
+                float v[LK];
 #pragma unroll
-                for (int kl = 0; kl < DC; ++kl) acc += g[kl] * v[kl];
-            }
-        } else if (t < 27 * ND + ND) {
-            const int ob = t - 27 * ND;
-            for (int p = 0; p < TY * TX; ++p) {
-                const float* g = sg + (p * ND + ob) * DC;
+                for (int i = 0; i < LK; ++i) v[i] = vr[i];
 #pragma unroll
-                for (int kl = 0; kl < DC; ++kl) acc += g[kl];
+                for (int o = 0; o < ND; ++o) {
+                    const float4* g4 = reinterpret_cast<const float4*>(sg + (p * ND + o) * GS);
+                    float g[DC];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 q = g4[i];
+                        g[4 * i] = q.x, g[4 * i + 1] = q.y, g[4 * i + 2] = q.z, g[4 * i + 3] = q.w;
+                    }
+#pragma unroll
+                    for (int kl = 0; kl < DC; ++kl) {
+                        acc[o][0] += g[kl] * v[kl];
+                        acc[o][1] += g[kl] * v[kl + 1];
+                        acc[o][2] += g[kl] * v[kl + 2];
+                    }
+                    if (sft == 0) {
+#pragma unroll
+                        for (int kl = 0; kl < DC; ++kl) accb[o] += g[kl];
+                    }
+                }
             }
         }
     }
+    // fold the pixel groups in order: red[pg][tap * ND + o], bias rows after the taps
+    __syncthreads();
+    float* red = sg;   // NPG * (27 ND + ND) <= NP ND GS floats
+    if (t < NACT) {
+#pragma unroll
+        for (int o = 0; o < ND; ++o)
+#pragma unroll
+            for (int dz = 0; dz < 3; ++dz) red[pg * (28 * ND) + (dz * 9 + sft) * ND + o] = acc[o][dz];
+        if (sft == 0) {
+#pragma unroll
+            for (int o = 0; o < ND; ++o) red[pg * (28 * ND) + 27 * ND + o] = accb[o];
+        }
+    }
+    __syncthreads();
     const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    if (t < 27 * ND + ND) a.ws[blk * (27 * ND + ND) + t] = acc;
+    if (t < 28 * ND) {
+        float s = 0.0f;
+        for (int q = 0; q < NPG; ++q) s += red[q * (28 * ND) + t];
+        a.ws[blk * (27 * ND + ND) + t] = s;
+    }
 }
+
+template <typename T, int MODE, int ND, bool CL>
+__global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) { bwd_w_body<T, MODE, ND, CL>(a); }
+template <typename T, int MODE, int ND>
+__global__ __launch_bounds__(NTH) void k_p3d_bwd_w_generic(P3 a) { bwd_w_body<T, MODE, ND, false>(a); }
 
 // fixed-order fp64 reduction of the partials -> dw [o][tap], dbias [o]: one workgroup per output
 // (strided fp64 partial sums per thread, then the wave butterflies and the 4 waves in order)
@@ -498,7 +582,21 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         aw.dy = dy;
         aw.ws = ws;
         const dim3 grid = grid_of(aw, 4, 16, 16);
-        P3D_LAUNCH(k_p3d_bwd_w, grid, st, aw, t);
+        // channels_last dy of a pack layer: 16-channel runs are contiguous and 16-byte aligned
+        const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
+        const bool cl = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 16 == 0 && a.ys[0] % vec == 0 &&
+                        a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+        if (cl) {
+            if (t->dtype == PSFM_P3D_BF16) {
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_w<uint16_t, PSFM_P3D_PACK, 4, true>), grid, dim3(NTH), 0, st, aw);
+                else hipLaunchKernelGGL((k_p3d_bwd_w<uint16_t, PSFM_P3D_PACK, 8, true>), grid, dim3(NTH), 0, st, aw);
+            } else {
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_w<float, PSFM_P3D_PACK, 4, true>), grid, dim3(NTH), 0, st, aw);
+                else hipLaunchKernelGGL((k_p3d_bwd_w<float, PSFM_P3D_PACK, 8, true>), grid, dim3(NTH), 0, st, aw);
+            }
+        } else {
+            P3D_LAUNCH(k_p3d_bwd_w_generic, grid, st, aw, t);
+        }
         const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
         if (t->d == 4)
             hipLaunchKernelGGL(k_p3d_reduce_w<4>, dim3(28 * 4), dim3(NTH), 0, st, (const float*)ws, nblk, dw, dbias);
