@@ -82,11 +82,13 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
 
 /* Backward of psfm_gn_act_fwd: dx (bf16) and, with res, dres (a second copy: both inputs are summed),
  * dbias (bias dtype; the column sum of the stored dx, as autograd forms a conv bias gradient; NULL
- * with bias NULL), dgamma / dbeta (fp32 [C]).  `counter` spans two slots. */
-int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* res, const void* bias, int bias_bf16,
-                    const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C,
-                    int G, int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta, float* ws,
-                    int* counter, void* stream);
+ * with bias NULL), dgamma / dbeta (fp32 [C]).  The activation's derivative is taken at its input,
+ * recomputed from x (+ res + bias), save_mean / save_invstd and gamma / beta — the forward output is
+ * not read back (one activation-sized read less per pass).  `counter` spans two slots. */
+int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,
+                    const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
+                    int N, int HW, int C, int G, int act, void* dx, void* dres, void* dbias, float* dgamma,
+                    float* dbeta, float* ws, int* counter, void* stream);
 
 const char* psfm_netops_last_error(void);
 

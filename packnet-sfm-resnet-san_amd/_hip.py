@@ -113,7 +113,7 @@ def lib():
         "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V, V], c_int),
         "psfm_gn_act_fwd": ([V, V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V],
                             c_int),
-        "psfm_gn_act_bwd": ([V, V, V, V, V, c_int, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,
+        "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,
                              V, V], c_int),
         "psfm_netops_last_error": ([], ctypes.c_char_p),
         "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),

@@ -660,9 +660,11 @@ __device__ __forceinline__ float gn_act_f(float w, int act) {
     if (act == PSFM_ACT_ELU) return w > 0.0f ? w : expm1f(w);
     return w;
 }
-__device__ __forceinline__ float gn_act_g(float g, float y, int act) {
-    if (act == PSFM_ACT_RELU) return y > 0.0f ? g : 0.0f;
-    if (act == PSFM_ACT_ELU) return y > 0.0f ? g : g * (y + 1.0f);
+// backward of the activation from its input w (recomputed from x, mean / invstd, gamma / beta: the
+// output y is not read back)
+__device__ __forceinline__ float gn_act_g(float g, float w, int act) {
+    if (act == PSFM_ACT_RELU) return w > 0.0f ? g : 0.0f;
+    if (act == PSFM_ACT_ELU) return w > 0.0f ? g : g * expf(w);
     return g;
 }
 
@@ -816,22 +818,24 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
     if (r < a.TR) {
         const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         float mu[VEC], is[VEC];
+        float ga[VEC], be[VEC];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
             mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
             is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
+            ga[i] = a.gamma[c0 + i];
+            be[i] = a.beta[c0 + i];
         }
         const size_t so = (size_t)n * a.HW * a.C;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
         ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<VEC> g[U], y[U], x[U];
+        Vec<VEC> g[U], x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int row = base_ + u * a.TR;
             const size_t o = so + (size_t)row * a.C + c0;
             const bool in = row < row1;
             g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-            if (a.act) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
             x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
             if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
@@ -839,8 +843,8 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float gg = gn_act_g(g[u].v[i], y[u].v[i], a.act);
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
+                const float gg = gn_act_g(g[u].v[i], xh * ga[i] + be[i], a.act);
                 acc[0][i] += gg;
                 acc[1][i] += gg * xh;
             }
@@ -897,22 +901,24 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
         const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
         const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         float mu[VEC], is[VEC];
+        float ga[VEC], be[VEC];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
             mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
             is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
+            ga[i] = a.gamma[c0 + i];
+            be[i] = a.beta[c0 + i];
         }
         const size_t so = (size_t)n * a.HW * a.C;
         const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
         ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<VEC> g[U], y[U], x[U];
+        Vec<VEC> g[U], x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int row = base_ + u * a.TR;
             const size_t o = so + (size_t)row * a.C + c0;
             const bool in = row < row1;
             g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-            if (a.act) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
             x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
             if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
@@ -923,8 +929,8 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
             Vec<VEC> d;
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float gg = gn_act_g(g[u].v[i], y[u].v[i], a.act);
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
+                const float gg = gn_act_g(g[u].v[i], xh * ga[i] + be[i], a.act);
                 d.v[i] = k1.v[i] * gg - k2.v[i] - xh * k3.v[i];
             }
             st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, d);
@@ -1243,23 +1249,21 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
     return 0;
 }
 
-int psfm_gn_act_bwd(const void* dy, const void* y, const void* x, const void* res, const void* bias, int bias_bf16,
-                    const float* gamma, const float* save_mean, const float* save_invstd, int N, int HW, int C, int G,
-                    int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta, float* ws, int* counter,
-                    void* stream) {
-    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
-        (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU) || (act && !y) || (res && !dres) ||
-        (bias && !dbias))
+int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,
+                    const float* gamma, const float* beta, const float* save_mean, const float* save_invstd, int N,
+                    int HW, int C, int G, int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta,
+                    float* ws, int* counter, void* stream) {
+    if (!dy || !x || !gamma || !beta || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
+        (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU) || (res && !dres) || (bias && !dbias))
         return fail(-1, "gn_act_bwd: bad arguments");
     GNArgs a{};
     Geo g;
     int vec;
     if (int e = gn_setup(a, N, HW, C, G, g, vec)) return e;
     a.dy = static_cast<const uint16_t*>(dy);
-    a.y = static_cast<const uint16_t*>(y);
     a.x = static_cast<const uint16_t*>(x);
     a.res = static_cast<const uint16_t*>(res);
-    a.bias = bias, a.bias_bf16 = bias_bf16, a.gamma = gamma;
+    a.bias = bias, a.bias_bf16 = bias_bf16, a.gamma = gamma, a.beta = beta;
     a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
     a.out = static_cast<uint16_t*>(dx);
     a.out2 = static_cast<uint16_t*>(dres);

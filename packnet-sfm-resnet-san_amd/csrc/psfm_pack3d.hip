@@ -7,7 +7,8 @@
 // the kernels stream the volume through LDS tiles (with a 1-voxel halo in k, y, x), keep the 216
 // weights in LDS ([tap][o]: two b128 broadcast reads per tap), and write every folded /
 // pixel-shuffled output element exactly once, straight into the caller's layout (strides).
-//   k_p3d_fwd      y  = conv3d(V)            4 x 16 pixels x 32 k per chunk
+//   k_p3d_fwd      y  = conv3d(V)            4 x 16 pixels x 32 k per chunk, thread = pixel x 8 k
+//                                            (d x 8 register outputs, 16-byte stores)
 //   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: 4 x 16 pixels x 16 k,
 //                                            16-byte staged halo tile, 4 pixels per thread
 //   k_p3d_bwd_x    dV = conv3d^T(dy)         any other layout: 4 x 8 pixels x 16 k
@@ -112,8 +113,102 @@ __device__ __forceinline__ void load_weights(const P3& a, float* sw) {
 }
 
 // --------------------------------------------------------------------------------------------
+// forward: y[o, k, p] = bias[o] + sum_taps w[o, tap] V[k + dz - 1, p + (dy, dx) - 1].  Per 4 x 16
+// pixel x 32 k chunk the V halo tile is staged in LDS; a thread owns one pixel and 8 consecutive k
+// and keeps all d x 8 outputs in registers: per (dy, dx) one 10-channel V run (16-byte aligned LDS
+// reads) serves the three dz and the 8 k (27 LDS reads per 27 x 8 x d FMAs), weights are LDS
+// broadcasts.  Channels_last pack outputs (the folded channel o K + k innermost) are written as
+// one 16-byte store of 8 bf16 (two of 4 fp32) per o; other layouts element by element.
+template <typename T, int MODE, int ND>
+__device__ __forceinline__ void fwd_body(const P3& a) {
+    constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 4;  // LK: 16-B rows
+    constexpr int KB = 8;                                                          // k per thread
+    __shared__ __attribute__((aligned(16))) float sv[LY * LX * LK];
+    __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
+    load_weights<ND>(a, sw);
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int kq = threadIdx.x % (DC / KB), p = threadIdx.x / (DC / KB), py = p / TX, px = p % TX;
+    const int gy = y0 + py, gx = x0 + px;
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC;
+        __syncthreads();
+        for (int e = threadIdx.x; e < LY * LX * LK; e += NTH) {
+            const int kk = e % LK, rest = e / LK, xx = rest % LX, yy = rest / LX;
+            const int gk = k0 - 1 + kk, gy2 = y0 - 1 + yy, gx2 = x0 - 1 + xx;
+            const bool in = kk < DC + 2 && gk >= 0 && gk < a.K && gy2 >= 0 && gy2 < a.Hv && gx2 >= 0 && gx2 < a.Wv;
+            sv[e] = in ? ld<T>(a.x, vaddr<MODE>(a, b, gk, gy2, gx2)) : 0.0f;
+        }
+        __syncthreads();
+        const int kb = k0 + kq * KB;
+        if (gy >= a.Hv || gx >= a.Wv || kb >= a.K) continue;
+        float acc[ND][KB];
+#pragma unroll
+        for (int o = 0; o < ND; ++o)
+#pragma unroll
+            for (int j = 0; j < KB; ++j) acc[o][j] = sw[27 * ND + o];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                const float4* vr = reinterpret_cast<const float4*>(sv + ((py + dy) * LX + (px + dx)) * LK + kq * KB);
+                float v[KB + 4];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const float4 q = vr[i];
+                    v[4 * i] = q.x, v[4 * i + 1] = q.y, v[4 * i + 2] = q.z, v[4 * i + 3] = q.w;
+                }
+#pragma unroll
+                for (int dz = 0; dz < 3; ++dz) {
+                    const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
+#pragma unroll
+                    for (int h = 0; h < ND / 4; ++h) {
+                        const float4 wv = w4[h];
+                        const float wo[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int j = 0; j < KB; ++j) acc[4 * h + u][j] += wo[u] * v[j + dz];
+                    }
+                }
+            }
+        if (kb + KB <= a.K) {
+#pragma unroll
+            for (int o = 0; o < ND; ++o) {
+                T* dst = static_cast<T*>(a.y) + yaddr<MODE>(a, b, o, kb, gy, gx);
+                if constexpr (sizeof(T) == 2) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint32_t lo = __float_as_uint(acc[o][2 * i]), hi = __float_as_uint(acc[o][2 * i + 1]);
+                        lo += 0x7fffu + ((lo >> 16) & 1u);
+                        hi += 0x7fffu + ((hi >> 16) & 1u);
+                        w[i] = (lo >> 16) | (hi & 0xffff0000u);
+                    }
+                    *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+                    reinterpret_cast<float4*>(dst)[0] = make_float4(acc[o][0], acc[o][1], acc[o][2], acc[o][3]);
+                    reinterpret_cast<float4*>(dst)[1] = make_float4(acc[o][4], acc[o][5], acc[o][6], acc[o][7]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int o = 0; o < ND; ++o)
+#pragma unroll
+                for (int j = 0; j < KB; ++j)
+                    if (kb + j < a.K) st<T>(a.y, yaddr<MODE>(a, b, o, kb + j, gy, gx), acc[o][j]);
+        }
+    }
+}
+
 template <typename T, int MODE, int ND>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_fwd(P3 a) {
+    fwd_body<T, MODE, ND>(a);
+}
+// other layouts (unpack layers, NCHW): thread = (k, pixel), element stores through yaddr
+template <typename T, int MODE, int ND>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_fwd_generic(P3 a) {
     constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 2;
     __shared__ float sv[LY * LX * LK];
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
@@ -142,7 +237,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
             float acc[ND];
 #pragma unroll
             for (int o = 0; o < ND; ++o) acc[o] = sw[27 * ND + o];
-#pragma unroll
+#pragma unroll 1  // the 216 weights of d = 8 fully unrolled would not fit 256 VGPRs
             for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
@@ -162,6 +257,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
         }
     }
 }
+
+
 
 // --------------------------------------------------------------------------------------------
 // dV[k, y, x] = sum_o sum_taps w[o, dz, dy, dx] dy[o, k - dz + 1, y - dy + 1, x - dx + 1]
@@ -193,7 +290,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
             const int gy = y0 + py, gx = x0 + px;
             if (gy >= a.Hv || gx >= a.Wv) continue;
             float acc = 0.0f;
-#pragma unroll
+#pragma unroll 1  // d = 8: the fully unrolled weights would spill
             for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
@@ -432,6 +529,7 @@ __device__ __forceinline__ void bwd_w_body(const P3& a) {
 
 template <typename T, int MODE, int ND, bool CL>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) { bwd_w_body<T, MODE, ND, CL>(a); }
+
 template <typename T, int MODE, int ND>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_generic(P3 a) { bwd_w_body<T, MODE, ND, false>(a); }
 
@@ -528,7 +626,22 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
     a.w = w;
     a.bias = bias;
     const dim3 grid = grid_of(a, 4, 16, 32);
-    P3D_LAUNCH(k_p3d_fwd, grid, (hipStream_t)stream, a, t);
+    hipStream_t st = (hipStream_t)stream;
+    // channels_last pack output: each thread's 8 folded channels are one aligned 16-byte run
+    const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
+    const bool vst = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 8 == 0 && a.ys[0] % vec == 0 &&
+                     a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+    if (vst) {
+        if (t->dtype == PSFM_P3D_BF16) {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd<uint16_t, PSFM_P3D_PACK, 4>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd<uint16_t, PSFM_P3D_PACK, 8>), grid, dim3(NTH), 0, st, a);
+        } else {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd<float, PSFM_P3D_PACK, 4>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd<float, PSFM_P3D_PACK, 8>), grid, dim3(NTH), 0, st, a);
+        }
+    } else {
+        P3D_LAUNCH(k_p3d_fwd_generic, grid, st, a, t);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail((int)e, std::string("launch: ") + hipGetErrorString(e));
 }

@@ -182,13 +182,13 @@ class _GNAct(torch.autograd.Function):
                                      ctypes.c_float(eps), N, HW, C, G, int(act), _hip.ptr(y), _hip.ptr(mean),
                                      _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
                    "psfm_gn_act_fwd")
-        ctx.save_for_backward(x, res, y, bias, weight, mean, invstd)
+        ctx.save_for_backward(x, res, bias, weight, beta, mean, invstd)
         ctx.G, ctx.act, ctx.counter = G, act, counter
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, res, y, bias, weight, mean, invstd = ctx.saved_tensors
+        x, res, bias, weight, beta, mean, invstd = ctx.saved_tensors
         dy = _rows(dy.to(x.dtype))
         N, C, H, W = x.shape
         HW, G = H * W, ctx.G
@@ -201,8 +201,8 @@ class _GNAct(torch.autograd.Function):
         db = torch.empty(C, device=dev, dtype=torch.float32)
         ws = torch.empty(L.psfm_gn_ws_floats(N, HW, C, G), device=dev, dtype=torch.float32)
         bf = int(bias is not None and bias.dtype == torch.bfloat16)
-        _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf,
-                                     _hip.ptr(weight), _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.act),
+        _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf, _hip.ptr(weight),
+                                     _hip.ptr(beta), _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.act),
                                      _hip.ptr(dx), _hip.ptr(dres), _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db),
                                      _hip.ptr(ws), _slot(ctx.counter, BWD), _hip.stream(dev)), "psfm_gn_act_bwd")
         return dx, dres, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None

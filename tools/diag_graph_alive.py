@@ -42,8 +42,17 @@ def chain(obj, depth=4, seen=None):
         chain(r, depth - 1, seen)
 
 
+VARIANT = os.environ.get("DIAG_VARIANT", "default")
+if VARIANT == "k1k2":
+    from packnet_sfm_amd.losses import _hip_photometric as HP
+    HP.FUSED_GRAD = False
 torch.manual_seed(0)
 m = bench.to_channels_last(bench.build_model(A, dev))
+if VARIANT == "eager_upsample":
+    m.lazy_upsample = False
+if VARIANT == "serial_pose":
+    m.overlap_pose_net = False
+print("[diag] variant", VARIANT, flush=True)
 tr = T.DDPTrainer(m, T.make_optimizer(m, 1e-4, 1e-4, capturable=True), dev, amp_dtype=None, graph=True)
 b = bench.synthetic_batch(2, 64, 192, dev, seed=0, channels_last=True)
 refs = []
@@ -78,6 +87,9 @@ def restore(snap):
 
 
 tr._restore = restore
-tr.train_step(b)
-torch.cuda.synchronize()
-print("[diag] done", flush=True)
+import warnings  # noqa: E402
+with warnings.catch_warnings(record=True) as w:
+    warnings.simplefilter("always")
+    tr.train_step(b)
+    torch.cuda.synchronize()
+print("[diag] done; AccumulateGrad warnings:", sum("AccumulateGrad" in str(x.message) for x in w), flush=True)
