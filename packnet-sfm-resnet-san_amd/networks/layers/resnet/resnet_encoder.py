@@ -122,5 +122,8 @@ class ResnetEncoder(nn.Module):
         feats.append(e.layer1(e.maxpool(x)))
         for layer in (e.layer2, e.layer3, e.layer4):
             feats.append(layer(feats[-1]))
-        self.features = feats
+        # not kept on the module (the reference stores self.features): a reference held between
+        # steps keeps the previous step's encoder graph alive, and with it the AccumulateGrad nodes
+        # of every encoder parameter — the next step (or HIP-graph capture) on another stream then
+        # reuses nodes bound to the old stream (tools/diag_accgrad_nodes.py)
         return feats

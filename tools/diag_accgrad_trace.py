@@ -32,7 +32,8 @@ for it in range(3):
     st = s if it == 0 else torch.cuda.Stream(device=dev)
     st.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(st), warnings.catch_warnings():
-        warnings.simplefilter("error")
+        warnings.simplefilter("ignore")
+        warnings.filterwarnings("error", message=".*AccumulateGrad.*")
         try:
             with torch.autograd.detect_anomaly(check_nan=False):
                 tr.train_step(b)
