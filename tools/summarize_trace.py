@@ -43,5 +43,21 @@ if len(k1) >= 3:
         lines.append("--- normalisation / epilogue kernels by grid (avg us per launch, launches/step) ---")
         for (k, gsz), v in sorted(bygrid.items(), key=lambda kv: (kv[0][0], -kv[1][0])):
             lines.append(f"{v[0] / 1e3 / v[1]:8.2f} us  x{v[1] / n:4.1f}  grid={gsz:>8}  {k}")
+    # timeline of the last step: start offset, duration, queue, gap to the previous kernel's end
+    # (any queue) -- where the step waits on the host or on a cross-stream dependency
+    lines.append("--- last step timeline (us: start, dur, idle-before, queue, kernel) ---")
+    j0 = k1[-2]
+    t0 = int(rows[j0]["Start_Timestamp"])
+    last_end = t0
+    idle = 0
+    for r in rows[j0:i1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = max(0, s - last_end)
+        idle += gap
+        q = r.get("Queue_Id", r.get("Stream_Id", "?"))
+        lines.append(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {gap / 1e3:7.1f}  q{q:>3}  "
+                     f"{r['Kernel_Name'][:90]}")
+        last_end = max(last_end, e)
+    lines.append(f"idle (no kernel running) in last step: {idle / 1e3:.1f} us")
 open(out, "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:3]))
