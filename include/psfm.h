@@ -141,9 +141,11 @@ int psfm_photometric_bwd(const psfm_params* p, const psfm_inputs* in, const psfm
 int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float* smooth_stats,
                         const float* grad_out, float* const* grad_sig, void* stream);
 
-/* Sum the per-tile dL/dT partials of up to PSFM_MAX_SCALES calls into grad_T [N][B][12]. */
+/* Sum the per-tile dL/dT partials of up to PSFM_MAX_SCALES calls into grad_T [N][B][grad_stride]:
+ * grad_stride 12 = dL/d[R|t] as [3][4]; 16 = dL/dT of the full [4][4] pose matrix (bottom row 0:
+ * the pose's constant row), so the gradient of Pose.mat needs no ATen slice / pad. */
 int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
-                          const psfm_workspace* const* ws, float* grad_T, void* stream);
+                          const psfm_workspace* const* ws, float* grad_T, int grad_stride, void* stream);
 
 /* Pre-pass of the K12 training step: K0 (automask candidates, skipped with clip_loss > 0 where
  * psfm_photometric_clip_stats made them) and the per-(scale, image) chunk sums of each sigmoid
@@ -172,11 +174,11 @@ int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const
 int psfm_photometric_grad_finish(const psfm_params* p, const float* smooth_stats, const float* grad_out,
                                  const float* const* grad_k12, float* const* grad_sig, void* stream);
 
-/* Pose gradient for the K12 path: grad_T [N][B][12] = grad_out * sum of the per-unit partials
- * of up to PSFM_MAX_SCALES calls (fixed order, fp64). */
+/* Pose gradient for the K12 path: grad_T [N][B][grad_stride] = grad_out * sum of the per-unit
+ * partials of up to PSFM_MAX_SCALES calls (fixed order, fp64); grad_stride as above. */
 int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
                                  const psfm_workspace* const* ws, const float* grad_out,
-                                 float* grad_T, void* stream);
+                                 float* grad_T, int grad_stride, void* stream);
 
 /* Standalone view_synthesis (geometry/camera_utils.py:27-59) for one context:
  * warped[B,3,H,W] = grid_sample(ref, project(reconstruct(depth))).  cam: [B][PSFM_CAMREC] records

@@ -66,6 +66,7 @@ class AugmentParams(ctypes.Structure):
 
 
 _lib = None
+POSE_MAX_CTX = 8  # include/psfm_pose.h PSFM_POSE_MAX_CTX
 
 
 def lib():
@@ -88,11 +89,11 @@ def lib():
         "psfm_finalize": ([c_int, PP, WSP, V, V, V], c_int),
         "psfm_photometric_bwd": ([P, IN, WS, V, V, V], c_int),
         "psfm_smoothness_bwd": ([P, IN, V, V, V, V], c_int),
-        "psfm_pose_grad_reduce": ([c_int, PP, WSP, V, V], c_int),
+        "psfm_pose_grad_reduce": ([c_int, PP, WSP, V, c_int, V], c_int),
         "psfm_photometric_prepass": ([P, IN, WS, V], c_int),
         "psfm_photometric_fwd_grad": ([P, IN, WS, V, V], c_int),
         "psfm_photometric_grad_finish": ([P, V, V, V, V, V], c_int),
-        "psfm_pose_grad_reduce_scaled": ([c_int, PP, WSP, V, V, V], c_int),
+        "psfm_pose_grad_reduce_scaled": ([c_int, PP, WSP, V, V, c_int, V], c_int),
         "psfm_view_synthesis_fwd": ([c_int, c_int, c_int, c_int, V, V, V, V, V], c_int),
         "psfm_view_synthesis_bwd": ([c_int, c_int, c_int, c_int, V, V, V, V, V, V, V, V], c_int),
         "psfm_tiles_per_image": ([c_int, c_int], c_int),
@@ -131,6 +132,11 @@ def lib():
         "psfm_augment_ws_bytes": ([ctypes.POINTER(AugmentParams)], c_size_t),
         "psfm_train_augment": ([ctypes.POINTER(AugmentParams), V, V, V, V, V, V, V], c_int),
         "psfm_augment_last_error": ([], ctypes.c_char_p),
+        # include/psfm_pose.h
+        "psfm_pose_from_vec_fwd": ([V, c_int, c_int, V, V], c_int),
+        "psfm_pose_from_vec_bwd": ([V, c_int, c_int, V, V, V], c_int),
+        "psfm_pinhole_cam_records": ([V, V, V, c_int, c_int, c_int, c_int, c_float, V, V], c_int),
+        "psfm_pose_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -150,7 +156,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_upcat_fwd", "psfm_upcat_bwd",
             "psfm_depth_metrics", "psfm_metrics_last_error",
             "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
-            "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error")
+            "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error",
+            "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error")
 
 
 def check(rc, what):
@@ -163,6 +170,8 @@ def check(rc, what):
             err = lib().psfm_metrics_last_error
         elif what.startswith(("psfm_augment", "psfm_train_augment")):
             err = lib().psfm_augment_last_error
+        elif what.startswith(("psfm_pose_from_vec", "psfm_pinhole_cam_records")):
+            err = lib().psfm_pose_last_error
         elif what.startswith("psfm_p3d"):
             err = lib().psfm_p3d_last_error
         else:

@@ -730,14 +730,15 @@ __global__ __launch_bounds__(1024) void k_clip_thr(ThrArgs t) {
     }
 }
 
-// dL/dT: sum over calls, scales and tiles (fixed order) -> grad_T [N][B][12]
+// dL/dT: sum over calls, scales and tiles (fixed order) -> grad_T [N][B][stride] (stride 16: the
+// [4][4] pose matrix, bottom row zero)
 struct PoseRedCall {
     const float* part;
     int S, N, B, tiles;
 };
 struct PoseRedArgs {
     PoseRedCall c[MAXS];
-    int ncalls, N, B;
+    int ncalls, N, B, stride;
     float* grad_T;
     const float* grad_out;  // K12 path: partials are for dL/dloss = 1 (NULL: already scaled)
 };
@@ -756,7 +757,10 @@ __global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
                 acc += wave_sum_d(part);
             }
         }
-        if (lane == 0) r.grad_T[item] = (float)(r.grad_out ? acc * (double)*r.grad_out : acc);
+        if (lane == 0) {
+            r.grad_T[(size_t)jb * r.stride + k] = (float)(r.grad_out ? acc * (double)*r.grad_out : acc);
+            if (r.stride == 16 && k < 4) r.grad_T[(size_t)jb * 16 + 12 + k] = 0.0f;
+        }
     }
 }
 
@@ -1211,9 +1215,11 @@ int psfm_smoothness_bwd(const psfm_params* p, const psfm_inputs* in, const float
 }
 
 int psfm_pose_grad_reduce(int ncalls, const psfm_params* const* calls,
-                          const psfm_workspace* const* ws, float* grad_T, void* stream) {
+                          const psfm_workspace* const* ws, float* grad_T, int grad_stride, void* stream) {
     if (ncalls < 1 || ncalls > MAXS || !calls || !ws || !grad_T) return fail(-1, "bad pose reduce args");
+    if (grad_stride != 12 && grad_stride != 16) return fail(-2, "grad_stride must be 12 or 16");
     PoseRedArgs r{};
+    r.stride = grad_stride;
     r.ncalls = ncalls;
     r.N = calls[0]->N;
     r.B = calls[0]->B;
@@ -1258,6 +1264,7 @@ int psfm_view_synthesis_bwd(int cam_model, int B, int H, int W, const float* ref
     r.ncalls = 1;
     r.N = 1;
     r.B = B;
+    r.stride = 12;
     r.grad_T = grad_T;
     r.c[0] = PoseRedCall{pose_part, 1, 1, B, tiles_img(H, W)};
     hipLaunchKernelGGL(k_pose_reduce, dim3((B * 12 + 3) / 4), dim3(256), 0, st, r);
@@ -1371,9 +1378,11 @@ int psfm_photometric_grad_finish(const psfm_params* p, const float* smooth_stats
 
 int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
                                  const psfm_workspace* const* ws, const float* grad_out,
-                                 float* grad_T, void* stream) {
+                                 float* grad_T, int grad_stride, void* stream) {
     if (ncalls < 1 || ncalls > MAXS || !calls || !ws || !grad_T || !grad_out) return fail(-1, "bad pose reduce args");
+    if (grad_stride != 12 && grad_stride != 16) return fail(-2, "grad_stride must be 12 or 16");
     PoseRedArgs r{};
+    r.stride = grad_stride;
     r.ncalls = ncalls;
     r.N = calls[0]->N;
     r.B = calls[0]->B;

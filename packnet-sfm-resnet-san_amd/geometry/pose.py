@@ -2,6 +2,7 @@
 (`identity`, `from_vec`, `inverse`, `transform_pose`, `transform_points`, `@`)."""
 import torch
 
+from ._hip_pose import pose_mats_from_vecs
 from .pose_utils import invert_pose, pose_vec2mat
 
 
@@ -20,11 +21,22 @@ class Pose:
 
     @classmethod
     def from_vec(cls, vec, mode):
-        """[B,6] vector -> Pose (pose.py:39-46)."""
+        """[B,6] vector -> Pose (pose.py:39-46).  Device fp32 vectors, mode 'euler': one HIP
+        launch each way (geometry/_hip_pose.py)."""
+        if mode == "euler" and vec.is_cuda and vec.dtype == torch.float32:
+            return cls(pose_mats_from_vecs(vec.reshape(len(vec), 1, 6))[0])
         top = pose_vec2mat(vec, mode)
         bottom = torch.zeros(len(vec), 1, 4, device=vec.device, dtype=vec.dtype)
         bottom[:, 0, 3] = 1.0
         return cls(torch.cat([top, bottom], 1))
+
+    @classmethod
+    def from_vecs(cls, vec, mode):
+        """[B,N,6] (a pose net's output) -> N Poses, [Pose.from_vec(vec[:, i], mode) for i]; on the
+        device one launch for all contexts."""
+        if mode == "euler" and vec.is_cuda and vec.dtype == torch.float32:
+            return [cls(m) for m in pose_mats_from_vecs(vec)]
+        return [cls.from_vec(vec[:, i], mode) for i in range(vec.shape[1])]
 
     @property
     def shape(self):

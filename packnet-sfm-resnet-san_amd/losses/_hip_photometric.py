@@ -12,7 +12,6 @@ import torch
 import torch.nn.functional as F
 
 from .. import _hip
-from ..geometry.camera_utils import scale_intrinsics, pinhole_inverse
 from ..utils.image import NearestScales
 
 
@@ -180,7 +179,9 @@ class PhotometricLossFn(torch.autograd.Function):
         dev = image.device
         B, _, H, W = image.shape
         N, n = len(contexts), len(sigs)
-        Tf = T.detach().reshape(N, B, 12).float()
+        # T: [N,B,3,4] ([R|t]) or [N,B,4,4] (Pose.mat; its bottom row is constant)
+        Tc = T.detach().float().contiguous()
+        t_stride = 4 * T.shape[-2]
 
         # group consecutive scales of equal size into one call (full-res: one call for all);
         # stored coarse maps with a nearest 2^k mapping count as full size (cfg["shifts"])
@@ -202,19 +203,22 @@ class PhotometricLossFn(torch.autograd.Function):
             raise NotImplementedError("fisheye (VADAS) cameras: N <= 2 contexts, SSIM candidates, and the K12 "
                                       "gradient path (FUSED_GRAD)")
         calls = []
+        L = _hip.lib()
         for (a, b) in groups:
             hw = size(a)
             scale = hw[1] / float(W)  # Camera.scaled(DW/W) (camera.py:84-108)
             if fish:
+                Tf = Tc[..., :3, :].reshape(N, B, 12)
                 cam = _fisheye_records(K, ref_K, Tf, scale, hw[0] / float(H), b - a, N, B, dev)
             else:
-                Kt = scale_intrinsics(K.clone(), scale, scale) if scale != 1.0 else K
-                Kr = scale_intrinsics(ref_K.clone(), scale, scale) if scale != 1.0 else ref_K
-                kinv = pinhole_inverse(Kt.float()).reshape(1, 1, B, 9).expand(b - a, N, B, 9)
-                kref = Kr.float().reshape(1, 1, B, 9).expand(b - a, N, B, 9)
-                tt = Tf.reshape(1, N, B, 12).expand(b - a, N, B, 12)
-                pad = torch.zeros(b - a, N, B, _hip.CAMREC - 30, device=dev, dtype=torch.float32)
-                cam = torch.cat([kinv, kref, tt, pad], -1).contiguous()
+                # Camera.scaled + Kinv + [R|t] records for every scale of the group: one launch
+                # (include/psfm_pose.h; the ATen chain was ~15 small kernels on the critical path)
+                cam = torch.empty(b - a, N, B, _hip.CAMREC, device=dev, dtype=torch.float32)
+                Kc, Krc = K.float().contiguous(), ref_K.float().contiguous()
+                _hip.require_device(Kc, Krc)
+                _hip.check(L.psfm_pinhole_cam_records(_hip.ptr(Kc), _hip.ptr(Krc), _hip.ptr(Tc), t_stride, B, N,
+                                                      b - a, scale, _hip.ptr(cam), _hip.stream(dev)),
+                           "psfm_pinhole_cam_records")
             im = _to_size(image, hw, "bilinear")
             cx = [_to_size(c, hw, "bilinear") for c in contexts]
             mk = _to_size(mask, hw, "nearest").contiguous() if mask is not None else None
@@ -222,7 +226,6 @@ class PhotometricLossFn(torch.autograd.Function):
                                _hip.CAM_FISHEYE if fish else _hip.CAM_PINHOLE,
                                shifts[a:b] if shifts else None))
 
-        L = _hip.lib()
         st = _hip.stream(dev)
         for c in calls:
             if cfg["clip"] > 0.0:
@@ -247,6 +250,7 @@ class PhotometricLossFn(torch.autograd.Function):
         _run("finalize", L.psfm_finalize, len(calls), pp, wp, _hip.ptr(smooth_stats), _hip.ptr(out), st,
              keep=(calls, smooth_stats, out))
         ctx.calls, ctx.smooth_stats, ctx.cfg, ctx.n_ctx, ctx.T_shape = calls, smooth_stats, cfg, N, T.shape
+        ctx.t_stride = t_stride
         ctx.fused = fused
         ctx.sig_shapes = [s.shape for s in sigs]
         loss, photo, smooth = out[0:1], out[1].clone(), out[2].clone()
@@ -263,7 +267,7 @@ class PhotometricLossFn(torch.autograd.Function):
         N, B = ctx.n_ctx, calls[0].params.B
         pp = (ctypes.POINTER(_hip.Params) * len(calls))(*[ctypes.pointer(c.params) for c in calls])
         wp = (ctypes.POINTER(_hip.Workspace) * len(calls))(*[ctypes.pointer(c.ws) for c in calls])
-        gT = torch.empty(N, B, 12, device=dev, dtype=torch.float32)
+        gT = torch.empty(N, B, ctx.t_stride, device=dev, dtype=torch.float32)
         if ctx.fused:  # gradient already computed by K12 for dL/dloss = 1: scale + normaliser term
             grads = []
             for c in calls:
@@ -273,7 +277,7 @@ class PhotometricLossFn(torch.autograd.Function):
                      keep=(c, ctx.smooth_stats, gout, gsig))
                 grads.extend(gsig)
             _run("pose_grad_reduce", L.psfm_pose_grad_reduce_scaled, len(calls), pp, wp, _hip.ptr(gout),
-                 _hip.ptr(gT), st, keep=(calls, gout, gT))
+                 _hip.ptr(gT), ctx.t_stride, st, keep=(calls, gout, gT))
             return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
         grads = []
         for c in calls:
@@ -286,7 +290,7 @@ class PhotometricLossFn(torch.autograd.Function):
                 _run("K3_smoothness_bwd", L.psfm_smoothness_bwd, ctypes.byref(c.params), ctypes.byref(c.inputs),
                      _hip.ptr(ctx.smooth_stats), _hip.ptr(gout), arr, st, keep=(c, ctx.smooth_stats, gout, gsig))
             grads.extend(gsig)
-        _run("pose_grad_reduce", L.psfm_pose_grad_reduce, len(calls), pp, wp, _hip.ptr(gT), st,
+        _run("pose_grad_reduce", L.psfm_pose_grad_reduce, len(calls), pp, wp, _hip.ptr(gT), ctx.t_stride, st,
              keep=(calls, gT))
         return (None, None, None, None, None, gT.reshape(ctx.T_shape), None) + (None,) * N + tuple(grads)
 

@@ -69,7 +69,9 @@ class MultiViewPhotometricLoss(LossBase):
             sigs = NearestScales([s.float() for s in inv_depths.stored[:self.n]], inv_depths.shape)
         else:
             sigs = [s.float() for s in inv_depths[:self.n]]  # nets may run under bf16 autocast
-        T = torch.stack([p.mat[:, :3, :] for p in poses], 0)  # [N,B,3,4], differentiable
+        # [N,B,4,4], differentiable: the whole matrices (the kernels read rows 0-2 and write a zero
+        # bottom-row gradient), so autograd needs no slice / zero-fill per pose
+        T = torch.stack([p.mat for p in poses], 0)
         cfg = dict(n=self.n, automask=bool(self.automask_loss),
                    reduce_op=_hip.REDUCE_MIN if self.photometric_reduce_op == "min" else _hip.REDUCE_MEAN,
                    ssim_w=float(self.ssim_loss_weight), C1=float(self.C1), C2=float(self.C2),

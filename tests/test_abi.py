@@ -19,7 +19,8 @@ def hip():
 
 def declared_functions():
     names = set()
-    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h", "psfm_pack3d.h", "psfm_augment.h"):
+    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h", "psfm_pack3d.h", "psfm_augment.h",
+              "psfm_pose.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src))
@@ -66,7 +67,10 @@ def test_fused_path_argument_checks(hip):
     assert L.psfm_photometric_fwd_grad(ctypes.byref(p), ctypes.byref(inp), ctypes.byref(ws), None, None) == -12
     assert b"workspace" in L.psfm_last_error()
     assert L.psfm_photometric_grad_finish(ctypes.byref(p), None, None, None, None, None) == -14
-    assert L.psfm_pose_grad_reduce_scaled(0, None, None, None, None, None) == -1
+    assert L.psfm_pose_grad_reduce_scaled(0, None, None, None, None, 12, None) == -1
+    assert L.psfm_pose_from_vec_fwd(None, 1, 1, None, None) == -1
+    assert L.psfm_pose_from_vec_bwd(None, 1, 9, None, None, None) == -1
+    assert L.psfm_pinhole_cam_records(None, None, None, 12, 1, 1, 1, 1.0, None, None) == -1
 
 
 @pytest.mark.parametrize("field,value,code", [("N", 0, -3), ("N", 5, -3), ("S", 0, -4), ("H", 1, -2),
