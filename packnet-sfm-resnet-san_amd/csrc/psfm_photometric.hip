@@ -817,6 +817,34 @@ struct GradFinishArgs {
     float smooth_w;
 };
 
+// the F x F block of the full-resolution gradient under one stored coarse pixel, summed in
+// row-major order: every load issued before the first add (F = 2, 4, 8: 16-byte row loads for
+// F >= 4), so a thread waits for memory once, not F*F times
+template <int F>
+__device__ __forceinline__ float block_sum_rowmajor(const float* __restrict__ r, int W, float go, float c) {
+    float v[F][F];
+#pragma unroll
+    for (int dy = 0; dy < F; ++dy) {
+        const float* row = r + (size_t)dy * W;
+        if constexpr (F >= 4) {
+#pragma unroll
+            for (int q = 0; q < F / 4; ++q) {
+                const float4 t = reinterpret_cast<const float4*>(row)[q];
+                v[dy][4 * q] = t.x, v[dy][4 * q + 1] = t.y, v[dy][4 * q + 2] = t.z, v[dy][4 * q + 3] = t.w;
+            }
+        } else {
+            const float2 t = *reinterpret_cast<const float2*>(row);
+            v[dy][0] = t.x, v[dy][1] = t.y;
+        }
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int dy = 0; dy < F; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < F; ++dx) acc += go * (v[dy][dx] + c);
+    return acc;
+}
+
 // g = gout * (g + c[s][b]); c = -(cx Ax + cy Ay) / mc^2 / (H W) where the mean is not clamped
 // (the d/ds of the 1/mean(s) normaliser; same expression as k_smooth_bwd)
 __global__ __launch_bounds__(NT) void k_grad_finish(GradFinishArgs a) {
@@ -847,20 +875,27 @@ __global__ __launch_bounds__(NT) void k_grad_finish(GradFinishArgs a) {
         return;
     }
     // stored coarse map: the adjoint of the nearest 2^sh upsampling sums each 2^sh x 2^sh block of
-    // the full-resolution gradient (row-major, fixed order: deterministic, no atomics)
+    // the full-resolution gradient (row-major, fixed order: deterministic, no atomics).  One
+    // coarse pixel per thread (the grid covers the full plane, >= 4x the coarse one)
     const int f = 1 << sh;
     const uint32_t Ws = (uint32_t)(a.W >> sh);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const uint32_t i = i0 + u * NT;
-        if (i >= cplane) break;
-        const uint32_t Y = i / Ws, X = i - Y * Ws;
-        const float* r = gi + ((size_t)Y * f) * a.W + (size_t)X * f;
-        float acc = 0.0f;
+    const uint32_t i = blockIdx.x * NT + threadIdx.x;
+    if (i >= cplane) return;
+    const uint32_t Y = i / Ws, X = i - Y * Ws;
+    const float* r = gi + ((size_t)Y * f) * a.W + (size_t)X * f;
+    float acc;
+    if (sh == 1) {
+        acc = block_sum_rowmajor<2>(r, a.W, go, c);
+    } else if (sh == 2) {
+        acc = block_sum_rowmajor<4>(r, a.W, go, c);
+    } else if (sh == 3) {
+        acc = block_sum_rowmajor<8>(r, a.W, go, c);
+    } else {
+        acc = 0.0f;
         for (int dy = 0; dy < f; ++dy)
             for (int dx = 0; dx < f; ++dx) acc += go * (r[(size_t)dy * a.W + dx] + c);
-        g[i] = acc;
     }
+    g[i] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -168,6 +168,7 @@ class PhotometricLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, image, mask, K, ref_K, T, n_ctx, *rest):
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the metric outputs
         # detached: the per-call records (_Call) live on ctx, and an input with a grad_fn stored
         # there would form a ctx -> tensor -> graph -> ctx cycle that keeps every step's autograd
         # graph (and its AccumulateGrad nodes) alive until the garbage collector runs

@@ -25,6 +25,7 @@ not on the hot path: the non-finite check accumulates on the device, tested ever
 `check_every` steps.
 """
 import contextlib
+import math
 import gc
 
 import torch
@@ -139,7 +140,10 @@ class DDPTrainer:
             output = self.ddp(batch, progress=progress)
         loss = output["loss"]
         loss.sum().backward()
-        self.nonfinite += (~torch.isfinite(loss.detach())).any().float()
+        # sticky non-finite flag in one launch: 0 * loss is 0 for a finite loss, NaN otherwise
+        # (the isfinite / any / cast / add chain was five kernels at the end of every step)
+        ld = loss.detach()
+        self.nonfinite.add_(ld.reshape(()) if ld.numel() == 1 else ld.float().sum(), alpha=0.0)
         if self.mp is not None:
             self.mp.grads_to_master()
         return output
@@ -362,7 +366,7 @@ class DDPTrainer:
         flag = self.nonfinite.clone()
         if self.world > 1 and dist.is_initialized():
             dist.all_reduce(flag)
-        if float(flag) > 0:
+        if not math.isfinite(float(flag)):
             raise ValueError(f"Non-finite loss within the last steps (step {self.step_idx})")
 
 

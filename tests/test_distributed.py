@@ -203,3 +203,34 @@ def test_multicamera_batches_fold_cameras_into_the_batch():
     b = loader.next_into(None)
     assert b["rgb"].shape == (8, 3, 16, 32) and b["intrinsics"].shape == (8, 3, 3)
     assert torch.equal(b["rgb"][4:8], ds[1]["rgb"]) and torch.equal(b["intrinsics"][4:8], ds[1]["intrinsics"])
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_check_finite_flags_a_nonfinite_loss_seen_steps_earlier(bad):
+    """The trainer's sticky non-finite flag (0 * loss accumulated per step) reports a NaN / inf
+    loss at the next check even when the steps after it were finite."""
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+
+    class Poisoned(TinyModel):
+        def __init__(self):
+            super().__init__()
+            self.calls = 0
+
+        def forward(self, batch, progress=0.0):
+            out = super().forward(batch, progress)
+            self.calls += 1
+            if self.calls == 2:
+                out["loss"] = out["loss"] * bad
+            return out
+
+    torch.manual_seed(0)
+    model = Poisoned()
+    tr = DDPTrainer(model, make_optimizer(model, 1e-3, 1e-3), torch.device("cpu"), amp_dtype=None, graph=False,
+                    flat=True)
+    tr.train_step(_batch(0))
+    tr.check_finite()   # finite so far
+    for _ in range(3):
+        tr.train_step(_batch(0))
+    with pytest.raises(ValueError, match="Non-finite"):
+        tr.check_finite()
