@@ -88,8 +88,14 @@ def parse(argv=None):
     ap.add_argument("--amp", default=None, choices=["bf16", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N>1 on one GPU (ranks share the device, host all-reduce)")
-    ap.add_argument("--comm", default="split", choices=["split", "graph"],
-                    help="split: all_reduce between two graph replays; graph: captured into the step graph")
+    ap.add_argument("--comm", default="auto", choices=["auto", "split", "graph", "overlap"],
+                    help="split: all_reduce between two graph replays; graph: captured into the step graph "
+                         "after the backward; overlap: bucketed, launched from gradient hooks during the "
+                         "backward on a side stream inside the step graph; auto: overlap over RCCL, split "
+                         "over gloo")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the all-reduce path at N=1 too (world-size-1 RCCL group): its cost on one GPU")
+    ap.add_argument("--bucket-mb", type=float, default=16.0, help="comm=overlap bucket size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU steps (median; +1 warm-up)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="for rocprofv3 runs")
@@ -387,7 +393,15 @@ def main():
                          f"(rehearse on fewer GPUs with --dist-backend gloo)")
     torch.cuda.set_device(local_rank % ndev)
     device = torch.device("cuda", local_rank % ndev)
-    if world > 1:
+    if args.comm == "auto":
+        args.comm = "overlap" if args.dist_backend == "nccl" else "split"
+    if args.dist_backend == "gloo" and args.comm != "split":
+        raise SystemExit("gloo collectives cannot be captured into a HIP graph: use --comm split")
+    if world == 1 and args.force_comm:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
+    elif world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
@@ -418,7 +432,7 @@ def main():
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)
     trainer = DDPTrainer(model, opt, device, amp_dtype=torch.bfloat16 if args.amp == "bf16" else None,
                          graph=not args.eager, bf16_weights=(args.amp == "bf16" and not args.eager),
-                         comm=args.comm)
+                         comm=args.comm, overlap_bucket_mb=args.bucket_mb, force_comm=args.force_comm)
     images_per_step = args.batch * args.cameras
     loader = None
     if args.data_path == "sampler":
@@ -493,7 +507,9 @@ def main():
                           "global_batch": images_per_step * world, "per_gpu_images": images_per_step,
                           "image_hw": [args.height, args.width], "parallelism": f"dp{world}",
                           "dist_backend": args.dist_backend if world > 1 else None,
-                          "comm": args.comm if world > 1 else None, "data_path": data,
+                          "comm": (f"{args.comm}" + (f" ({args.bucket_mb:g} MB buckets)" if args.comm == "overlap" else "")
+                                   + (" (forced at N=1)" if world == 1 else "")) if (world > 1 or args.force_comm)
+                          else None, "data_path": data,
                           "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
@@ -509,7 +525,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

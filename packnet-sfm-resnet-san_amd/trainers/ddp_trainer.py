@@ -13,7 +13,9 @@ Execution modes:
     gradient into its own graph-static tensor; for world size > 1 they are packed into ONE flat
     fp32 buffer and averaged by RCCL:
       - comm='split': fwd+bwd+pack graph | all_reduce (host-enqueued, async) | Adam graph;
-      - comm='graph': the all_reduce is captured into the same graph (RCCL graph capture).
+      - comm='graph': the all_reduce is captured into the same graph (RCCL graph capture);
+      - comm='overlap': bucketed all-reduce launched from gradient hooks while the backward
+        runs, on a side stream inside the same graph (grad_buckets.py).
     At world size 1 the whole step is one graph.
   * eager: torch DDP (bucketed all-reduce overlapped with backward) — CPU/gloo and debugging;
     `flat=True` runs the graph mode's flat-buffer algebra eagerly.
@@ -48,7 +50,8 @@ def make_optimizer(model, depth_lr=1e-4, pose_lr=1e-4, name="Adam", **kw):
 
 class DDPTrainer:
     def __init__(self, model, optimizer, device, amp_dtype=torch.bfloat16, bucket_cap_mb=64,
-                 check_every=0, graph=None, flat=None, bf16_weights=False, fused_optim=None, comm="split"):
+                 check_every=0, graph=None, flat=None, bf16_weights=False, fused_optim=None, comm="split",
+                 overlap_bucket_mb=16.0, force_comm=False):
         self.device = device
         self.model = model
         self.optimizer = optimizer
@@ -57,9 +60,12 @@ class DDPTrainer:
         self.step_idx = 0
         self.nonfinite = torch.zeros((), device=device)
         self.world = hvd.world_size()
+        # dp: the gradient all-reduce runs (force_comm: also at world size 1, to exercise the
+        # collective path on one device)
+        self.dp = self.world > 1 or force_comm
         self.use_graph = (device.type == "cuda") if graph is None else graph
-        if comm not in ("split", "graph"):
-            raise ValueError(f"comm must be 'split' or 'graph', got {comm!r}")
+        if comm not in ("split", "graph", "overlap"):
+            raise ValueError(f"comm must be 'split', 'graph' or 'overlap', got {comm!r}")
         self.comm = comm
         # flat: gradients packed into one flat buffer + one all-reduce per step (the graph mode's
         # algebra; also runnable eagerly, e.g. on CPU/gloo for tests)
@@ -77,6 +83,17 @@ class DDPTrainer:
             else:
                 from .mixed_precision import Bf16MasterWeights
                 self.mp = Bf16MasterWeights(model, optimizer, dtype=amp_dtype or torch.bfloat16)
+        # comm='overlap': gradient hooks feed the all-reduce buckets; the first backward only
+        # records the order gradients become ready (the buckets' launch order)
+        self.buckets, self._ready_order, self._capturing = None, None, False
+        self.overlap = comm == "overlap" and self.flat and self.dp
+        if self.overlap:
+            if self.mp is not None:
+                raise NotImplementedError("comm='overlap' needs the fused optimizer or fp32 weights")
+            self.overlap_bytes = int(overlap_bucket_mb * (1 << 20))
+            self._ready_order = []
+            for p in self.params:
+                p.register_post_accumulate_grad_hook(self._grad_ready)
         # BatchNorm step counters: host-side while graphs replay (see _detach_bn_counters)
         self._bn, self._bn_step0 = [], 0
         if self.flat:
@@ -129,6 +146,27 @@ class DDPTrainer:
             self.flat_grad.mul_(scale)
         torch._foreach_copy_(grads, views)
 
+    def _grad_ready(self, p):
+        if self.buckets is not None:
+            self.buckets.on_grad(p)
+        elif self._ready_order is not None:
+            self._ready_order.append(p)
+
+    def _build_buckets(self):
+        from .grad_buckets import GradBuckets
+        if self.fused is not None:
+            ps = [p for p in self.fused.params if p.grad is not None]
+            offs = [self.fused.offsets[self.fused._index[id(p)]] for p in ps]
+        else:
+            ps, _ = self._grads()
+            offs, o = [], 0
+            for p in ps:
+                offs.append(o)
+                o += p.numel()
+        self.buckets = GradBuckets(ps, offs, self.flat_grad, self.overlap_bytes, self.device,
+                                   fused=self.fused, order=self._ready_order)
+        self._ready_order = None
+
     def autocast(self):
         if self.amp_dtype is None or self.device.type != "cuda":
             return contextlib.nullcontext()
@@ -139,7 +177,13 @@ class DDPTrainer:
         with self.autocast():
             output = self.ddp(batch, progress=progress)
         loss = output["loss"]
+        if self.buckets is not None:
+            self.buckets.arm(self._capturing)
+        elif self._ready_order is not None:
+            self._ready_order.clear()
         loss.sum().backward()
+        if self.buckets is not None:   # join the bucket all-reduces launched during the backward
+            self.buckets.finish()
         # sticky non-finite flag in one launch: 0 * loss is 0 for a finite loss, NaN otherwise
         # (the isfinite / any / cast / add chain was five kernels at the end of every step)
         ld = loss.detach()
@@ -150,7 +194,9 @@ class DDPTrainer:
 
     def _opt_step(self, capturing=False):
         if self.fused is not None:  # world > 1: Adam reads the all-reduced flat buffer directly
-            if self.world > 1:
+            if self.dp:
+                if self.buckets is not None:  # bucket packs bound their own tables
+                    self.fused.bind(capturing)
                 self.fused.step(self.flat_grad, 1.0 / self.world, capturing)
             else:
                 self.fused.step(None, 1.0, capturing)
@@ -230,16 +276,23 @@ class DDPTrainer:
         # addresses, no accumulate kernels); every replay rewrites them
         self._zero_grad()
         inv_world = 1.0 / self.world
-        if self.world == 1 or self.comm == "graph":
+        if not self.dp or self.comm in ("graph", "overlap"):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.static_output = self._forward_backward(static_batch, progress)
-                if self.world > 1:
-                    self._pack(capturing=True)
-                    dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-                    if self.fused is None:
-                        self._unpack(inv_world)
-                self._opt_step(capturing=True)
+            self._capturing = True
+            try:
+                with torch.cuda.graph(g):
+                    self.static_output = self._forward_backward(static_batch, progress)
+                    if self.buckets is not None:
+                        if self.fused is None:
+                            self.buckets.unpack(inv_world)
+                    elif self.dp:
+                        self._pack(capturing=True)
+                        dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+                        if self.fused is None:
+                            self._unpack(inv_world)
+                    self._opt_step(capturing=True)
+            finally:
+                self._capturing = False
             self.graphs = (g,)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
@@ -253,6 +306,8 @@ class DDPTrainer:
             self.graphs = (g1, g2)
         if self.fused is not None:  # gradient addresses of the captured graph -> kernel tables
             self.fused.finish_capture()
+        if self.buckets is not None:
+            self.buckets.finish_capture()
         self._captured_n = self._scale_count(progress)
         self._captured_lr = [g["lr"] for g in self.optimizer.param_groups]
 
@@ -312,11 +367,18 @@ class DDPTrainer:
             self.optimizer.zero_grad(set_to_none=True)
 
     def _allreduce(self):
-        if self.world > 1:
-            self._pack()
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+        if not self.dp:
+            return
+        if self.buckets is not None:  # reduced bucket by bucket during the backward
             if self.fused is None:
-                self._unpack(1.0 / self.world)
+                self.buckets.unpack(1.0 / self.world)
+            return
+        self._pack()
+        dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+        if self.fused is None:
+            self._unpack(1.0 / self.world)
+        if self.overlap and self._ready_order:   # first backward seen: cut the buckets
+            self._build_buckets()
 
     # ------------------------------------------------------------------------------------------
     def train_step(self, batch, progress=0.0):
@@ -364,7 +426,7 @@ class DDPTrainer:
 
     def check_finite(self):
         flag = self.nonfinite.clone()
-        if self.world > 1 and dist.is_initialized():
+        if self.dp and dist.is_initialized():
             dist.all_reduce(flag)
         if not math.isfinite(float(flag)):
             raise ValueError(f"Non-finite loss within the last steps (step {self.step_idx})")

@@ -62,6 +62,7 @@ class FusedMixedAdam:
                 inits.append((off, init))
                 off += (p.numel() + 3) // 4 * 4
         self.total = off
+        self._index = {id(p): k for k, p in enumerate(self.params)}
         f32 = dict(device=device, dtype=torch.float32)
         self.master = torch.zeros(off, **f32)
         for o, init in inits:
@@ -96,18 +97,8 @@ class FusedMixedAdam:
     def bind(self, capturing=False):
         """Describe the current gradients to the kernel (parameters without a gradient are
         skipped, like torch.optim.Adam).  Inside a graph capture the upload is deferred."""
-        rows, numels = [], []
-        for p, gi, off in zip(self.params, self.groups, self.offsets):
-            g = p.grad
-            if g is None:
-                continue
-            if g.dtype not in (torch.float32, torch.bfloat16) or g.stride() != p.stride():
-                raise RuntimeError(f"fused Adam: gradient {g.dtype} {g.stride()} vs parameter {p.stride()}")
-            storage_flat(g)
-            flags = (GRAD_BF16 if g.dtype == torch.bfloat16 else 0) | \
-                    (PARAM_BF16 if p.dtype == torch.bfloat16 else 0)
-            rows.append((g.data_ptr(), p.data_ptr(), p.numel(), off, gi, flags))
-            numels.append(p.numel())
+        rows = self.rows_for(self.params)
+        numels = [r[2] for r in rows]
         table = np.array(rows, dtype=TENSOR_DT)
         key = tuple(numels), tuple(r[3] for r in rows)
         if key != self._bound_key:
@@ -129,6 +120,23 @@ class FusedMixedAdam:
             self._pending = blob
         else:
             self.table[:blob.numel()].copy_(blob)
+
+    def rows_for(self, params):
+        """Table rows (grad, param, numel, offset, group, flags) of those of `params` that have a
+        gradient, in the given order."""
+        rows = []
+        for p in params:
+            g = p.grad
+            if g is None:
+                continue
+            k = self._index[id(p)]
+            if g.dtype not in (torch.float32, torch.bfloat16) or g.stride() != p.stride():
+                raise RuntimeError(f"fused Adam: gradient {g.dtype} {g.stride()} vs parameter {p.stride()}")
+            storage_flat(g)
+            flags = (GRAD_BF16 if g.dtype == torch.bfloat16 else 0) | \
+                    (PARAM_BF16 if p.dtype == torch.bfloat16 else 0)
+            rows.append((g.data_ptr(), p.data_ptr(), p.numel(), self.offsets[k], self.groups[k], flags))
+        return rows
 
     def finish_capture(self):
         if self._pending is not None:

@@ -1,5 +1,6 @@
 """Multi-process data-parallel logic on CPU (gloo, world size 2): the trainer's gradient
-averaging (flat-buffer all-reduce = the graph mode's algebra, and torch-DDP eager mode) must give
+averaging (flat-buffer all-reduce = the graph mode's algebra, the bucketed all-reduce launched from
+gradient hooks during the backward (comm='overlap'), and torch-DDP eager mode) must give
 every rank the same parameters, equal to a single process stepping on the averaged gradient."""
 import os
 import tempfile
@@ -42,15 +43,19 @@ def _worker(rank, world, init_file, mode, out_dir):
     torch.manual_seed(0)
     model = TinyModel()
     opt = make_optimizer(model, 1e-2, 1e-2)
-    tr = DDPTrainer(model, opt, torch.device("cpu"), amp_dtype=None, graph=False, flat=(mode == "flat"))
+    kw = dict(comm="overlap", overlap_bucket_mb=300 / 2 ** 20) if mode == "overlap" else {}
+    tr = DDPTrainer(model, opt, torch.device("cpu"), amp_dtype=None, graph=False, flat=(mode != "ddp"), **kw)
     for _ in range(3):
         tr.train_step(_batch(rank))
+    if mode == "overlap":   # the first step cut the buckets; steps 2-3 reduced them during the backward
+        assert tr.buckets is not None and len(tr.buckets.buckets) >= 3, tr.buckets
+        assert sorted(tr.buckets.launch_order) == list(range(len(tr.buckets.buckets)))
     torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["flat", "ddp"])
+@pytest.mark.parametrize("mode", ["flat", "ddp", "overlap"])
 def test_two_rank_gradient_average(mode):
     world = 2
     with tempfile.TemporaryDirectory() as d:

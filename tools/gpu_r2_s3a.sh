@@ -1,0 +1,27 @@
+#!/bin/bash
+# session-3 re-entry check: whole GPU suite, smoke, default bench (with the CPU baseline), rocprof kernel stats
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/s3a; rm -rf "$OUT"; mkdir -p "$OUT"
+export TMPDIR=/tmp
+export MIOPEN_USER_DB_PATH=/tmp/miopen_udb MIOPEN_CUSTOM_CACHE_DIR=/tmp/miopen_cache
+mkdir -p $MIOPEN_USER_DB_PATH $MIOPEN_CUSTOM_CACHE_DIR
+(for i in $(seq 1 80); do date >> "$OUT/heartbeat.txt"; sleep 15; done) & hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
+cd "$ROOT"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1; rc=$?
+echo "[tests] rc=$rc"; grep -E "FAILED|ERROR|passed|failed" "$OUT/gpu_tests.log" | tail -6
+case $rc in 0) ;; *) exit $rc;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
+echo "[smoke] rc=$rc"; tail -6 "$OUT/smoke.log"
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+echo "[bench] rc=$rc"; cut -c1-400 "$OUT/bench.json"
+[ $rc -ne 0 ] && exit $rc
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+   -- python3 "$ROOT/bench.py" --steps 6 --warmup 5 --no-cpu-baseline) > "$OUT/prof.log" 2>&1; rc=$?
+echo "[prof] rc=$rc"
+[ $rc -ne 0 ] && exit $rc
+cp "$OUT"/prof/run_kernel_stats.csv "$OUT/kernel_stats.csv" 2>/dev/null || find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+python3 tools/summarize_trace.py "$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)" "$OUT/step_timeline.txt" && tail -1 "$OUT/step_timeline.txt"
+rm -rf "$OUT/prof"
