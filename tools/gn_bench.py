@@ -1,6 +1,6 @@
 """Fused GroupNorm + ELU (psfm_gn_act) at the layer shapes of a PackNet step: records every
 gn_act call of one forward of the configured depth net, then times each distinct shape's forward
-(stats + apply) and backward (stats + apply) as HIP graph replays between HIP events, and prints
+(stats + apply) and backward (stats + apply) between HIP events, and prints
 the algorithmic HBM bytes per pass and the fraction of 8 TB/s.
   python tools/gn_bench.py [--depth-net PackNet01] [--batch 6] [--iters 20]
 Algorithmic bytes (bf16 activations, 2 B/elem; residual r where the layer has one):
@@ -8,12 +8,14 @@ Algorithmic bytes (bf16 activations, 2 B/elem; residual r where the layer has on
   bwd: stats reads dy, x (+r), apply reads dy, x (+r), writes dx (+dr) -> (4 + 2r + 1 + r) * 2 B/elem"""
 import argparse
 import collections
+import faulthandler
 import json
 import os
 import sys
 
 import torch
 
+faulthandler.enable()
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 ap = argparse.ArgumentParser()
@@ -62,24 +64,20 @@ FU.gn_act = rec
 b = bench.synthetic_batch(1, args.height, args.width, torch.device("cpu"), seed=0)
 with torch.no_grad():
     model.depth_net(b["rgb"])
+print(f"{sum(calls.values())} gn_act calls, {len(calls)} shapes", flush=True)
 
 
 def timed(fn):
+    """HIP events around args.iters back-to-back eager calls (the launches queue ahead of the GPU
+    for the large shapes; small shapes are an upper bound — rocprofv3 kernel stats give the kernel
+    time alone)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g, stream=s):
-            for _ in range(args.iters):
-                fn()
-    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    g.replay()
     e0.record()
-    g.replay()
+    for _ in range(args.iters):
+        fn()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1e3 / args.iters
