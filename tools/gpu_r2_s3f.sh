@@ -1,0 +1,18 @@
+#!/bin/bash
+# whole GPU suite (incl. the capture-fallback test), smoke, default bench
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/s3f; rm -rf "$OUT"; mkdir -p "$OUT"
+export TMPDIR=/tmp
+export MIOPEN_USER_DB_PATH=/tmp/miopen_udb MIOPEN_CUSTOM_CACHE_DIR=/tmp/miopen_cache
+mkdir -p $MIOPEN_USER_DB_PATH $MIOPEN_CUSTOM_CACHE_DIR
+(for i in $(seq 1 80); do date >> "$OUT/heartbeat.txt"; sleep 15; done) & hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
+cd "$ROOT"
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1; rc=$?
+echo "[tests] rc=$rc"; grep -E "FAILED|ERROR|passed|failed" "$OUT/gpu_tests.log" | tail -8
+[ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
+echo "[smoke] rc=$rc"; tail -2 "$OUT/smoke.log"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+echo "[bench] rc=$rc"; cut -c1-200 "$OUT/bench.json"
