@@ -88,11 +88,11 @@ def parse(argv=None):
     ap.add_argument("--amp", default=None, choices=["bf16", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N>1 on one GPU (ranks share the device, host all-reduce)")
-    ap.add_argument("--comm", default="auto", choices=["auto", "split", "graph", "overlap"],
-                    help="split: all_reduce between two graph replays; graph: captured into the step graph "
-                         "after the backward; overlap: bucketed, launched from gradient hooks during the "
-                         "backward on a side stream inside the step graph; auto: overlap over RCCL, split "
-                         "over gloo")
+    ap.add_argument("--comm", default="split", choices=["split", "graph", "overlap"],
+                    help="split: all_reduce between two graph replays (default: no collective inside a "
+                         "graph); graph: captured into the step graph after the backward; overlap: "
+                         "bucketed, launched from gradient hooks during the backward on a side stream "
+                         "inside the step graph")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the all-reduce path at N=1 too (world-size-1 RCCL group): its cost on one GPU")
     ap.add_argument("--bucket-mb", type=float, default=16.0, help="comm=overlap bucket size")
@@ -393,8 +393,6 @@ def main():
                          f"(rehearse on fewer GPUs with --dist-backend gloo)")
     torch.cuda.set_device(local_rank % ndev)
     device = torch.device("cuda", local_rank % ndev)
-    if args.comm == "auto":
-        args.comm = "overlap" if args.dist_backend == "nccl" else "split"
     if args.dist_backend == "gloo" and args.comm != "split":
         raise SystemExit("gloo collectives cannot be captured into a HIP graph: use --comm split")
     if world == 1 and args.force_comm:

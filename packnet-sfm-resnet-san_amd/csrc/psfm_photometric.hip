@@ -795,13 +795,21 @@ __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
     const float* x = pick4(a.sig, s) + (size_t)b * (a.plane >> (2 * sh));
     const uint32_t W = (uint32_t)a.W, Ws = W >> sh;
     float v[1] = {0.0f};
-    if (sh == 0) {
-        for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) v[0] += x[i];
-    } else {
-        for (uint32_t i = lo + threadIdx.x; i < hi; i += NT) {
-            const uint32_t y = i / W, c = i - y * W;
-            v[0] += x[(y >> sh) * Ws + (c >> sh)];
+    // 8 loads in flight per thread, then the adds in the plain loop's order (i = lo + tid, + NT, ...)
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * NT) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t i = i0 + u * NT;
+            if (sh == 0) {
+                t[u] = i < hi ? x[i] : 0.0f;
+            } else {
+                const uint32_t y = i / W, c = i - y * W;
+                t[u] = i < hi ? x[(y >> sh) * Ws + (c >> sh)] : 0.0f;
+            }
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[0] += t[u];
     }
     block_sum<1>(v, red);
     if (threadIdx.x == 0) a.part[((size_t)s * a.B + b) * fused::SIGCH + ch] = v[0];

@@ -27,9 +27,8 @@ not on the hot path: the non-finite check accumulates on the device, tested ever
 `check_every` steps.
 """
 import contextlib
-import gc
 import math
-import warnings
+import gc
 
 import torch
 import torch.distributed as dist
@@ -277,28 +276,25 @@ class DDPTrainer:
         # addresses, no accumulate kernels); every replay rewrites them
         self._zero_grad()
         inv_world = 1.0 / self.world
-        self.graphs = None
         if not self.dp or self.comm in ("graph", "overlap"):
-            failed = None
+            g = torch.cuda.CUDAGraph()
+            self._capturing = True
             try:
-                self.graphs = (self._capture_one(static_batch, progress, inv_world),)
-            except RuntimeError as e:
-                if not self.dp:
-                    raise
-                failed = e
-            if self.dp and self._any_rank(failed is not None):
-                # a collective that cannot be captured on this system: every rank falls back
-                # together to the host-enqueued all-reduce between two graphs
-                warnings.warn(f"comm={self.comm!r}: capturing the all-reduce into the step graph failed "
-                              f"({failed if failed is not None else 'on another rank'}); using comm='split'")
-                self.comm, self.overlap, self.buckets, self.graphs = "split", False, None, None
-                self.static_output = None
-                if self.fused is not None:
-                    self.fused._pending = None
-                torch.cuda.synchronize(self.device)
-                gc.collect()
-                self._zero_grad()
-        if self.graphs is None:
+                with torch.cuda.graph(g):
+                    self.static_output = self._forward_backward(static_batch, progress)
+                    if self.buckets is not None:
+                        if self.fused is None:
+                            self.buckets.unpack(inv_world)
+                    elif self.dp:
+                        self._pack(capturing=True)
+                        dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+                        if self.fused is None:
+                            self._unpack(inv_world)
+                    self._opt_step(capturing=True)
+            finally:
+                self._capturing = False
+            self.graphs = (g,)
+        else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):
                 self.static_output = self._forward_backward(static_batch, progress)
@@ -314,34 +310,6 @@ class DDPTrainer:
             self.buckets.finish_capture()
         self._captured_n = self._scale_count(progress)
         self._captured_lr = [g["lr"] for g in self.optimizer.param_groups]
-
-    def _capture_one(self, static_batch, progress, inv_world):
-        """The whole step (and, for comm 'graph' / 'overlap', its all-reduce) as one graph."""
-        g = torch.cuda.CUDAGraph()
-        self._capturing = True
-        try:
-            with torch.cuda.graph(g):
-                self.static_output = self._forward_backward(static_batch, progress)
-                if self.buckets is not None:
-                    if self.fused is None:
-                        self.buckets.unpack(inv_world)
-                elif self.dp:
-                    self._pack(capturing=True)
-                    dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-                    if self.fused is None:
-                        self._unpack(inv_world)
-                self._opt_step(capturing=True)
-        finally:
-            self._capturing = False
-        return g
-
-    def _any_rank(self, flag):
-        if not (dist.is_available() and dist.is_initialized()):
-            return flag
-        dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([1.0 if flag else 0.0], device=dev)
-        dist.all_reduce(t)
-        return float(t) > 0
 
     def _scale_count(self, progress):
         loss = getattr(self.model, "_photometric_loss", None)

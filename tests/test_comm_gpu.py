@@ -91,34 +91,3 @@ def test_overlap_step_equals_single_allreduce_step(rccl_world1):
         assert len(to.buckets.buckets) >= 4
     finally:
         torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = old
-
-
-def test_failed_collective_capture_falls_back_to_split(rccl_world1, monkeypatch):
-    """A collective that cannot be captured (simulated: the first bucket launch raises while the
-    step is being captured) makes every rank fall back to comm='split' (two graphs, host-enqueued
-    all-reduce), and the step still reduces and applies every gradient."""
-    import warnings
-    from packnet_sfm_amd.trainers import grad_buckets as GB
-    dev = rccl_world1
-    m, t, bench = _trainer(dev, "overlap", fp32=False)
-    orig = GB.GradBuckets._launch
-
-    def flaky(self, b):
-        if self.capturing:
-            raise RuntimeError("simulated: collective not capturable")
-        return orig(self, b)
-    monkeypatch.setattr(GB.GradBuckets, "_launch", flaky)
-    batches = [bench.synthetic_batch(2, 64, 192, dev, seed=s, channels_last=True) for s in range(2)]
-    static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in batches[0].items()}
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        t.train_step(static)
-    assert any("using comm='split'" in str(x.message) for x in w)
-    assert t.comm == "split" and len(t.graphs) == 2 and t.buckets is None
-    t.train_step(batches[1])
-    torch.cuda.synchronize()
-    fresh = t.fused.new_flat_grad()
-    t.fused.pack(fresh)
-    torch.cuda.synchronize()
-    assert torch.equal(fresh, t.flat_grad)
-    assert int(t.fused.step_count) == 2
