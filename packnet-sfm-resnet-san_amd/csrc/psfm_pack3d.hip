@@ -9,8 +9,9 @@
 // pixel-shuffled output element exactly once, straight into the caller's layout (strides).
 //   k_p3d_fwd      y  = conv3d(V)            4 x 16 pixels x 32 k per chunk, thread = pixel x 8 k
 //                                            (d x 8 register outputs, 16-byte stores)
-//   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: 4 x 16 pixels x 16 k,
-//                                            16-byte staged halo tile, 4 pixels per thread
+//   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: one 4 x 16 pixel x 16 k
+//                                            chunk per workgroup (XCD-aware order), o in passes
+//                                            of 4, thread = 4 pixels x a k pair (packed f32)
 //   k_p3d_bwd_x    dV = conv3d^T(dy)         any other layout: 4 x 8 pixels x 16 k
 //   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (spatial shift, pixel group), ND x 3
 //                  register partials; 16-byte dy staging for channels_last pack layers), fixed-order
@@ -35,6 +36,7 @@ int fail(int code, const std::string& msg) {
 }
 
 constexpr int NTH = 256;
+typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
 // ND: Conv3d output features d — 8 (PackNet01) or 4 (PackNetSAN01, num_3d_feat = 4)
 
@@ -310,37 +312,47 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))
     }
 }
 
-// --------------------------------------------------------------------------------------------
-// dx for PACK with a channel-contiguous dy (channels_last: the folded channel o K + k is the
-// innermost index — the layout the nets run in).  Per 4 x 16 pixels x 16 k chunk the dy halo tile
-// (6 x 18 pixels x ND x 18 k) is staged with 16-byte loads (every load of a thread issued before
-// the first LDS write) into fp32 LDS [yy][xx][o][pos], pos = k - k0 + 2; each thread then
-// computes 4 neighbouring pixels of one k (register blocking along x: 6 LDS reads per 12 FMAs;
-// the per-pixel stride is 4 mod 8 words, so the x-blocked reads of a half-wave hit 32 distinct
-// banks).  Weights are wave-uniform and come through the scalar path (SGPR operands).
+// dV of a channels_last pack layer, k-pair form: 128 threads, thread = 4 neighbouring pixels x TWO
+// consecutive k of a 4 x 16 pixel x 16 k chunk, both k in the halves of packed f32 pairs.  The
+// per-(pixel, o) run is stored from k0-1 (index 0) so that the four values (k-1, k, k+1, k+2) a
+// thread needs per pixel column are two aligned 8-byte LDS reads: (k-1, k) and (k+1, k+2) are the
+// dz = 2 and dz = 0 operand pairs, (k, k+1) the dz = 1 pair — 12 ds_read_b64 feed 36 v_pk_fma_f32
+// (72 MACs) per (o, dy) where the one-k form spent 18 ds_read_b32 on 36 MACs.
+// One 16-k chunk per workgroup on an XCD-aware 1-D grid: a 128-byte line of a (pixel, o) dy run
+// holds 64 k = four chunks, and the four workgroups that read it run back to back on ONE XCD (the
+// grid's workgroup w goes to XCD w % 8; logical index = w's rank within its XCD, chunk fastest),
+// so the line is fetched into that XCD's L2 once instead of once per chunk.
 template <typename T, int ND>
-__global__ __launch_bounds__(NTH, 2) void k_p3d_bwd_x_cl(P3 a) {
-    constexpr int TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2;
-    constexpr int OS = 20;                // per-o run: pos 1 = k0-1, 2..17 = k0..k0+15, 18 = k0+16
-    constexpr int PS = ND * OS + 4;       // per-pixel stride (4 mod 8)
-    constexpr int VEC = 16 / sizeof(T);   // elements per 16-byte load
-    constexpr int UNITS = LY * LX * ND;   // (pixel, o) runs per chunk
-    constexpr int ITER = (UNITS + NTH - 1) / NTH;
+__global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn) {
+    constexpr int NT2 = 128, TY = 4, TX = 16, DC = 16, LY = TY + 2, LX = TX + 2;
+    constexpr int OP = ND < 4 ? ND : 4;   // o per staging pass: 36 KB of LDS, 4 workgroups per CU
+    constexpr int OS = 20;                // per-o run: index 0 = k0-1, 1..16 = k0..k0+15, 17 = k0+16
+    constexpr int PS = OP * OS + 4;       // per-pixel stride (even: 8-byte aligned pairs)
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int UNITS = LY * LX * OP;
+    constexpr int ITER = (UNITS + NT2 - 1) / NT2;
+    static_assert(ND % OP == 0, "o passes");
     __shared__ __attribute__((aligned(16))) float sg[LY * LX * PS];
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
-    const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
-    const int t = threadIdx.x, dl = t % DC, r = t / DC, py = r / 4, px0 = (r % 4) * 4;
+    const int nch = a.K / DC;
+    int L;
+    {
+        const int n = gridDim.x, w = blockIdx.x, q = n / 8, rm = n % 8, xcd = w % 8, idx = w / 8;
+        L = xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
+    }
+    const int k0 = (L % nch) * DC;
+    const int rest = L / nch, tile = rest % (gxn * gyn), b = rest / (gxn * gyn);
+    const int x0 = (tile % gxn) * TX, y0 = (tile / gxn) * TY;
+    const int t = threadIdx.x, kp = t % 8, r = t / 8, py = r / 4, px0 = (r % 4) * 4;
     const T* dyb = static_cast<const T*>(a.dy) + b * a.ys[0];
     const int ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
-    for (int ch = c_lo; ch < c_hi; ++ch) {
-        const int k0 = ch * DC;
+    f2 acc[4] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+    for (int o0 = 0; o0 < ND; o0 += OP) {
         uint4 v[ITER][DC / VEC];
         float e0[ITER], e1[ITER];
 #pragma unroll
         for (int i = 0; i < ITER; ++i) {
-            const int u = t + i * NTH;
-            const int yy = u / (LX * ND), rem = u - yy * (LX * ND), xx = rem / ND, o = rem - xx * ND;
+            const int u = t + i * NT2;
+            const int yy = u / (LX * OP), rem = u - yy * (LX * OP), xx = rem / OP, o = o0 + rem - xx * OP;
             const int gy = y0 - 1 + yy, gx = x0 - 1 + xx;
             const bool in = u < UNITS && (unsigned)gy < (unsigned)a.Hv && (unsigned)gx < (unsigned)a.Wv;
             const T* src = dyb + (in ? gy * ys2 + gx * ys3 + o * a.K + k0 : 0);
@@ -350,51 +362,69 @@ __global__ __launch_bounds__(NTH, 2) void k_p3d_bwd_x_cl(P3 a) {
             e0[i] = in && k0 > 0 ? ldi<T>(src, -1) : 0.0f;
             e1[i] = in && k0 + DC < a.K ? ldi<T>(src, DC) : 0.0f;
         }
-        __syncthreads();   // the previous chunk's reads of sg are done
+        __syncthreads();   // the previous pass's reads of sg are done
 #pragma unroll
         for (int i = 0; i < ITER; ++i) {
-            const int u = t + i * NTH;
+            const int u = t + i * NT2;
             if (u >= UNITS) break;
-            const int yy = u / (LX * ND), rem = u - yy * (LX * ND), xx = rem / ND, o = rem - xx * ND;
-            float* d = sg + (yy * LX + xx) * PS + o * OS;
-            d[1] = e0[i];
-            d[DC + 2] = e1[i];
-            float2* d2 = reinterpret_cast<float2*>(d + 2);
+            const int yy = u / (LX * OP), rem = u - yy * (LX * OP), xx = rem / OP, o = rem - xx * OP;
+            float2* d2 = reinterpret_cast<float2*>(sg + (yy * LX + xx) * PS + o * OS);
+            float f[DC];
 #pragma unroll
             for (int j = 0; j < DC / VEC; ++j) {
                 const uint32_t w4[4] = {v[i][j].x, v[i][j].y, v[i][j].z, v[i][j].w};
                 if (sizeof(T) == 2) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        d2[j * 4 + q] = make_float2(__uint_as_float(w4[q] << 16), __uint_as_float(w4[q] & 0xffff0000u));
+                    for (int q = 0; q < 4; ++q) {
+                        f[j * 8 + 2 * q] = __uint_as_float(w4[q] << 16);
+                        f[j * 8 + 2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+                    }
                 } else {
-                    d2[j * 2 + 0] = make_float2(__uint_as_float(w4[0]), __uint_as_float(w4[1]));
-                    d2[j * 2 + 1] = make_float2(__uint_as_float(w4[2]), __uint_as_float(w4[3]));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) f[j * 4 + q] = __uint_as_float(w4[q]);
                 }
             }
+            d2[0] = make_float2(e0[i], f[0]);
+#pragma unroll
+            for (int j = 1; j < DC / 2; ++j) d2[j] = make_float2(f[2 * j - 1], f[2 * j]);
+            d2[DC / 2] = make_float2(f[DC - 1], e1[i]);
         }
         __syncthreads();
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll 1
-        for (int o = 0; o < ND; ++o)
+        for (int o = 0; o < OP; ++o)
 #pragma unroll
-            for (int dz = 0; dz < 3; ++dz)
+            for (int dy = 0; dy < 3; ++dy) {
+                const float* g = sg + ((py + 2 - dy) * LX + px0) * PS + o * OS + 2 * kp;
+                f2 pa[6], pb[6], pm[6];   // (k-1, k), (k+1, k+2), (k, k+1) per pixel column
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy) {
-                    const float* g = sg + ((py + 2 - dy) * LX + px0) * PS + o * OS + dl + 3 - dz;
-                    float g6[6];
-#pragma unroll
-                    for (int j = 0; j < 6; ++j) g6[j] = g[j * PS];
-                    const float* w = a.w + o * 27 + (dz * 3 + dy) * 3;
-                    const float w0 = w[0], w1 = w[1], w2 = w[2];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[q] += w0 * g6[q + 2] + w1 * g6[q + 1] + w2 * g6[q];
+                for (int j = 0; j < 6; ++j) {
+                    const float2 lo = *reinterpret_cast<const float2*>(g + j * PS);
+                    const float2 hi = *reinterpret_cast<const float2*>(g + j * PS + 2);
+                    pa[j] = f2{lo.x, lo.y};
+                    pb[j] = f2{hi.x, hi.y};
+                    pm[j] = f2{lo.y, hi.x};
                 }
-        const int k = k0 + dl, gy = y0 + py;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int gx = x0 + px0 + q;
-            if (gy < a.Hv && gx < a.Wv) st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k, gy, gx), acc[q]);
+                for (int dz = 0; dz < 3; ++dz) {
+                    const float* w = a.w + (o0 + o) * 27 + (dz * 3 + dy) * 3;
+                    const f2 w0 = f2{w[0], w[0]}, w1 = f2{w[1], w[1]}, w2 = f2{w[2], w[2]};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const f2 c0 = dz == 0 ? pb[q + 2] : dz == 1 ? pm[q + 2] : pa[q + 2];
+                        const f2 c1 = dz == 0 ? pb[q + 1] : dz == 1 ? pm[q + 1] : pa[q + 1];
+                        const f2 c2 = dz == 0 ? pb[q] : dz == 1 ? pm[q] : pa[q];
+                        acc[q] += w0 * c0 + w1 * c1 + w2 * c2;
+                    }
+                }
+            }
+    }
+    const int k = k0 + 2 * kp, gy = y0 + py;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int gx = x0 + px0 + q;
+        if (gy < a.Hv && gx < a.Wv) {
+            st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k, gy, gx), acc[q].x);
+            st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k + 1, gy, gx), acc[q].y);
         }
     }
 }
@@ -676,13 +706,14 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
                         a.ys[0] % vec == 0 && a.ys[2] % vec == 0 && a.ys[3] % vec == 0 &&
                         (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
         if (cl) {
-            const dim3 grid = grid_of(a, 4, 16, 16);
+            const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
+            const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / 16)));   // one 16-k chunk per workgroup
             if (t->dtype == PSFM_P3D_BF16) {
-                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 4>), grid, dim3(NTH), 0, st, a);
-                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 8>), grid, dim3(NTH), 0, st, a);
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 4>), g1, dim3(128), 0, st, a, gxn, gyn);
+                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<uint16_t, 8>), g1, dim3(128), 0, st, a, gxn, gyn);
             } else {
-                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 4>), grid, dim3(NTH), 0, st, a);
-                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 8>), grid, dim3(NTH), 0, st, a);
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 4>), g1, dim3(128), 0, st, a, gxn, gyn);
+                else hipLaunchKernelGGL((k_p3d_bwd_x_cl<float, 8>), g1, dim3(128), 0, st, a, gxn, gyn);
             }
         } else {
             const dim3 grid = grid_of(a, 4, 8, 16);
