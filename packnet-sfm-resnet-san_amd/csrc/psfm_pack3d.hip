@@ -92,6 +92,10 @@ __device__ __forceinline__ float ldi<uint16_t>(const uint16_t* p, int i) {
 template <int MODE>
 __device__ __forceinline__ int64_t vaddr(const P3& a, int b, int k, int y, int x) {
     if (MODE == PSFM_P3D_PACK) {
+        if (a.r == 2) {   // every PackNet layer (wave-uniform): shifts instead of integer divisions
+            const int c = k >> 2, i = (k >> 1) & 1, j = k & 1;
+            return b * a.xs[0] + c * a.xs[1] + (int64_t)(2 * y + i) * a.xs[2] + (int64_t)(2 * x + j) * a.xs[3];
+        }
         const int rr = a.r * a.r, c = k / rr, q = k - c * rr, i = q / a.r, j = q - i * a.r;
         return b * a.xs[0] + c * a.xs[1] + (int64_t)(y * a.r + i) * a.xs[2] + (int64_t)(x * a.r + j) * a.xs[3];
     }
@@ -103,6 +107,10 @@ __device__ __forceinline__ int64_t yaddr(const P3& a, int b, int o, int k, int y
     const int q = o * a.K + k;
     if (MODE == PSFM_P3D_PACK)
         return b * a.ys[0] + q * a.ys[1] + (int64_t)y * a.ys[2] + (int64_t)x * a.ys[3];
+    if (a.r == 2) {
+        const int c = q >> 2, i = (q >> 1) & 1, j = q & 1;
+        return b * a.ys[0] + c * a.ys[1] + (int64_t)(2 * y + i) * a.ys[2] + (int64_t)(2 * x + j) * a.ys[3];
+    }
     const int rr = a.r * a.r, c = q / rr, s = q - c * rr, i = s / a.r, j = s - i * a.r;
     return b * a.ys[0] + c * a.ys[1] + (int64_t)(y * a.r + i) * a.ys[2] + (int64_t)(x * a.r + j) * a.ys[3];
 }
