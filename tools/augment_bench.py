@@ -27,9 +27,12 @@ ap.add_argument("--shape", default="192x640")
 ap.add_argument("--cpu-seconds", type=float, default=10.0)
 ap.add_argument("--no-cpu-baseline", action="store_true")
 ap.add_argument("--jitter", default="0.2,0.2,0.2,0.05", help="'none' = no colour jitter (rgb = copy)")
+ap.add_argument("--lib", default=None, help="alternative build of libpsfm_hip.so (A/B)")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
+if args.lib:
+    _hip.LIB_PATH, _hip._lib = args.lib, None
 from packnet_sfm_amd.datasets import augmentations as AUG  # noqa: E402
 
 dev = torch.device("cuda:0")
