@@ -32,7 +32,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = True
-    model = bench.build_model(ns, dev).to(memory_format=torch.channels_last)
+    model = bench.to_channels_last(bench.build_model(ns, dev))
     opt = make_optimizer(model, 1e-4, 1e-4, fused=True)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=True)
     tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16, graph=False, flat=True, bf16_weights=True)
