@@ -6,7 +6,7 @@ import torch.nn as nn
 
 from ...utils.image import UpsampleNearest
 from ..layers.packnet.layers01 import (Conv2D, InvDepth, PackLayerConv3d, ResidualBlock,
-                                       UnpackLayerConv3d)
+                                       UnpackLayerConv3d, merge_cat)
 
 
 class PackNet01(nn.Module):
@@ -72,7 +72,7 @@ class PackNet01(nn.Module):
             parts = [unpacked + skip]
         if disp is not None:
             parts.append(disp)
-        return parts[0] if len(parts) == 1 else torch.cat(parts, 1)
+        return merge_cat(parts)
 
     def forward(self, rgb):
         x = self.pre_calc(rgb)

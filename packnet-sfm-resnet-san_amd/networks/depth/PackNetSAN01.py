@@ -18,7 +18,7 @@ import torch.nn as nn
 
 from ...utils.image import UpsampleNearest
 from ..layers.packnet.layers01 import (Conv2D, InvDepth, PackLayerConv3d, ResidualBlock,
-                                       UnpackLayerConv3d)
+                                       UnpackLayerConv3d, merge_cat)
 
 
 class Encoder(nn.Module):
@@ -84,7 +84,7 @@ class Decoder(nn.Module):
             parts = [unpacked + skip]
         if disp is not None:
             parts.append(disp)
-        return parts[0] if len(parts) == 1 else torch.cat(parts, 1)
+        return merge_cat(parts)
 
     def forward(self, x5p, skips):
         skip1, skip2, skip3, skip4, skip5 = skips

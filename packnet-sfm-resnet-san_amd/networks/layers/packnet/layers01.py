@@ -76,6 +76,33 @@ class InvDepth(nn.Module):
         return self.activ(self.conv1(self.pad(x))) / self.min_depth
 
 
+def _channels_last_view(t):
+    """t with channels_last strides: a view for a contiguous one-channel map (its bytes are the
+    same in both layouts), otherwise the layout conversion."""
+    if t.dim() == 4 and t.shape[1] == 1 and t.is_contiguous():
+        _, _, h, w = t.shape
+        return t.as_strided(t.shape, (h * w, 1, w, 1))
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def merge_cat(parts):
+    """torch.cat(parts, 1) of a decoder stage (PackNet01.py / PackNetSAN01.py `_merge`).  Under
+    autocast the reference's cat promotes the bf16 features and the fp32 disparity map to an fp32
+    tensor that the next (autocast) convolution casts straight back to bf16, and the mixed layouts
+    made it NCHW (two more full-size copies before the channels_last convolution).  Casting the
+    parts to the autocast dtype first gives that convolution the identical bf16 input (the bf16
+    parts round-trip exactly, the disparity is rounded once either way) and the same gradients, and
+    with every part channels_last the cat is written in the layout the convolution reads."""
+    if len(parts) == 1:
+        return parts[0]
+    x0 = parts[0]
+    if (x0.is_cuda and x0.dim() == 4 and torch.is_autocast_enabled("cuda")
+            and x0.dtype == torch.get_autocast_dtype("cuda")
+            and x0.is_contiguous(memory_format=torch.channels_last)):
+        return torch.cat([_channels_last_view(p.to(x0.dtype)) for p in parts], 1)
+    return torch.cat(parts, 1)
+
+
 def packing(x, r=2):
     """[B,C,H,W] -> [B,C*r*r,H/r,W/r]; channel index = c*r*r + dy*r + dx (inverse of PixelShuffle)."""
     b, c, h, w = x.shape
