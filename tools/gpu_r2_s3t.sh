@@ -12,6 +12,7 @@ trap 'kill $hb 2>/dev/null' EXIT
 cd "$ROOT"
 bash tools/gpu_pmc_bench.sh > "$OUT/pmc.log" 2>&1; rc=$?
 echo "[pmc] rc=$rc"; tail -3 "$OUT/pmc.log"; [ $rc -ne 0 ] && exit $rc
+cp "$ROOT"/gpurun_out/pmc/*.json "$OUT/" && rm -rf "$ROOT"/gpurun_out/pmc   # raw passes exceed the copy-back cap
 (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
    -- python3 "$ROOT/bench.py" --config kitti-packnet --steps 8 --warmup 4 --no-cpu-baseline --no-kernel-timing) > "$OUT/prof.log" 2>&1; rc=$?
 echo "[prof packnet] rc=$rc"; [ $rc -ne 0 ] && exit $rc
