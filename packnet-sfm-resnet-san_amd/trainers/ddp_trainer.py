@@ -67,6 +67,11 @@ class DDPTrainer:
         if comm not in ("split", "graph", "overlap"):
             raise ValueError(f"comm must be 'split', 'graph' or 'overlap', got {comm!r}")
         self.comm = comm
+        if comm != "split" and self.world > 1:
+            import warnings
+            warnings.warn(f"comm={comm!r} captures the RCCL collectives into the step graph; with more than one "
+                          "rank this path has no recorded multi-GPU run yet (the default 'split' keeps the "
+                          "all-reduce outside the graphs)", RuntimeWarning, stacklevel=2)
         # flat: gradients packed into one flat buffer + one all-reduce per step (the graph mode's
         # algebra; also runnable eagerly, e.g. on CPU/gloo for tests)
         self.flat = self.use_graph if flat is None else (flat or self.use_graph)
@@ -340,9 +345,10 @@ class DDPTrainer:
                                                  device=m.running_mean.device)
 
     def state_dict(self):
-        """model.state_dict() in the reference checkpoint format (model_checkpoint.py:66-76
-        'state_dict'): fp32 master weights in place of the bf16 working copies, and every
-        BatchNorm `num_batches_tracked` present and current."""
+        """The SfmModel's own state_dict (keys 'depth_net.…' / 'pose_net.…', the layout
+        SfmModel.load_state_dict takes) with fp32 master weights in place of the bf16 working
+        copies and every BatchNorm `num_batches_tracked` present and current.  The reference's
+        checkpoint FILE wraps ModelWrapper keys ('model.depth_net.…'): see checkpoint()."""
         sd = self.model.state_dict()
         names = {id(m): n for n, m in self.model.named_modules()}
         for m, base in self._bn:
@@ -357,6 +363,17 @@ class DDPTrainer:
                 for p, m in zip(self.mp.lp, self.mp.master):
                     sd[pname[id(p)]] = m.detach().clone()
         return sd
+
+    def checkpoint(self, config=None, epoch=0, scheduler=None):
+        """The dict the reference's ModelCheckpoint saves (models/model_checkpoint.py:66-76):
+        {'config', 'epoch', 'state_dict', 'optimizer', 'scheduler'} with 'state_dict' keyed as
+        ModelWrapper.state_dict() is — the SfmModel under 'model.' — so utils/load.py
+        load_network(net, ckpt['state_dict'], 'depth_net') strips the prefix as for a reference
+        checkpoint.  Written with torch.save(), it loads with weights_only=True."""
+        sd = {"model." + k: v.detach().cpu() for k, v in self.state_dict().items()}
+        return {"config": config, "epoch": int(epoch), "state_dict": sd,
+                "optimizer": self.optimizer.state_dict(),
+                "scheduler": scheduler.state_dict() if scheduler is not None else None}
 
     def _zero_grad(self):
         """Model grads -> None (autograd then owns fresh, graph-static tensors); the fp32 master

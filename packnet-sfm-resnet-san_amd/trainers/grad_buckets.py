@@ -58,11 +58,27 @@ class GradBuckets:
             self.launch_order = sorted(range(len(self.buckets)), key=lambda b: first.get(b, len(order)))
         else:
             self.launch_order = list(range(len(self.buckets)))[::-1]
+        self.launch_order = self._agree(self.launch_order, device)
         self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.armed = False
         self.capturing = False
         if fused is not None:
             self._plan_tables()
+
+    @staticmethod
+    def _agree(order, device):
+        """Every rank must issue its bucket collectives in ONE order, or the all-reduces pair up
+        different buckets (a hang for different sizes, silently mixed slices for equal ones).
+        Rank 0's learned order is broadcast and adopted by all ranks (as torch DDP broadcasts its
+        rebuilt bucket order)."""
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return order
+        dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor(order, dtype=torch.int64, device=dev)
+        dist.broadcast(t, src=0)
+        agreed = [int(v) for v in t.cpu()]
+        assert sorted(agreed) == sorted(order), "ranks cut different buckets"
+        return agreed
 
     # -------------------------------------------------------------------------------------------
     def _plan_tables(self):
@@ -125,8 +141,11 @@ class GradBuckets:
                                         _hip.ptr(self.flat), _hip.stream(self.device)), "psfm_grad_pack")
         else:
             for k in range(i, j):
-                g, off = self.params[k].grad, self.offsets[k]
-                self.flat[off:off + g.numel()].view_as(g).copy_(g)
+                g, off, p = self.params[k].grad, self.offsets[k], self.params[k]
+                if g is None:   # no gradient this step (e.g. a scale dropped): its slice sums zeros
+                    self.flat[off:off + p.numel()].zero_()
+                else:
+                    self.flat[off:off + g.numel()].view_as(g).copy_(g)
 
     def _launch(self, b):
         self._pack(b)

@@ -196,3 +196,20 @@ def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e
         O.photometric_loss(img, ctx, s_a, Kd, Kd, md, mk, grid_mask=sensitive, **kw)[0].sum().backward()
         bound = np.abs(pose[0] - v.grad.numpy())
     return alts, pose, bound
+
+
+def pose_check_bounded(got, ref64, bound, tol=1e-3):
+    """dL/dpose parity with the flagged pixels' share as the only slack: every entry within
+    tol * max|ref64| + 2 * bound of the float64 oracle `ref64`, where `bound` is how much the
+    flagged (fp32-ambiguous) pixels contribute to that entry (oracle_alternatives(pose_vec=...,
+    sensitive=...)).  Inputs with no flagged pixel get bound = 0: plain tol * max.
+    Returns (ok, stats)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref64, dtype=np.float64)
+    bound = np.zeros_like(ref) if bound is None else np.asarray(bound, dtype=np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    slack = tol * scale + 2.0 * bound
+    ratio = float((np.abs(got - ref) / slack).max())
+    stats = {"rel_err_vs_fp64": float(np.abs(got - ref).max() / scale),
+             "flagged_share_of_max": float(bound.max() / scale), "worst_err_over_allowance": ratio}
+    return ratio <= 1.0, stats

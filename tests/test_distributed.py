@@ -239,3 +239,114 @@ def test_check_finite_flags_a_nonfinite_loss_seen_steps_earlier(bad):
         tr.train_step(_batch(0))
     with pytest.raises(ValueError, match="Non-finite"):
         tr.check_finite()
+
+
+# -------------------------------------------------------------------------------------------------
+# a parameter that stops receiving gradients after the bucket-learning step, and the
+# bucket launch order agreed across ranks
+class DroppingHead(TinyModel):
+    """`extra` contributes to the loss in the first step only (as an inverse-depth head of a scale
+    that ProgressiveScaling drops later): from step 2 on its gradient is None."""
+
+    def __init__(self):
+        super().__init__()
+        self.extra = torch.nn.Linear(3, 1)
+        self.calls = 0
+
+    def forward(self, batch, progress=0.0):
+        out = super().forward(batch, progress)
+        self.calls += 1
+        if self.calls == 1:
+            out["loss"] = out["loss"] + 0.1 * self.extra(batch["rgb"].mean((2, 3))).pow(2).mean()
+        return out
+
+
+def _drop_worker(rank, world, init_file, out_dir):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer
+    torch.manual_seed(0)
+    model = DroppingHead()
+    opt = torch.optim.Adam([{"params": list(model.depth_net.parameters()) + list(model.extra.parameters()),
+                             "lr": 1e-2}, {"params": model.pose_net.parameters(), "lr": 1e-2}])
+    tr = DDPTrainer(model, opt, torch.device("cpu"), amp_dtype=None, graph=False, flat=True, comm="overlap",
+                    overlap_bucket_mb=300 / 2 ** 20)
+    for _ in range(3):
+        tr.train_step(_batch(rank))
+    assert model.extra.weight.grad is None
+    torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlap_buckets_with_a_parameter_that_loses_its_gradient():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_drop_worker, args=(world, os.path.join(d, "init"), d), nprocs=world, join=True)
+        s0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        s1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+    torch.manual_seed(0)
+    ref = DroppingHead()
+    opt = torch.optim.Adam([{"params": list(ref.depth_net.parameters()) + list(ref.extra.parameters()), "lr": 1e-2},
+                            {"params": ref.pose_net.parameters(), "lr": 1e-2}])
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        calls = ref.calls
+        loss = 0
+        for r in range(world):
+            ref.calls = calls   # both ranks see the same step index
+            loss = loss + ref(_batch(r))["loss"].sum()
+        (loss / world).backward()
+        opt.step()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(s0[k], v, atol=1e-6, rtol=1e-5), k
+
+
+def _order_worker(rank, world, init_file, out_dir):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.grad_buckets import GradBuckets
+    ps = [torch.nn.Parameter(torch.zeros(10)) for _ in range(4)]
+    flat = torch.zeros(40)
+    # each rank "observed" a different gradient order in its learning step
+    order = ps[::-1] if rank == 0 else [ps[1], ps[0], ps[3], ps[2]]
+    gb = GradBuckets(ps, [0, 10, 20, 30], flat, 40, torch.device("cpu"), order=order)
+    torch.save(torch.tensor(gb.launch_order), os.path.join(out_dir, f"o{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_launch_order_is_rank0s_on_every_rank():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_order_worker, args=(world, os.path.join(d, "init"), d), nprocs=world, join=True)
+        o = [torch.load(os.path.join(d, f"o{r}.pt"), weights_only=True).tolist() for r in range(world)]
+    assert o[0] == o[1] == [3, 2, 1, 0]
+
+
+def test_checkpoint_round_trips_through_load_network(tmp_path):
+    """DDPTrainer.checkpoint() is the reference's checkpoint dict (model_checkpoint.py:66-76, keys
+    under 'model.'); the reference's prefix-stripping loader (utils/load.py:114-163) restores the
+    depth and pose nets from the saved file."""
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    from packnet_sfm_amd.utils.load import load_network
+    torch.manual_seed(0)
+    model = TinyModel()
+    tr = DDPTrainer(model, make_optimizer(model, 1e-2, 1e-2), torch.device("cpu"), amp_dtype=None, graph=False,
+                    flat=True)
+    tr.train_step(_batch(0))
+    ck = tr.checkpoint(config={"name": "tiny"}, epoch=3)
+    assert set(ck) == {"config", "epoch", "state_dict", "optimizer", "scheduler"}
+    assert all(k.startswith("model.") for k in ck["state_dict"])
+    path = tmp_path / "epoch=3.ckpt"
+    torch.save(ck, path)
+    torch.manual_seed(1)
+    fresh = TinyModel()
+    _, n, total = load_network(fresh.depth_net, str(path), "depth_net")
+    assert n == total == len(fresh.depth_net.state_dict())
+    load_network(fresh.pose_net, str(path), ["pose_net"])
+    for k, v in model.state_dict().items():
+        assert torch.equal(fresh.state_dict()[k], v), k

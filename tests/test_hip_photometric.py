@@ -13,8 +13,11 @@ Tolerances (BASELINE.json north_star: 1e-4 rel fp32):
     outcome at the flagged places (the other min selection at near-ties, the other bilinear cell
     at kinks, or both: golden_util.oracle_alternatives), or else stay within 5e-2 * max; at most
     5 % of the pixels may be flagged; the counts are printed;
-  * dL/dpose: 1e-3 relative on inputs with no sensitive pixel (test_kink_free_*); on golden
-    inputs that contain kinks, 2e-2 (one kink pixel moves the 24x80 pose gradient by ~1e-2).
+  * dL/dpose: every entry within 1e-3 * max|g| of the float64 oracle plus twice the flagged
+    pixels' own contribution to that entry (golden_util.pose_check_bounded: the oracle re-run in
+    float64 with the flagged pixels' warp gradients dropped gives that contribution); inputs with
+    no flagged pixel get no slack at all (test_kink_free_*).  The worst error / allowance ratio
+    is printed.
 """
 import numpy as np
 import pytest
@@ -73,28 +76,30 @@ def run_hip_case(z, dev, mask_none=False):
 
 
 def _sensitive(z):
-    """(sensitive maps, oracle dL/dsig with every near-tie flipped) — or (None, None) for a
-    multi-resolution case (checked without exclusions)."""
+    """(sensitive maps, oracle dL/dsig alternatives, (fp64 oracle dL/dpose, flagged-pixel pose
+    bound)) — or (None, None, None) for a multi-resolution case (checked without exclusions)."""
     from oracle import photometric_oracle as O
     kw = _kw(z)
     nctx = sum(1 for k in z if k.startswith("ctx"))
     T = torch.from_numpy
     sigs = [T(z[f"sig{i}"]) for i in range(kw["num_scales"])]
     if any(s.shape[-2:] != sigs[0].shape[-2:] for s in sigs):
-        return None, None
+        return None, None, None
     mats = [O.pose_vec_to_mat(T(z["vec"])[:, j]) for j in range(nctx)]
     image, ctx = T(z["image"]), [T(z[f"ctx{j}"]) for j in range(nctx)]
     sens, ties = O.sensitive_pixels(image, ctx, sigs, T(z["K"]), mats, kw["min_depth"], kw["max_depth"],
                                     kw["automask_loss"], kw["ssim_loss_weight"], return_ties=True)
-    alt = gu.oracle_alternatives(image, ctx, sigs, T(z["K"]), mats, T(z["mask"]),
+    alt, alt_pose, bound = gu.oracle_alternatives(
+                                 image, ctx, sigs, T(z["K"]), mats, T(z["mask"]),
                                  ties if kw["photometric_reduce_op"] == "min" else None,
+                                 pose_vec=T(z["vec"]), sensitive=sens,
                                  num_scales_=kw["num_scales"], ssim_loss_weight=kw["ssim_loss_weight"],
                                  smooth_loss_weight=kw["smooth_loss_weight"], C1=kw["C1"], C2=kw["C2"],
                                  photometric_reduce_op=kw["photometric_reduce_op"], clip_loss=kw["clip_loss"],
                                  automask_loss=kw["automask_loss"], min_depth=kw["min_depth"],
                                  max_depth=kw["max_depth"], progressive_scaling=kw["progressive_scaling"],
                                  progress=float(z.get("progress", 0.0)))
-    return [m.numpy() for m in sens], alt
+    return [m.numpy() for m in sens], alt, (alt_pose[0], bound)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -104,7 +109,7 @@ def test_loss_and_grads_match_reference_golden(dev, case):
     assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["photometric_loss"].cpu(), z["photometric_loss"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < LOSS_TOL
-    sens, alt = _sensitive(z)
+    sens, alt, pose_ref = _sensitive(z)
     n_used = int(z.get("n_used", len(sigs)))
     for i, s in enumerate(sigs):
         if i >= n_used:   # ProgressiveScaling dropped this scale: no gradient, as in the reference
@@ -114,8 +119,12 @@ def test_loss_and_grads_match_reference_golden(dev, case):
                                        None if sens is None else sens[i], GRAD_TOL)
         print(f"{case} dL/dsig{i}: {st}")
         assert ok, f"dL/dsig{i}: {st}"
-    n_sens = 0 if sens is None else int(sum(m.sum() for m in sens))
-    assert gu.rel_err(vec.grad.cpu(), z["grad_vec"]) < (GRAD_TOL if n_sens == 0 else 2e-2)
+    if pose_ref is None:   # multi-resolution case: no exclusions, the reference golden at 1e-3
+        assert gu.rel_err(vec.grad.cpu(), z["grad_vec"]) < GRAD_TOL
+        return
+    ok, st = gu.pose_check_bounded(vec.grad.cpu(), *pose_ref, tol=GRAD_TOL)
+    print(f"{case} dL/dpose: {st}")
+    assert ok, f"dL/dpose: {st}"
 
 
 def _seeded_inputs(seed, B, H, W, nctx=2):
@@ -197,16 +206,20 @@ def test_kitti_full_res_golden(dev):
     out["loss"].sum().backward()
     assert gu.rel_err(out["loss"].detach().cpu(), z["loss"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z["smoothness_loss"]) < LOSS_TOL
-    # 983k warp evaluations: kinks and near-ties always exist at this size; ATen-GPU vs the CPU
-    # golden differs by 2.8e-3 on this pose gradient (tools/debug_grads.py) -> 5e-3 here
-    assert gu.rel_err(v_d.grad.cpu(), z["grad_vec"]) < 5e-3
     from oracle import photometric_oracle as O
     mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
     sens, ties = O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0, return_ties=True)
     s_c = [s.clone().requires_grad_(True) for s in sigs]
     ref = O.photometric_loss(image, ctx, s_c, K, K, mats, None)
     ref[0].sum().backward()
-    alt = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties)
+    alt, alt_pose, bound = gu.oracle_alternatives(image, ctx, sigs, K, mats, None, ties, pose_vec=vec,
+                                                  sensitive=sens)
+    # 983k warp evaluations: kinks and near-ties always exist at this size (ATen-GPU vs the CPU
+    # golden itself differs by 2.8e-3 on this pose gradient, tools/debug_grads.py); the bound is
+    # the flagged pixels' own share
+    ok, st = gu.pose_check_bounded(v_d.grad.cpu(), alt_pose[0], bound, tol=GRAD_TOL)
+    print(f"kitti dL/dpose: {st}")
+    assert ok, f"dL/dpose: {st}"
     idx = torch.from_numpy(z["sample_idx"])
     for i in range(4):
         g_cpu = s_c[i].grad.reshape(-1)
@@ -326,12 +339,9 @@ def test_benchmarked_shapes_match_oracle(dev, B, H, W):
     # the pose gradient sums ~10^6 warps, among them the flagged pixels: every entry within
     # 1e-3 * max|g| + 2 x the flagged pixels' own contribution to that entry (float64 oracle with
     # their warp gradients dropped, golden_util.oracle_alternatives) of the float64 oracle
-    got_v, ref_v = v_d.grad.cpu().double().numpy(), alt_pose[0]
-    slack = 1e-3 * np.abs(ref_v).max() + 2.0 * pose_bound
-    ratio = float((np.abs(got_v - ref_v) / slack).max())
-    print(f"B={B} {H}x{W} dL/dpose: rel err vs fp64 oracle {gu.rel_err(got_v, ref_v):.2e}, flagged-pixel share "
-          f"{float((pose_bound / np.abs(ref_v).max()).max()):.2e} of max, worst |err| / allowance {ratio:.2f}")
-    assert ratio <= 1.0
+    ok, st = gu.pose_check_bounded(v_d.grad.cpu(), alt_pose[0], pose_bound, tol=GRAD_TOL)
+    print(f"B={B} {H}x{W} dL/dpose: {st}")
+    assert ok, f"dL/dpose: {st}"
 
 
 @pytest.mark.parametrize("B,H,W,clip", [(2, 32, 96, 0.0), (4, 192, 640, 0.0), (1, 64, 128, 0.5)])

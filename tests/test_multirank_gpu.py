@@ -1,0 +1,138 @@
+"""The multi-GPU training path of BASELINE configs 4 / 5 with more than one rank, on one GPU.
+
+`bench.py --gpus N` runs one process per GPU, each a DDPTrainer(graph=True, comm='split') over its
+DistributedSampler partition (models/model_wrapper.py:1138-1144): the step graph (forward,
+backward, gradient pack into the flat fp32 buffer), a host-enqueued all_reduce of that buffer, and
+the optimizer graph reading it with 1/world — the reference's per-step averaging
+(trainers/horovod_trainer.py:222-284).  RCCL refuses two ranks on one device, so the two ranks
+here share cuda:0 over gloo (gloo all-reduces device tensors through the host); everything else
+is the bench's path.
+
+  * bf16 nets + fused mixed-precision Adam (the bench default): after 3 steps both ranks hold
+    bitwise identical fp32 master weights and bf16 model weights;
+  * fp32 nets with deterministic MIOpen solvers: both ranks' weights equal, bit for bit, one
+    process stepping torch Adam on the average of the two ranks' gradients of the same samples.
+"""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B, H, W, STEPS = 2, 64, 192, 3
+
+
+class _A:
+    depth_net, pose_net, batch, height, width = "ResNetSAN01", "PoseNet", B, H, W
+    min_depth, max_depth = 0.5, 80.0
+
+
+def _setup(mode):
+    import bench
+    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.deterministic = mode == "fp32det"
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = bench.to_channels_last(bench.build_model(_A, dev))
+    return bench, dev, model
+
+
+def _worker(rank, world, init_file, out_dir, mode):
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench, dev, model = _setup(mode)
+    from packnet_sfm_amd.datasets.synthetic import ResidentLoader, SyntheticSfmDataset, get_datasampler
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    bf16 = mode == "bf16"
+    opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=bf16)
+    tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16 if bf16 else None, graph=True,
+                    bf16_weights=bf16, comm="split")
+    assert tr.dp and tr.world == world and not tr.overlap
+    ds = SyntheticSfmDataset(4 * B * world, H, W, 2, 1, seed=0)
+    loader = ResidentLoader(ds, B, get_datasampler(ds, "train"), dev)
+    batch = bench.net_layout(loader.next_into(None))
+    seen = [loader.partition[0:B]]
+    losses = []
+    for i in range(STEPS):
+        if i:
+            k = loader.step_in_epoch
+            loader.next_into(tr.static_batch)
+            seen.append(loader.partition[k * B:(k + 1) * B])
+        losses.append(float(tr.train_step(batch)["loss"]))
+    torch.cuda.synchronize()
+    assert len(tr.graphs) == 2   # split: step graph | all_reduce | optimizer graph
+    out = {"seen": torch.tensor(seen), "losses": torch.tensor(losses),
+           "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()}}
+    if tr.fused is not None:
+        out["master"] = tr.fused.master.cpu()
+        assert int(tr.fused.step_count) == STEPS
+    torch.save(out, os.path.join(out_dir, f"{mode}_r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(mode, world=2):
+    import __graft_entry__
+    __graft_entry__.build()
+    d = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(world, os.path.join(d, "init"), d, mode), nprocs=world, join=True)
+    return [torch.load(os.path.join(d, f"{mode}_r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def test_two_ranks_bf16_fused_split_path_keep_identical_masters():
+    r0, r1 = _run("bf16")
+    # the sampler gave the ranks disjoint samples, so they computed different gradients ...
+    assert not set(r0["seen"].flatten().tolist()) & set(r1["seen"].flatten().tolist())
+    assert not torch.equal(r0["losses"], r1["losses"])
+    # ... and stepped on the same averaged gradient
+    assert torch.equal(r0["master"], r1["master"])
+    for n, p in r0["params"].items():
+        assert torch.equal(p, r1["params"][n]), n
+    assert torch.isfinite(r0["master"]).all()
+
+
+def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
+    r = _run("fp32det")
+    for n, p in r[0]["params"].items():
+        assert torch.equal(p, r[1]["params"][n]), n
+    # one process, the same initial weights, eager steps on the average of the ranks' gradients
+    bench, dev, model = _setup("fp32det")
+    from packnet_sfm_amd.datasets.synthetic import SyntheticSfmDataset
+    from packnet_sfm_amd.trainers.ddp_trainer import make_optimizer
+    opt = make_optimizer(model, 1e-4, 1e-4, capturable=True)
+    ds = SyntheticSfmDataset(4 * B * 2, H, W, 2, 1, seed=0)
+
+    def batch_of(idx):
+        s = [ds[i] for i in idx]
+        rgb = torch.stack([x["rgb"] for x in s]).to(dev)
+        ctx = [torch.stack([x["rgb_context"][j] for x in s]).to(dev) for j in range(2)]
+        b = {"rgb": rgb, "rgb_context": ctx, "rgb_original": rgb, "rgb_context_original": ctx,
+             "intrinsics": torch.stack([x["intrinsics"] for x in s]).to(dev)}
+        return bench.net_layout(b)
+
+    params = [p for p in model.parameters() if p.requires_grad]
+    try:
+        torch.backends.cudnn.deterministic = True
+        for step in range(STEPS):
+            per_rank = []
+            for k in range(2):
+                for p in params:
+                    p.grad = None
+                out = model(batch_of(r[k]["seen"][step].tolist()))
+                assert float(out["loss"]) == float(r[k]["losses"][step]), (step, k)
+                out["loss"].sum().backward()
+                per_rank.append([p.grad.clone() if p.grad is not None else None for p in params])
+            for p, g0, g1 in zip(params, *per_rank):
+                p.grad = None if g0 is None else (g0 + g1) * 0.5
+            opt.step()
+        torch.cuda.synchronize()
+    finally:
+        torch.backends.cudnn.deterministic = False
+    for n, p in model.named_parameters():
+        assert torch.equal(p.detach().float().cpu(), r[0]["params"][n]), n

@@ -256,3 +256,50 @@ def test_config1_depthresnet_poseresnet_step_on_gpu_matches_cpu_oracle():
     assert set(got) == set(ref_norms)
     bad = {n: (got[n], r) for n, r in ref_norms.items() if abs(got[n] - r) > 2e-2 * r + 1e-12}
     assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_ddad_packnet_san_four_camera_step_matches_oracle_on_its_outputs():
+    """BASELINE config 5 per GPU (configs/train_packnet_san_ddad.yaml): one DDAD sample of 4
+    cameras at 384x640 (5-D batch, folded into the batch by flatten_cameras == stack_batch,
+    model_utils.py:68-94), PackNetSAN01 (d = 4 pack / unpack kernels) + PoseNet under bf16
+    autocast, HIP loss.  The loss and both metrics equal the oracle evaluated on the step's own
+    network outputs (sigmoid maps upsampled to full resolution, pose matrices, per-camera
+    intrinsics) within 1e-4; the backward through both nets runs and leaves finite gradients
+    in every parameter."""
+    import __graft_entry__
+    __graft_entry__.build()
+    import bench
+    from oracle import photometric_oracle as O
+    from packnet_sfm_amd.datasets.synthetic import SyntheticSfmDataset
+    dev = torch.device("cuda:0")
+    torch.backends.cudnn.benchmark = False
+    args = bench.parse(["--config", "ddad-packnet-san"])
+    torch.manual_seed(0)
+    model = bench.to_channels_last(bench.build_model(args, dev))
+    s = SyntheticSfmDataset(1, 384, 640, 2, cameras=4, seed=5)[0]
+    assert s["rgb"].shape == (4, 3, 384, 640)
+    batch = {"rgb": s["rgb"][None].to(dev), "rgb_context": [c[None].to(dev) for c in s["rgb_context"]],
+             "intrinsics": s["intrinsics"][None].to(dev)}
+    batch["rgb_original"], batch["rgb_context_original"] = batch["rgb"], batch["rgb_context"]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = model(batch, progress=0.0)
+    out["loss"].sum().backward()
+    torch.cuda.synchronize()
+    inv = [out["inv_depths"][i].detach().float().cpu() for i in range(4)]
+    assert all(tuple(t.shape) == (4, 1, 384, 640) for t in inv)
+    mats = [p.mat.detach().float().cpu() for p in out["poses"]]
+    rgb, ctx, K = s["rgb"], list(s["rgb_context"]), s["intrinsics"]
+    torch.set_num_threads(16)
+    ref = O.photometric_loss(rgb, ctx, inv, K, K, mats, None, num_scales_=4, ssim_loss_weight=0.85,
+                             smooth_loss_weight=0.001, photometric_reduce_op="min", automask_loss=True,
+                             clip_loss=0.0, min_depth=0.5, max_depth=200.0)
+    print(f"4-camera 384x640 loss: HIP {float(out['loss']):.8f}, oracle {float(ref[0]):.8f}")
+    assert gu.rel_err(out["loss"].detach().cpu(), ref[0].detach()) < 1e-4
+    assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), ref[2].detach()) < 1e-4
+    assert gu.rel_err(out["metrics"]["photometric_loss"].cpu(), ref[0].detach()) < 1e-4   # the fork's alias
+    # the LiDAR fusion weights of PackNetSAN01 (depth_net.weight / .bias) are unused on the RGB path
+    missing = [n for n, p in model.named_parameters() if p.requires_grad and p.grad is None]
+    assert missing == ["depth_net.weight", "depth_net.bias"], missing[:5]
+    bad = [n for n, p in model.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
+    assert not bad, bad[:5]
