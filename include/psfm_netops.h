@@ -15,12 +15,14 @@
  *
  * Layout: an activation is a bf16 matrix [M, C] row-major — the storage order of an NHWC
  * (torch.channels_last) tensor with M = N*H*W (GroupNorm: [N, HW, C]).  Statistics and
- * parameters are fp32.  Reductions are deterministic and single-launch: per-workgroup partials
- * in `ws`, summed in a fixed order (fp64) by the last workgroup of each group of 16 and then by
- * the last group to finish — no float atomics.  Arrivals are counted in `counter`, an int array
- * of PSFM_NETOPS_COUNTER_INTS ("one slot", psfm_gn_act_bwd: two slots) zeroed once by the
- * caller and re-armed by the kernels, so graph replays reuse it.  Two launches that may run
- * concurrently must not share a slot.
+ * parameters are fp32.  Reductions are deterministic (no float atomics) and use no counters:
+ * each pass writes one partial row per workgroup into `ws`, and the next launch sums what it
+ * needs in a fixed order (fp64) — the GroupNorm apply pass its sample's group rows in its
+ * prologue, a small column-total kernel the parameter gradients.  The kernel boundary orders
+ * the partial rows before their readers, so no device-scope arrival rounds are needed.
+ * BatchNorm (bn_act, off by default: MIOpen's BN is faster on these nets) still reduces in
+ * one launch with arrival counts in `counter`, an int array of PSFM_NETOPS_COUNTER_INTS
+ * zeroed once by the caller and re-armed by the kernels.
  *
  * Conventions as include/psfm.h: device pointers, caller-owned buffers, stream-ordered,
  * graph-capturable; return 0 / <0 bad argument / >0 hipError_t, message from
@@ -54,9 +56,10 @@ size_t psfm_gn_ws_floats(int N, int HW, int C, int G);
 int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y,
                       void* stream);
 
-/* dx = dy * act'(y) (bf16), dbias = sum_rows dx (written in the bias dtype).  dy has y's dtype. */
+/* dx = dy * act'(y) (bf16), dbias = sum_rows dx (written in the bias dtype).  dy has y's dtype.
+ * Two launches: dx + per-workgroup partial rows, then the column totals. */
 int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void* dx, void* dbias,
-                      int bias_bf16, float* ws, int* counter, void* stream);
+                      int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
@@ -71,24 +74,26 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, int* counter, void* stream);
 
-/* y = act(GroupNorm(G)(x [+ res] + bias)) per sample: x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
+/* y = act(GroupNorm(G)(x [+ res] + bias)) per sample (two launches: statistics rows, then apply with
+ * the per-sample reduction in its prologue): x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
  * or NULL, gamma/beta fp32 [C], act PSFM_ACT_NONE / RELU / ELU.  PoseNet conv_gn (conv + GN + ReLU,
  * PoseNet.py:15-19); PackNet Conv2D (conv + GN(16) + ELU, layers01.py:10-37) and ResidualConv's
  * GN(conv2 + shortcut) + ELU (res = the conv2 branch, layers01.py:40-61).  save_mean / save_invstd
  * [N*G]. */
 int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
                     const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
-                    float* save_invstd, float* ws, int* counter, void* stream);
+                    float* save_invstd, float* ws, void* stream);
 
 /* Backward of psfm_gn_act_fwd: dx (bf16) and, with res, dres (a second copy: both inputs are summed),
  * dbias (bias dtype; the column sum of the stored dx, as autograd forms a conv bias gradient; NULL
  * with bias NULL), dgamma / dbeta (fp32 [C]).  The activation's derivative is taken at its input,
  * recomputed from x (+ res + bias), save_mean / save_invstd and gamma / beta — the forward output is
- * not read back (one activation-sized read less per pass).  `counter` spans two slots. */
+ * not read back (one activation-sized read less per pass).  Three launches: statistics rows, apply
+ * (dx + conv-bias rows), parameter-gradient column totals. */
 int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,
                     const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                     int N, int HW, int C, int G, int act, void* dx, void* dres, void* dbias, float* dgamma,
-                    float* dbeta, float* ws, int* counter, void* stream);
+                    float* dbeta, float* ws, void* stream);
 
 const char* psfm_netops_last_error(void);
 

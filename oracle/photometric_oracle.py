@@ -371,20 +371,22 @@ def depth_metrics(gt, pred, min_depth, max_depth, crop="garg", use_gt_scale=True
 # test helpers: where is a fp32 implementation allowed to disagree with the reference's gradient?
 # ---------------------------------------------------------------------------------------------------------------------
 def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, automask=True,
-                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=1e-4, margin_eps=5e-5, l1_eps=5e-5,
+                     ssim_w=0.85, C1=1e-4, C2=9e-4, coord_eps=2e-4, margin_eps=5e-5, l1_eps=1e-4,
                      return_ties=False):
     """Per-scale boolean maps [B,1,h,w] of pixels whose gradient is discontinuous at fp32 precision:
 
-    * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer (1e-4: an fp32
-      pixel coordinate in [512, 1024) has a 6.1e-5 ulp) — d(warp)/d(ix)
+    * bilinear kinks: a sampling coordinate within `coord_eps` px of an integer (2e-4: ~3 ulps of
+      an fp32 pixel coordinate in [512, 1024), which passes through ~20 fp32 operations: lift,
+      transform, project, normalise / un-normalise; 1e-4 let a real flip through in the rand_mask
+      golden's pose gradient) — d(warp)/d(ix)
       jumps there (grid_sample's derivative is piecewise constant in the tap cell), so two fp32
       implementations that round ix to opposite sides get different gradients at that pixel;
     * min-reprojection near-ties: best and second-best candidate within `margin_eps` (fp32 SSIM
       carries ~1e-5 absolute error from the E[x^2]-mu^2 cancellation, so two fp32 implementations
       can order candidates differently below that) — the
       selected candidate (and so the gradient of the 3x3 SSIM window around it) can flip.
-    * L1 sign near-ties: a warped value within `l1_eps` of the target in some channel (5e-5: a
-      1e-4 px coordinate difference on a steep texture moves the warped value that much) — the
+    * L1 sign near-ties: a warped value within `l1_eps` of the target in some channel (1e-4: a
+      2e-4 px coordinate difference on a steep texture moves the warped value that much) — the
       derivative of |est - tgt| flips sign there (the selected candidate's 3x3 SSIM window aside,
       only that pixel's gradient moves).
     Computed in float64 from the same inputs.  Full-resolution scales only.  With `return_ties`

@@ -43,7 +43,6 @@ constexpr int U = 4;              // row steps unrolled (independent loads in fl
 constexpr int TARGET_BLOCKS = 512;
 constexpr int GS = 16;     // workgroups per reduction group (ngroups)
 constexpr int MAX_KC = 1024;      // widest partial row (BN: 2*C, C <= 512)
-constexpr int CTR = PSFM_NETOPS_COUNTER_INTS;
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (NaN stays NaN)
@@ -346,9 +345,7 @@ struct BiasArgs {
     const void* dy;
     const void* y;
     void* out;  // y (fwd) / dx (bwd)
-    void* dbias;
-    float* ws;
-    int* counter;
+    float* ws;  // bwd: per-workgroup partial rows of the bias gradient [nblk][C]
     int M, C, act, bias_bf16, G, TR, rpb, nblk;
 };
 
@@ -384,8 +381,6 @@ __global__ __launch_bounds__(NT) void k_bias_act_fwd(BiasArgs a) {
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bias_act_bwd(BiasArgs a) {
     __shared__ float red[NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[1][VEC];
@@ -429,16 +424,71 @@ __global__ __launch_bounds__(NT) void k_bias_act_bwd(BiasArgs a) {
         }
         ROW_LOOP_END
     }
+    // this workgroup's column sums -> its partial row; k_cols_finish sums the rows (next launch)
     block_colsum<VEC, 1>(acc, red, a.G, a.TR);
-    store_row<VEC, 1>(a.ws + (size_t)blockIdx.x * a.C, acc, a.C, c0, r);
-    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, a.C));
-    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, a.C, fin, scratch)) return;
-    for (int c = t; c < a.C; c += NT) {
-        if (a.bias_bf16)
-            static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)fin[c]);
-        else
-            static_cast<float*>(a.dbias)[c] = (float)fin[c];
+    if (r == 0) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) a.ws[(size_t)blockIdx.x * a.C + c0 + i] = acc[0][i];
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Column totals of partial rows, the second launch of every reduction above and below (no
+// arrival counters: the kernel boundary orders the partial rows before their readers).
+// Job j: out_j[c] = sum over rows r < nrows of src_j[r * stride + off + c], c < ncols, in fp64:
+// lane l of 64 sums rows l, l + 64, ... (8 loads in flight per thread), then a fixed tree over
+// the lanes — deterministic.  Workgroup = 4 columns x 64 lanes; grid (ceil(cols / 4), jobs).
+// ------------------------------------------------------------------------------------------
+struct ColJob {
+    const float* src;
+    void* out;
+    int stride, off, nrows, ncols, out_bf16;
+};
+struct FinishArgs {
+    ColJob job[3];
+};
+
+__global__ __launch_bounds__(256) void k_cols_finish(FinishArgs a) {
+    __shared__ double part[256];
+    const ColJob j = a.job[blockIdx.y];
+    const int t = threadIdx.x, cl = t & 3, lane = t >> 2;
+    const int c = blockIdx.x * 4 + cl;
+    double s = 0.0;
+    if (c < j.ncols) {
+        for (int r0 = lane; r0 < j.nrows; r0 += 8 * 64) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int rr = r0 + u * 64;
+                v[u] = rr < j.nrows ? j.src[(size_t)rr * j.stride + j.off + c] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+    }
+    part[t] = s;
+    __syncthreads();
+    for (int h = 32; h >= 1; h >>= 1) {
+        if (lane < h) part[t] += part[t + 4 * h];
+        __syncthreads();
+    }
+    if (lane == 0 && c < j.ncols) {
+        if (j.out_bf16)
+            static_cast<uint16_t*>(j.out)[c] = f2bf((float)part[t]);
+        else
+            static_cast<float*>(j.out)[c] = (float)part[t];
+    }
+}
+
+inline hipError_t launch_finish(const ColJob* jobs, int njobs, hipStream_t st) {
+    FinishArgs a{};
+    int cols = 1;
+    for (int k = 0; k < njobs; ++k) {
+        a.job[k] = jobs[k];
+        cols = std::max(cols, jobs[k].ncols);
+    }
+    hipLaunchKernelGGL(k_cols_finish, dim3((cols + 3) / 4, njobs), dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -650,8 +700,18 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW).  Each sample is
-// its own reduction segment (bpn workgroups, counters at counter + n*(1+ngroups(bpn))).
+// GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW),
+// bpn workgroups per sample.  No arrival counters: each pass writes per-workgroup partial rows
+// and the NEXT launch reduces what it needs in a fixed order —
+//   forward:  stats (rows of per-group sum / sum of squares, 2*NG floats) -> apply (every
+//             workgroup sums its sample's bpn group rows in its prologue: mean / invstd);
+//   backward: stats (rows of per-group A = sum gamma*dyr, Bq = sum gamma*dyr*xhat and
+//             per-channel S1 = sum dyr, S2 = sum dyr*xhat, X = sum xhat) -> apply (prologue: A, Bq
+//             of its sample -> dx coefficients) whose last ceil(C/4) workgroups finish the
+//             parameter gradients from the same rows: dbeta = sum S1, dgamma = sum S2 and the conv
+//             bias gradient in closed form, sum_hw dx = k1*S1 - HW*k2 - k3*X per sample.
+// The apply passes issue their first activation loads before the prologue, so the per-sample
+// reduction (bpn x 2*NG floats, L2-resident) overlaps them: two launches each way, no rounds.
 // ------------------------------------------------------------------------------------------
 // GroupNorm activations: ReLU (PoseNet conv_gn) or ELU(alpha = 1) (PackNet Conv2D / ResidualConv,
 // layers01.py:10-37, :40-61: x > 0 ? x : expm1(x); backward from the result: y > 0 ? g : g (y + 1))
@@ -668,48 +728,72 @@ __device__ __forceinline__ float gn_act_g(float g, float w, int act) {
     return g;
 }
 
+constexpr int MAX_C = 512;   // widest GroupNorm layer (PackNet encoder: 512)
+constexpr int MAX_NG = 128;  // 2 * NG partial columns must fit one workgroup
+
 struct GNArgs {
     const uint16_t* x;
     const uint16_t* res;  // optional second input summed with x (PackNet ResidualConv)
     const void* bias;     // optional (null = 0)
     const uint16_t* dy;
-    const uint16_t* y;
     const float* gamma;
     const float* beta;
     float* save_mean;    // [N*NG]
     float* save_invstd;  // [N*NG]
     uint16_t* out;
     uint16_t* out2;       // backward: dres (a second copy of dx) when res is given
-    void* dbias;
+    void* dbias;          // backward: conv-bias gradient (bias dtype) or null
     float* dgamma;
     float* dbeta;
-    float* ws;
-    int* counter;
+    float* ws;            // stats rows [N*bpn][RW]
     float eps;
-    int N, HW, C, NG, act, bias_bf16, G, TR, rpb, bpn;  // act: PSFM_ACT_*; bpn: workgroups per sample
+    int N, HW, C, NG, act, bias_bf16, G, TR, rpb, bpn, RW;  // act: PSFM_ACT_*; bpn: workgroups per sample
 };
 
-// workspace: stats tree [N segs][2C] | coef [N][3][C] | per-sample bwd rows [N][2C] fp64 |
-//            dbias tree [1 seg of N*bpn][C]
-__device__ __forceinline__ size_t gn_off_coef(const GNArgs& a) { return tree_ws_floats(a.N, a.bpn, 2 * a.C); }
-__device__ __forceinline__ size_t gn_off_nrows(const GNArgs& a) { return align4(gn_off_coef(a) + (size_t)a.N * 3 * a.C); }
-__device__ __forceinline__ size_t gn_off_dbias(const GNArgs& a) { return gn_off_nrows(a) + 2 * (size_t)a.N * 2 * a.C; }
-
-// stats segment of sample n: block rows at ws + n*bpn*KC, group rows after all block rows.
-__device__ __forceinline__ bool gn_tree(const GNArgs& a, int n, int bl, double* fin, double* scratch) {
-    const int KC = 2 * a.C;
-    float* rows = a.ws + (size_t)n * a.bpn * KC;
-    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(a.N, a.bpn, KC)) + (size_t)n * ngroups(a.bpn) * KC;
-    return tree_reduce(rows, grp, a.counter + n * (1 + ngroups(a.bpn)), bl, a.bpn, KC, fin, scratch);
+// tot[j] = sum over the sample's nrows partial rows (stride RW) of column j < KC, fp64, rows split
+// over NT/KC lanes in a fixed order; every thread of the workgroup takes part (barriers inside).
+__device__ void group_totals(const float* rows, int nrows, int RW, int KC, double* tot, double* scr) {
+    const int t = threadIdx.x, L = NT / KC, j = t % KC, l = t / KC;
+    if (l < L) {
+        double s = 0.0;
+        for (int r0 = l; r0 < nrows; r0 += 8 * L) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int rr = r0 + u * L;
+                v[u] = rr < nrows ? rows[(size_t)rr * RW + j] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        scr[l * KC + j] = s;
+    }
+    __syncthreads();
+    if (t < KC) {
+        double s = 0.0;
+        for (int ll = 0; ll < L; ++ll) s += scr[ll * KC + t];
+        tot[t] = s;
+    }
+    __syncthreads();
 }
 
-// forward pass 1: per (n, c) sum / sumsq of x+bias; finishing workgroup of sample n -> per
-// (n, g) mean / invstd and per (n, c) affine coefficients (bias folded: y = (x+bias)*scale + shift).
+// per-channel column sums (row lane 0 of block_colsum) -> LDS chan[k][C]
+template <int VEC, int K>
+__device__ __forceinline__ void chan_to_lds(const float (&acc)[K][VEC], float* chan, int C, int c0, int r) {
+    if (r == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) chan[k * C + c0 + i] = acc[k][i];
+    }
+    __syncthreads();
+}
+
+// forward pass 1: per (workgroup, group) sum / sumsq of x (+ res) + bias -> partial row [2][NG]
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
+    __shared__ float chan[2 * MAX_C];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
@@ -742,79 +826,91 @@ __global__ __launch_bounds__(NT) void k_gn_fwd_stats(GNArgs a) {
         ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * 2 * a.C, acc, a.C, c0, r);
-    if (!gn_tree(a, n, bl, fin, scratch)) return;
-    float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
+    chan_to_lds<VEC, 2>(acc, chan, a.C, c0, r);
     const int cpg = a.C / a.NG;
-    const double inv_cnt = 1.0 / ((double)a.HW * cpg);
-    for (int c = t; c < a.C; c += NT) {
-        const int g = c / cpg;
-        double s = 0.0, q = 0.0;
-        for (int u = 0; u < cpg; ++u) {  // group sums in channel order
-            s += fin[g * cpg + u];
-            q += fin[a.C + g * cpg + u];
-        }
-        const double mean = s * inv_cnt;
-        const double var = fmax(q * inv_cnt - mean * mean, 0.0);
-        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        if (c % cpg == 0) {
-            a.save_mean[n * a.NG + g] = (float)mean;
-            a.save_invstd[n * a.NG + g] = invstd;
-        }
-        const float scale = a.gamma[c] * invstd;
-        coef[c] = scale;
-        coef[a.C + c] = a.beta[c] - (float)mean * scale;
+    float* row = a.ws + (size_t)blockIdx.x * a.RW;
+    for (int j = t; j < 2 * a.NG; j += NT) {  // group sums in channel order
+        const int k = j / a.NG, g = j - k * a.NG;
+        float s = 0.0f;
+        for (int u = 0; u < cpg; ++u) s += chan[k * a.C + g * cpg + u];
+        row[j] = s;
     }
 }
 
+// forward pass 2: prologue = this sample's group statistics from the stats rows; y = act(...).
+// The first U rows of every thread are loaded before the prologue (their latency overlaps it).
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_fwd_apply(GNArgs a) {
+    __shared__ double tot[2 * MAX_NG];
+    __shared__ double scr[NT];
+    __shared__ float gmean[MAX_NG], ginv[MAX_NG];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
-    const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
-    const Vec<VEC> sc = ld_f<VEC>(coef + c0), sh = ld_f<VEC>(coef + a.C + c0);
-    const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
     const size_t so = (size_t)n * a.HW * a.C;
     const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    const bool live = r < a.TR;
     Vec<VEC> v[U];
+    auto load = [&](int base) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        v[u] = row < row1 ? ld_bf<VEC>(a.x + so + (size_t)row * a.C + c0) : zero<VEC>();
-        if (a.res && row < row1) add_bf<VEC>(v[u], a.res + so + (size_t)row * a.C + c0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            v[u].v[i] = gn_act_f((v[u].v[i] + b.v[i]) * sc.v[i] + sh.v[i], a.act);
+        for (int u = 0; u < U; ++u) {
+            const int row = base + u * a.TR;
+            v[u] = row < row1 ? ld_bf<VEC>(a.x + so + (size_t)row * a.C + c0) : zero<VEC>();
+            if (a.res && row < row1) add_bf<VEC>(v[u], a.res + so + (size_t)row * a.C + c0);
         }
-        st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, v[u]);
+    };
+    if (live) load(row0 + r);
+    group_totals(a.ws + (size_t)n * a.bpn * a.RW, a.bpn, a.RW, 2 * a.NG, tot, scr);
+    const int cpg = a.C / a.NG;
+    if (t < a.NG) {
+        const double inv_cnt = 1.0 / ((double)a.HW * cpg);
+        const double mean = tot[t] * inv_cnt;
+        const double var = fmax(tot[a.NG + t] * inv_cnt - mean * mean, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        gmean[t] = (float)mean;
+        ginv[t] = invstd;
+        if (bl == 0) {
+            a.save_mean[n * a.NG + t] = (float)mean;
+            a.save_invstd[n * a.NG + t] = invstd;
+        }
     }
-    ROW_LOOP_END
+    __syncthreads();
+    if (!live) return;
+    Vec<VEC> sc, sh;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+        const int g = (c0 + i) / cpg;
+        sc.v[i] = a.gamma[c0 + i] * ginv[g];
+        sh.v[i] = a.beta[c0 + i] - gmean[g] * sc.v[i];
+    }
+    const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
+    for (int base = row0 + r; base < row1; base += U * a.TR) {
+        if (base != row0 + r) load(base);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base + u * a.TR;
+            if (row >= row1) break;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) v[u].v[i] = gn_act_f((v[u].v[i] + b.v[i]) * sc.v[i] + sh.v[i], a.act);
+            st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, v[u]);
+        }
+    }
 }
 
-// backward pass 1: per (n, c): S1 = sum dyr, S2 = sum dyr*xhat.  Finishing workgroup of sample
-// n: per (n, g) A = sum_{c in g} gamma S1, Bq = sum_{c in g} gamma S2 -> dx coefficients
-// dx = invstd (gamma dyr - A/cnt - xhat Bq/cnt); it stores (S1, S2)[n] and the last sample to
-// finish sums them over n (sample order) into dbeta / dgamma.
+// backward pass 1: per workgroup: S1 = sum dyr, S2 = sum dyr*xhat, X = sum xhat per channel, and
+// per group A = sum_{c in g} gamma S1, Bq = sum_{c in g} gamma S2
+// -> row [A(NG) | Bq(NG) | S1(C) | S2(C) | X(C)]
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
-    __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
+    __shared__ float red[3 * NT * VEC];
+    __shared__ float chan[3 * MAX_C];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
     const int cpg = a.C / a.NG;
-    float acc[2][VEC];
+    float acc[3][VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
+    for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = acc[2][i] = 0.0f;
     if (r < a.TR) {
         const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
         float mu[VEC], is[VEC];
@@ -840,118 +936,166 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_stats(GNArgs a) {
             if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
+            const bool in_u = base_ + u * a.TR < row1;
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
                 const float gg = gn_act_g(g[u].v[i], xh * ga[i] + be[i], a.act);
                 acc[0][i] += gg;
                 acc[1][i] += gg * xh;
+                acc[2][i] += in_u ? xh : 0.0f;
             }
+        }
         ROW_LOOP_END
     }
-    block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * 2 * a.C, acc, a.C, c0, r);
-    if (!gn_tree(a, n, bl, fin, scratch)) return;
-    float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;  // k1 = gamma*invstd, k2 = A/cnt*invstd, k3 = Bq/cnt*invstd
-    double* nrows = reinterpret_cast<double*>(a.ws + gn_off_nrows(a));  // [N][2C]
-    const double cnt = (double)a.HW * cpg;
-    for (int c = t; c < a.C; c += NT) {
-        const int g = c / cpg;
-        double A = 0.0, Bq = 0.0;
-        for (int u = 0; u < cpg; ++u) {
-            const int cc = g * cpg + u;
-            A += (double)a.gamma[cc] * fin[cc];
-            Bq += (double)a.gamma[cc] * fin[a.C + cc];
-        }
-        const double is = a.save_invstd[n * a.NG + g];
-        coef[c] = a.gamma[c] * (float)is;
-        coef[a.C + c] = (float)(A / cnt * is);
-        coef[2 * a.C + c] = (float)(Bq / cnt * is);
+    block_colsum<VEC, 3>(acc, red, a.G, a.TR);
+    chan_to_lds<VEC, 3>(acc, chan, a.C, c0, r);
+    float* row = a.ws + (size_t)blockIdx.x * a.RW;
+    for (int j = t; j < 2 * a.NG; j += NT) {
+        const int k = j / a.NG, g = j - k * a.NG;
+        float s = 0.0f;
+        for (int u = 0; u < cpg; ++u) s += a.gamma[g * cpg + u] * chan[k * a.C + g * cpg + u];
+        row[j] = s;
     }
-    for (int c = t; c < 2 * a.C; c += NT) st_part(nrows + (size_t)n * 2 * a.C + c, fin[c]);
-    if (!arrive(a.counter + a.N * (1 + ngroups(a.bpn)), a.N)) return;
-    for (int c = t; c < a.C; c += NT) {
-        double db = 0.0, dg = 0.0;
+    for (int j = t; j < 3 * a.C; j += NT) row[2 * a.NG + j] = chan[j];
+}
+
+// parameter gradients from the backward stats rows (the last ceil(C/4) workgroups of the apply
+// launch): workgroup = 4 channels x 64 lanes, lane l works on sample l / (64 / N) (N <= 64) and sums
+// its share of that sample's rows (fp64, fixed order) -> per (sample, channel) S1, S2, X and the
+// sample's group totals A, Bq -> dbeta = sum_n S1, dgamma = sum_n S2,
+// dbias = sum_n (k1 S1 - HW k2 - k3 X) (k as in the apply pass, in fp64).
+__device__ void gn_bwd_params(const GNArgs& a, int f) {
+    __shared__ double part[5][NT];
+    __shared__ double nt[5][64][4];
+    const int t = threadIdx.x, cl = t & 3, lane = t >> 2;
+    const int c = f * 4 + cl;
+    const int lpn = 64 / a.N, n = lane / lpn, li = lane % lpn;
+    const int cpg = a.C / a.NG;
+    double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (c < a.C && n < a.N) {
+        const int g = c / cpg;
+        const int col[5] = {2 * a.NG + c, 2 * a.NG + a.C + c, 2 * a.NG + 2 * a.C + c, g, a.NG + g};
+        for (int r0 = li; r0 < a.bpn; r0 += 2 * lpn) {
+            float v[2][5];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int rr = r0 + u * lpn;
+                const float* row = a.ws + (size_t)(n * a.bpn + (rr < a.bpn ? rr : 0)) * a.RW;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) v[u][k] = rr < a.bpn ? row[col[k]] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int k = 0; k < 5; ++k) s[k] += (double)v[u][k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) part[k][t] = s[k];
+    __syncthreads();
+    if (t < 4 * a.N) {   // per (sample, channel): lanes in order
+        const int cc = t & 3, nn = t >> 2;
+        for (int k = 0; k < 5; ++k) {
+            double q = 0.0;
+            for (int l = 0; l < lpn; ++l) q += part[k][((nn * lpn + l) << 2) | cc];
+            nt[k][nn][cc] = q;
+        }
+    }
+    __syncthreads();
+    if (t < 4 && c < a.C) {
+        const int g = c / cpg;
+        const double cnt = (double)a.HW * cpg, ga = a.gamma[c];
+        double db = 0.0, dg = 0.0, dbias = 0.0;
         for (int nn = 0; nn < a.N; ++nn) {
-            db += ld_part(nrows + (size_t)nn * 2 * a.C + c);
-            dg += ld_part(nrows + (size_t)nn * 2 * a.C + a.C + c);
+            const double S1 = nt[0][nn][t], S2 = nt[1][nn][t], X = nt[2][nn][t];
+            const double is = a.save_invstd[nn * a.NG + g];
+            db += S1;
+            dg += S2;
+            dbias += ga * is * S1 - (double)a.HW * (nt[3][nn][t] / cnt * is) - (nt[4][nn][t] / cnt * is) * X;
         }
         a.dbeta[c] = (float)db;
         a.dgamma[c] = (float)dg;
+        if (a.dbias) {
+            if (a.bias_bf16)
+                static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)dbias);
+            else
+                static_cast<float*>(a.dbias)[c] = (float)dbias;
+        }
     }
 }
 
-// backward pass 2: dx = k1*dyr - k2 - xhat*k3 with xhat = (x + bias - mean)*invstd, and the conv
-// bias gradient as autograd forms it: the column sum of the stored (bf16) dx over n, hw.
+// backward pass 2: prologue = A, Bq of this sample -> dx = k1*dyr - k2 - xhat*k3 with
+// k1 = gamma*invstd, k2 = A/cnt*invstd, k3 = Bq/cnt*invstd, xhat = (x + bias - mean)*invstd.
+// Workgroups past N*bpn compute the parameter gradients (gn_bwd_params).
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
-    __shared__ float red[NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
+    if ((int)blockIdx.x >= a.N * a.bpn) {
+        gn_bwd_params(a, blockIdx.x - a.N * a.bpn);
+        return;
+    }
+    __shared__ double tot[2 * MAX_NG];
+    __shared__ double scr[NT];
+    __shared__ float gk2[MAX_NG], gk3[MAX_NG];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
     const int cpg = a.C / a.NG;
-    float acc[1][VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[0][i] = 0.0f;
-    if (r < a.TR) {
-        const float* coef = a.ws + gn_off_coef(a) + (size_t)n * 3 * a.C;
-        const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
-        const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
-        float mu[VEC], is[VEC];
-        float ga[VEC], be[VEC];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
-            is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
-            ga[i] = a.gamma[c0 + i];
-            be[i] = a.beta[c0 + i];
-        }
-        const size_t so = (size_t)n * a.HW * a.C;
-        const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
-        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<VEC> g[U], x[U];
+    const size_t so = (size_t)n * a.HW * a.C;
+    const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
+    const bool live = r < a.TR;
+    Vec<VEC> g[U], x[U];
+    auto load = [&](int base) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int row = base_ + u * a.TR;
+            const int row = base + u * a.TR;
             const size_t o = so + (size_t)row * a.C + c0;
             const bool in = row < row1;
             g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
             x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
             if (a.res && in) add_bf<VEC>(x[u], a.res + o);
         }
+    };
+    if (live) load(row0 + r);
+    group_totals(a.ws + (size_t)n * a.bpn * a.RW, a.bpn, a.RW, 2 * a.NG, tot, scr);
+    if (t < a.NG) {
+        const double cnt = (double)a.HW * cpg;
+        const double is = a.save_invstd[n * a.NG + t];
+        gk2[t] = (float)(tot[t] / cnt * is);
+        gk3[t] = (float)(tot[a.NG + t] / cnt * is);
+    }
+    __syncthreads();
+    if (!live) return;
+    const Vec<VEC> b = a.bias ? ld_param<VEC>(a.bias, a.bias_bf16, c0) : zero<VEC>();
+    float mu[VEC], is[VEC], ga[VEC], be[VEC], k1[VEC], k2[VEC], k3[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+        const int gi = (c0 + i) / cpg;
+        mu[i] = a.save_mean[n * a.NG + gi];
+        is[i] = a.save_invstd[n * a.NG + gi];
+        ga[i] = a.gamma[c0 + i];
+        be[i] = a.beta[c0 + i];
+        k1[i] = ga[i] * is[i];
+        k2[i] = gk2[gi];
+        k3[i] = gk3[gi];
+    }
+    for (int base = row0 + r; base < row1; base += U * a.TR) {
+        if (base != row0 + r) load(base);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int row = base_ + u * a.TR;
+            const int row = base + u * a.TR;
             if (row >= row1) break;
             Vec<VEC> d;
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
                 const float xh = (x[u].v[i] + b.v[i] - mu[i]) * is[i];
                 const float gg = gn_act_g(g[u].v[i], xh * ga[i] + be[i], a.act);
-                d.v[i] = k1.v[i] * gg - k2.v[i] - xh * k3.v[i];
+                d.v[i] = k1[i] * gg - k2[i] - xh * k3[i];
             }
             st_bf<VEC>(a.out + so + (size_t)row * a.C + c0, d);
             if (a.out2) st_bf<VEC>(a.out2 + so + (size_t)row * a.C + c0, d);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) acc[0][i] += bfround(d.v[i]);
         }
-        ROW_LOOP_END
-    }
-    block_colsum<VEC, 1>(acc, red, a.G, a.TR);
-    float* rows = a.ws + gn_off_dbias(a);
-    const int nb = a.N * a.bpn;
-    store_row<VEC, 1>(rows + (size_t)blockIdx.x * a.C, acc, a.C, c0, r);
-    double* grp = reinterpret_cast<double*>(rows + tree_grp_off(1, nb, a.C));
-    if (!tree_reduce(rows, grp, a.counter + CTR, blockIdx.x, nb, a.C, fin, scratch)) return;
-    if (!a.dbias) return;
-    for (int c = t; c < a.C; c += NT) {
-        if (a.bias_bf16)
-            static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)fin[c]);
-        else
-            static_cast<float*>(a.dbias)[c] = (float)fin[c];
     }
 }
 
@@ -962,11 +1106,9 @@ void set_geo(A& a, const Geo& g) {
     a.rpb = g.rpb;
 }
 
-// host mirrors of the GN workspace offsets
-size_t gn_ws(int N, int bpn, int C) {
-    return align4(tree_ws_floats(N, bpn, 2 * C) + (size_t)N * 3 * C) + 2 * (size_t)N * 2 * C +
-           tree_ws_floats(1, N * bpn, C);
-}
+// host mirror of the GN workspace: stats rows [N*bpn][RW] (RW = 2NG + 3C covers both passes)
+inline int gn_rw_bwd(int C, int G) { return 2 * G + 3 * C; }
+size_t gn_ws(int N, int bpn, int C, int G) { return align4((size_t)N * bpn * gn_rw_bwd(C, G)); }
 
 inline int check_vec(int C, const char* what) {
     if (pick_vec(C) == 1 && C > NT) return fail(-2, (std::string(what) + ": C must be a multiple of 8 or <= 256").c_str());
@@ -974,16 +1116,9 @@ inline int check_vec(int C, const char* what) {
     return 0;
 }
 
-// GN geometry: per-sample workgroups so that all segments' counters fit one counter slot and
-// the whole grid stays <= TARGET_BLOCKS.
+// GN geometry: the grid stays <= TARGET_BLOCKS workgroups over the N samples
 inline Geo gn_geometry(int N, int HW, int C) {
-    int target = std::max(1, TARGET_BLOCKS / N);
-    Geo g = geometry(HW, C, pick_vec(C), target);
-    while (N * (1 + ngroups(g.nblk)) + 1 > CTR && target > 1) {
-        target /= 2;
-        g = geometry(HW, C, pick_vec(C), target);
-    }
-    return g;
+    return geometry(HW, C, pick_vec(C), std::max(1, TARGET_BLOCKS / N));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1100,8 +1235,7 @@ size_t psfm_netops_ws_floats(int M, int C) {
 }
 
 size_t psfm_gn_ws_floats(int N, int HW, int C, int G) {
-    (void)G;
-    return gn_ws(N, gn_geometry(N, HW, C).nblk, C);
+    return gn_ws(N, gn_geometry(N, HW, C).nblk, C, G);
 }
 
 int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y, void* stream) {
@@ -1124,9 +1258,8 @@ int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int
 }
 
 int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void* dx, void* dbias, int bias_bf16,
-                      float* ws, int* counter, void* stream) {
-    if (!dy || !y || !dx || !dbias || !ws || !counter || M < 1 || C < 1)
-        return fail(-1, "bias_act_bwd: bad arguments");
+                      float* ws, void* stream) {
+    if (!dy || !y || !dx || !dbias || !ws || M < 1 || C < 1) return fail(-1, "bias_act_bwd: bad arguments");
     if (int e = check_vec(C, "bias_act_bwd")) return e;
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
@@ -1134,16 +1267,17 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
     a.dy = dy;
     a.y = y;
     a.out = dx;
-    a.dbias = dbias;
     a.ws = ws;
-    a.counter = counter;
     a.M = M, a.C = C, a.act = act, a.bias_bf16 = bias_bf16, a.nblk = g.nblk;
     set_geo(a, g);
+    hipStream_t st = (hipStream_t)stream;
     if (vec == 8)
-        hipLaunchKernelGGL(k_bias_act_bwd<8>, dim3(g.nblk), dim3(NT), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(k_bias_act_bwd<8>, dim3(g.nblk), dim3(NT), 0, st, a);
     else
-        hipLaunchKernelGGL(k_bias_act_bwd<1>, dim3(g.nblk), dim3(NT), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(k_bias_act_bwd<1>, dim3(g.nblk), dim3(NT), 0, st, a);
     NETOPS_LAUNCH_CHECK();
+    const ColJob job{ws, dbias, C, 0, g.nblk, C, bias_bf16};
+    if (hipError_t e = launch_finish(&job, 1, st)) return fail((int)e, "bias_act_bwd: finish launch");
     return 0;
 }
 
@@ -1211,10 +1345,9 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
 static int gn_setup(GNArgs& a, int N, int HW, int C, int G, Geo& g, int& vec) {
     if (N < 1 || HW < 1 || C < 1 || G < 1 || C % G != 0) return fail(-1, "groupnorm: bad shape");
     if (int e = check_vec(C, "groupnorm")) return e;
+    if (C > MAX_C || G > MAX_NG || N > 64) return fail(-2, "groupnorm: C <= 512, G <= 128, N <= 64");
     vec = pick_vec(C);
     g = gn_geometry(N, HW, C);
-    if (N * (1 + ngroups(g.nblk)) + 1 > CTR) return fail(-2, "groupnorm: batch too large for one counter slot");
-    if (ngroups(N * g.nblk) + 1 > CTR) return fail(-2, "groupnorm: grid too large for one counter slot");
     a.N = N, a.HW = HW, a.C = C, a.NG = G, a.bpn = g.nblk;
     set_geo(a, g);
     return 0;
@@ -1222,8 +1355,8 @@ static int gn_setup(GNArgs& a, int N, int HW, int C, int G, Geo& g, int& vec) {
 
 int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
                     const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
-                    float* save_invstd, float* ws, int* counter, void* stream) {
-    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || !counter ||
+                    float* save_invstd, float* ws, void* stream) {
+    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws ||
         (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU))
         return fail(-1, "gn_act_fwd: bad arguments");
     GNArgs a{};
@@ -1235,7 +1368,7 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
     a.bias = bias, a.bias_bf16 = bias_bf16, a.gamma = gamma, a.beta = beta, a.eps = eps;
     a.save_mean = save_mean, a.save_invstd = save_invstd;
     a.out = static_cast<uint16_t*>(y);
-    a.ws = ws, a.counter = counter, a.act = act;
+    a.ws = ws, a.act = act, a.RW = 2 * G;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid(N * g.nblk);
     if (vec == 8) {
@@ -1252,8 +1385,8 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
 int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,
                     const float* gamma, const float* beta, const float* save_mean, const float* save_invstd, int N,
                     int HW, int C, int G, int act, void* dx, void* dres, void* dbias, float* dgamma, float* dbeta,
-                    float* ws, int* counter, void* stream) {
-    if (!dy || !x || !gamma || !beta || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
+                    float* ws, void* stream) {
+    if (!dy || !x || !gamma || !beta || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws ||
         (act != PSFM_ACT_NONE && act != PSFM_ACT_RELU && act != PSFM_ACT_ELU) || (res && !dres) || (bias && !dbias))
         return fail(-1, "gn_act_bwd: bad arguments");
     GNArgs a{};
@@ -1267,15 +1400,16 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
     a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
     a.out = static_cast<uint16_t*>(dx);
     a.out2 = static_cast<uint16_t*>(dres);
-    a.dbias = dbias, a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws, a.counter = counter, a.act = act;
+    a.ws = ws, a.act = act, a.RW = gn_rw_bwd(C, G);
+    a.dbias = dbias, a.dgamma = dgamma, a.dbeta = dbeta;
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid(N * g.nblk);
+    const dim3 grid(N * g.nblk), grid_apply(N * g.nblk + (C + 3) / 4);
     if (vec == 8) {
         hipLaunchKernelGGL(k_gn_bwd_stats<8>, grid, dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_gn_bwd_apply<8>, grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_gn_bwd_apply<8>, grid_apply, dim3(NT), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_gn_bwd_stats<1>, grid, dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_gn_bwd_apply<1>, grid, dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_gn_bwd_apply<1>, grid_apply, dim3(NT), 0, st, a);
     }
     NETOPS_LAUNCH_CHECK();
     return 0;

@@ -39,12 +39,13 @@ def _rows(t):
 
 
 SLOT = 256  # PSFM_NETOPS_COUNTER_INTS (include/psfm_netops.h)
-FWD, BWD = 0, 1  # counter slots: forward kernels | backward kernels (gn_act_bwd: slots 1 and 2)
+FWD, BWD = 0, 1  # counter slots of the (opt-in) fused BatchNorm: forward | backward kernels
 
 
 def _counter(module, device):
-    """Arrival counters of the module's fused reductions: 3 slots, zeroed once here and re-armed
-    by the kernels after every launch (graph replays reuse them)."""
+    """Arrival counters of the fused BatchNorm's single-launch reductions: zeroed once here and
+    re-armed by the kernels after every launch (graph replays reuse them).  GroupNorm and the
+    bias epilogues need none (partial rows + a next-launch reduction)."""
     c = getattr(module, "_psfm_counter", None)
     if c is None or c.device != device:
         c = torch.zeros(3 * SLOT, dtype=torch.int32, device=device)
@@ -59,7 +60,7 @@ def _slot(t, i):
 # ----------------------------------------------------------------------------------------------
 class _BiasAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, act, counter):
+    def forward(ctx, x, bias, act):
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -69,7 +70,7 @@ class _BiasAct(torch.autograd.Function):
         _hip.check(L.psfm_bias_act_fwd(_hip.ptr(x), _hip.ptr(bias), int(bias.dtype == torch.bfloat16), M, C, act,
                                        _hip.ptr(y), _hip.stream(x.device)), "psfm_bias_act_fwd")
         ctx.save_for_backward(y)
-        ctx.act, ctx.counter, ctx.bias_dtype, ctx.x_dtype = act, counter, bias.dtype, x.dtype
+        ctx.act, ctx.bias_dtype, ctx.x_dtype = act, bias.dtype, x.dtype
         return y
 
     @staticmethod
@@ -83,16 +84,17 @@ class _BiasAct(torch.autograd.Function):
         db = torch.empty(C, device=y.device, dtype=ctx.bias_dtype)
         ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=y.device, dtype=torch.float32)
         _hip.check(L.psfm_bias_act_bwd(_hip.ptr(dy), _hip.ptr(y), M, C, ctx.act, _hip.ptr(dx), _hip.ptr(db),
-                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _slot(ctx.counter, BWD),
-                                       _hip.stream(y.device)), "psfm_bias_act_bwd")
-        return dx, db, None, None
+                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _hip.stream(y.device)),
+                   "psfm_bias_act_bwd")
+        return dx, db, None
 
 
-def bias_act(x, bias, act, module):
-    """act(x + bias): x = conv output WITHOUT its bias (F.conv2d(..., None)); `module` owns the
-    reduction counter.  Sigmoid outputs are fp32 (they feed the fp32 photometric loss)."""
+def bias_act(x, bias, act, module=None):
+    """act(x + bias): x = conv output WITHOUT its bias (F.conv2d(..., None)).  Sigmoid outputs are
+    fp32 (they feed the fp32 photometric loss).  `module` (unused: the reductions need no device
+    state) is kept for the call sites."""
     if _fusable(x, "bias") and bias is not None:
-        return _BiasAct.apply(x, bias, act, _counter(module, x.device))
+        return _BiasAct.apply(x, bias, act)
     y = x if bias is None else x + bias.to(x.dtype).view(1, -1, 1, 1)
     if act == ACT_RELU:
         return torch.relu(y)
@@ -166,7 +168,7 @@ def bn_act(x, bn, relu=True, residual=None):
 # ----------------------------------------------------------------------------------------------
 class _GNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, bias, weight, beta, G, eps, act, counter):
+    def forward(ctx, x, res, bias, weight, beta, G, eps, act):
         x = _rows(x)
         res = _rows(res.to(x.dtype)) if res is not None else None
         N, C, H, W = x.shape
@@ -180,10 +182,9 @@ class _GNAct(torch.autograd.Function):
         bf = int(bias is not None and bias.dtype == torch.bfloat16)
         _hip.check(L.psfm_gn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf, _hip.ptr(weight), _hip.ptr(beta),
                                      ctypes.c_float(eps), N, HW, C, G, int(act), _hip.ptr(y), _hip.ptr(mean),
-                                     _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
-                   "psfm_gn_act_fwd")
+                                     _hip.ptr(invstd), _hip.ptr(ws), _hip.stream(dev)), "psfm_gn_act_fwd")
         ctx.save_for_backward(x, res, bias, weight, beta, mean, invstd)
-        ctx.G, ctx.act, ctx.counter = G, act, counter
+        ctx.G, ctx.act = G, act
         return y
 
     @staticmethod
@@ -204,8 +205,8 @@ class _GNAct(torch.autograd.Function):
         _hip.check(L.psfm_gn_act_bwd(_hip.ptr(dy), _hip.ptr(x), _hip.ptr(res), _hip.ptr(bias), bf, _hip.ptr(weight),
                                      _hip.ptr(beta), _hip.ptr(mean), _hip.ptr(invstd), N, HW, C, G, int(ctx.act),
                                      _hip.ptr(dx), _hip.ptr(dres), _hip.ptr(dbias), _hip.ptr(dw), _hip.ptr(db),
-                                     _hip.ptr(ws), _slot(ctx.counter, BWD), _hip.stream(dev)), "psfm_gn_act_bwd")
-        return dx, dres, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None, None
+                                     _hip.ptr(ws), _hip.stream(dev)), "psfm_gn_act_bwd")
+        return dx, dres, dbias, dw.to(weight.dtype), db.to(weight.dtype), None, None, None
 
 
 ACT_ELU = 3  # PSFM_ACT_ELU (GroupNorm only)
@@ -218,8 +219,7 @@ def gn_act(x, bias, gn, relu=True, act=None, residual=None):
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
     if (_fusable(x, "gn") and gn.affine and x.shape[1] % gn.num_groups == 0
             and (residual is None or (residual.shape == x.shape and residual.device == x.device))):
-        return _GNAct.apply(x, residual, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), act,
-                            _counter(gn, x.device))
+        return _GNAct.apply(x, residual, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), act)
     if residual is not None:
         x = x + residual
     if bias is not None:

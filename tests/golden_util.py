@@ -155,7 +155,7 @@ def grad_check_bounded(got, ref, ref_alts, sensitive, tol=1e-3, cap=0.15, max_fr
     return ok, stats
 
 
-def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=1e-4, pose_vec=None,
+def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=2e-4, pose_vec=None,
                         sensitive=None, **kw):
     """dL/dsig of the oracle evaluated in float64 — as is, and with the other fp32 outcome at every
     ambiguous place: (ties flipped), (kinks on the other bilinear cell), (both).  The float64

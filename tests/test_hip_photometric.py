@@ -134,7 +134,7 @@ def _seeded_inputs(seed, B, H, W, nctx=2):
     return image, ctx, gu.kitti_K(B, H, W), gu.pose_vecs(g, B, nctx), [gu.sigmoid_maps(g, B, H, W) for _ in range(4)]
 
 
-# shapes small enough that a seed with no flagged pixel exists (1e-4 px kink band, 5e-5 min / L1
+# shapes small enough that a seed with no flagged pixel exists (2e-4 px kink band, 5e-5 min / 1e-4 L1
 # near-ties over 4 scales x 2 contexts): partial band (H < RB), one / two / three stripes
 @pytest.mark.parametrize("B,H,W", [(1, 8, 40), (1, 6, 70), (1, 5, 130)])
 def test_kink_free_inputs_match_oracle_tightly(dev, B, H, W):

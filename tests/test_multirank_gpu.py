@@ -58,17 +58,32 @@ def _worker(rank, world, init_file, out_dir, mode):
     loader = ResidentLoader(ds, B, get_datasampler(ds, "train"), dev)
     batch = bench.net_layout(loader.next_into(None))
     seen = [loader.partition[0:B]]
+    # this rank's own packed gradient as it enters the all-reduce (host-enqueued between the two
+    # graph replays) and the averaged buffer the optimizer graph read
+    own, avg, real = [], [], dist.all_reduce
+
+    def spy(t, *a, **k):
+        if t.numel() > 1000 and not tr._capturing and tr.graphs is not None:
+            torch.cuda.synchronize()
+            own.append(t.detach().cpu().clone())
+        return real(t, *a, **k)
+    dist.all_reduce = spy
     losses = []
-    for i in range(STEPS):
-        if i:
-            k = loader.step_in_epoch
-            loader.next_into(tr.static_batch)
-            seen.append(loader.partition[k * B:(k + 1) * B])
-        losses.append(float(tr.train_step(batch)["loss"]))
-    torch.cuda.synchronize()
+    try:
+        for i in range(STEPS):
+            if i:
+                k = loader.step_in_epoch
+                loader.next_into(tr.static_batch)
+                seen.append(loader.partition[k * B:(k + 1) * B])
+            losses.append(float(tr.train_step(batch)["loss"]))
+            torch.cuda.synchronize()
+            avg.append(tr.flat_grad.detach().cpu().clone())
+    finally:
+        dist.all_reduce = real
     assert len(tr.graphs) == 2   # split: step graph | all_reduce | optimizer graph
-    out = {"seen": torch.tensor(seen), "losses": torch.tensor(losses),
-           "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()}}
+    assert len(own) == STEPS, len(own)
+    out = {"seen": torch.tensor(seen), "losses": torch.tensor(losses), "own": torch.stack(own),
+           "avg": torch.stack(avg), "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()}}
     if tr.fused is not None:
         out["master"] = tr.fused.master.cpu()
         assert int(tr.fused.step_count) == STEPS
@@ -116,7 +131,10 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
              "intrinsics": torch.stack([x["intrinsics"] for x in s]).to(dev)}
         return bench.net_layout(b)
 
-    params = [p for p in model.parameters() if p.requires_grad]
+    params = [p for g in opt.param_groups for p in g["params"]]   # the trainer's pack order
+
+    def flat(grads):
+        return torch.cat([g.reshape(-1).float() for g in grads if g is not None]).cpu()
     try:
         torch.backends.cudnn.deterministic = True
         for step in range(STEPS):
@@ -128,8 +146,13 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
                 assert float(out["loss"]) == float(r[k]["losses"][step]), (step, k)
                 out["loss"].sum().backward()
                 per_rank.append([p.grad.clone() if p.grad is not None else None for p in params])
+                # the rank's packed gradient of the same samples (graph replay vs eager)
+                got, ref = r[k]["own"][step], flat(per_rank[-1])
+                assert torch.equal(got, ref), (step, k, float((got - ref).abs().max()))
             for p, g0, g1 in zip(params, *per_rank):
                 p.grad = None if g0 is None else (g0 + g1) * 0.5
+            got, ref = r[0]["avg"][step], flat([p.grad for p in params])
+            assert torch.equal(got, ref), (step, float((got - ref).abs().max()))
             opt.step()
         torch.cuda.synchronize()
     finally:

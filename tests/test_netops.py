@@ -27,6 +27,16 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+def _check_conv_bias_grad(db, dx, db_ref, dx_ref, shape, rel):
+    """Fused GroupNorm conv-bias gradient vs the fp32 chain: within the bf16 rounding noise of the
+    M = N*H*W summands (4 sigma) + rel * max, and as close to the column sum of our own bf16 dx."""
+    M = shape[0] * shape[2] * shape[3]
+    noise = 4 * M ** 0.5 * 2 ** -8 * dx_ref.float().pow(2).mean().sqrt()
+    own = dx.double().sum((0, 2, 3)).float()
+    assert (db.float() - db_ref).abs().max() <= noise + rel * db_ref.abs().max()
+    assert (db.float() - own).abs().max() <= noise + rel * own.abs().max()
+
+
 @pytest.fixture(scope="module")
 def dev():
     if not torch.cuda.is_available():
@@ -146,13 +156,10 @@ def test_gn_act_matches_torch(dev, shape):
     y.backward(_cl(dy))
     yr.backward(dy.float())
     _close(x.grad, xr.grad, 2e-2)
-    # conv-bias gradient = column sum of the stored bf16 dx (what autograd sums): exact w.r.t.
-    # our dx; against the fp32 reference it carries the bf16 rounding noise of M summands
-    own = x.grad.double().sum((0, 2, 3))
-    assert torch.allclose(conv_b.grad.double(), own, rtol=1e-2, atol=1e-3 * own.abs().max().item() + 1e-6)
-    M = shape[0] * shape[2] * shape[3]
-    noise = 4 * M ** 0.5 * 2 ** -8 * xr.grad.float().pow(2).mean().sqrt()
-    assert (conv_b.grad.float() - br.grad).abs().max() <= noise + 3e-2 * br.grad.abs().max()
+    # conv-bias gradient in closed form from the statistics rows (sum_hw dx = k1 S1 - HW k2 - k3 X):
+    # the sum of the exact dx; autograd would sum the bf16-rounded dx instead, which differs from
+    # it by the rounding noise of M summands — both within that noise of the fp32 reference
+    _check_conv_bias_grad(conv_b.grad, x.grad, br.grad, xr.grad, shape, 3e-2)
     _close(gn.weight.grad, wr.grad, 2e-2)
     _close(gn.bias.grad, betar.grad, 2e-2)
 
@@ -291,7 +298,70 @@ def test_gn_elu_matches_torch(dev, shape, residual, bias):
     if residual:
         assert torch.equal(r.grad, x.grad)
     if bias:
-        own = x.grad.double().sum((0, 2, 3))
-        assert torch.allclose(conv_b.grad.double(), own, rtol=1e-2, atol=1e-3 * own.abs().max().item() + 1e-6)
+        _check_conv_bias_grad(conv_b.grad, x.grad, br.grad, xr.grad, shape, 3e-2)
     _close(gn.weight.grad, wr.grad, 2e-2)
     _close(gn.bias.grad, betar.grad, 2e-2)
+
+
+@gpu
+@pytest.mark.parametrize("shape,act,residual", [((2, 64, 24, 80), FU.ACT_ELU, True), ((4, 16, 96, 320), FU.ACT_RELU, False)])
+def test_gn_forward_only_captures_into_a_hip_graph(dev, shape, act, residual):
+    """The forward-only GroupNorm call (eval / no_grad: PackNet's eval forward) captured into a HIP
+    graph, three calls per graph: replays equal the eager calls bit for bit, also after the input
+    changed (a stale partial row or a stats pass outside the graph would show).  This is the call
+    whose capture once crashed (round-2 commit 2c99221); the reductions now keep no device state
+    between launches (no lazily allocated arrival counters)."""
+    g = torch.Generator(device="cpu").manual_seed(6)
+    C = shape[1]
+    gn = nn.GroupNorm(16, C).to(dev)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    b = torch.randn(C, generator=g).to(dev, torch.bfloat16)
+    xs = [_cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) for _ in range(2)]
+    rs = [_cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) if residual else None for _ in range(2)]
+    call = lambda x, r: FU.gn_act(x, b, gn, act=act, residual=r)  # noqa: E731
+    with torch.no_grad():
+        eager = [call(x, r) for x, r in zip(xs, rs)]
+        x_st = xs[0].clone()
+        r_st = rs[0].clone() if residual else None
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            call(x_st, r_st)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            outs = [call(x_st, r_st) for _ in range(3)]
+        for k in (0, 1):
+            x_st.copy_(xs[k])
+            if residual:
+                r_st.copy_(rs[k])
+            graph.replay()
+            torch.cuda.synchronize()
+            for y in outs:
+                assert torch.equal(y, eager[k])
+
+
+@gpu
+def test_gn_and_bias_reductions_are_deterministic(dev):
+    """GroupNorm + ELU and bias + ReLU forward / backward repeated: every output and gradient bit
+    identical run to run (fixed-order partial-row reductions, no atomics)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    gn = nn.GroupNorm(16, 64).to(dev)
+    x = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
+    r = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
+    b = torch.randn(64, generator=g).to(dev, torch.bfloat16)
+    dy = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
+    outs = []
+    for _ in range(3):
+        xi, ri, bi = x.clone().requires_grad_(True), r.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        gn.zero_grad(set_to_none=True)
+        y = FU.gn_act(xi, bi, gn, act=FU.ACT_ELU, residual=ri)
+        z = FU.bias_act(y, bi, FU.ACT_RELU)
+        z.backward(dy)
+        torch.cuda.synchronize()
+        outs.append([t.detach().clone() for t in (y, z, xi.grad, ri.grad, bi.grad, gn.weight.grad, gn.bias.grad)])
+    for o in outs[1:]:
+        for a_, b_ in zip(o, outs[0]):
+            assert torch.equal(a_, b_)
