@@ -213,3 +213,14 @@ def pose_check_bounded(got, ref64, bound, tol=1e-3):
     stats = {"rel_err_vs_fp64": float(np.abs(got - ref).max() / scale),
              "flagged_share_of_max": float(bound.max() / scale), "worst_err_over_allowance": ratio}
     return ratio <= 1.0, stats
+
+
+def decoder_inputs(B=1, H=32, W=96, seed=91):
+    """Seeded ResNet18 encoder features (post-ReLU, H/2 .. H/32) and upstream gradients for the
+    decoder goldens (tools/gen_goldens.py gen_decoders; tests/test_decoders.py regenerates them)."""
+    g = torch.Generator().manual_seed(seed)
+    chans = [64, 64, 128, 256, 512]
+    feats = [torch.relu(torch.randn(B, c, H >> (i + 1), W >> (i + 1), generator=g)) for i, c in enumerate(chans)]
+    up_disp = [torch.randn(B, 1, H >> i, W >> i, generator=g) for i in range(4)]
+    up_pose = torch.randn(B, 2, 1, 6, generator=g)
+    return feats, up_disp, up_pose

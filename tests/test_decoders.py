@@ -1,0 +1,125 @@
+"""ResNet-side heads of BASELINE configs 1 / 2 against the reference itself: DepthDecoder
+(packnet_sfm/networks/layers/resnet/depth_decoder.py:16-64) and PoseDecoder (pose_decoder.py:13-53)
+fed seeded encoder features with the golden's weights (tests/golden/decoders_resnet.npz, written by
+tools/gen_goldens.py gen_decoders from the reference).  The torchvision trunk in front of them
+stays parity-unpinned (torchvision is absent); these heads are not.
+
+  * CPU (the reference op chain): outputs 1e-5, every pinned gradient element 1e-4 * max;
+  * GPU fp32 (MIOpen convolutions): 1e-3 * max per element;
+  * GPU bf16 autocast, channels_last — the production path, where the decoder runs the HIP
+    epilogues psfm_upcat (upsample + skip cat) and psfm_bias_act (bias + ReLU / sigmoid): every
+    output / gradient within 2x the error of the reference's own op chain under the same autocast
+    (+ 1e-2 of max), and the fused kernels must actually have run."""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+
+
+def _nets(dev):
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.networks.layers.resnet.depth_decoder import DepthDecoder
+    from packnet_sfm_amd.networks.layers.resnet.pose_decoder import PoseDecoder
+    dec = DepthDecoder(np.array([64, 64, 128, 256, 512]))
+    pdec = PoseDecoder(np.array([64, 64, 128, 256, 512]), num_input_features=1, num_frames_to_predict_for=2)
+    gu.det_init_(dec)
+    gu.det_init_(pdec)
+    return dec.to(dev), pdec.to(dev)
+
+
+def _run(dev, amp=False, channels_last=False):
+    """(outputs, gradients) of both decoders for the golden's inputs / upstream gradients."""
+    feats, up_disp, up_pose = gu.decoder_inputs()
+    dec, pdec = _nets(dev)
+    fmt = torch.channels_last if channels_last else torch.contiguous_format
+    if channels_last:
+        dec, pdec = dec.to(memory_format=fmt), pdec.to(memory_format=fmt)
+    f = [t.to(dev).contiguous(memory_format=fmt).requires_grad_(True) for t in feats]
+    ctx = torch.autocast("cuda", dtype=torch.bfloat16) if amp else torch.autocast("cpu", enabled=False)
+    with ctx:
+        out = dec(f)
+        last = f[-1].detach().clone().requires_grad_(True)
+        aa, tr = pdec([[None, None, None, None, last]])
+    disps = [out[("disp", i)].float() for i in range(4)]
+    pose = torch.cat([aa, tr], -1).float()
+    (sum((d * u.to(dev)).sum() for d, u in zip(disps, up_disp)) + (pose * up_pose.to(dev)).sum()).backward()
+    res = {f"disp{i}": d.detach().cpu() for i, d in enumerate(disps)}
+    res.update(axisangle=aa.detach().float().cpu(), translation=tr.detach().float().cpu(),
+               grad_pose_feat=last.grad.float().cpu())
+    res.update({f"grad_feat{i}": t.grad.float().cpu() for i, t in enumerate(f)})
+    res.update({f"grad:{n}": p.grad.float().cpu() for n, p in dec.named_parameters()})
+    res.update({f"pgrad:{n}": p.grad.float().cpu() for n, p in pdec.named_parameters()})
+    return res
+
+
+def _keys(z):
+    return [k for k in z if k.startswith(("disp", "axisangle", "translation", "grad_feat", "grad_pose_feat",
+                                          "grad:", "pgrad:"))]
+
+
+def _err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _check(res, z, tol):
+    bad = {k: _err(res[k], z[k]) for k in _keys(z) if _err(res[k], z[k]) > tol}
+    assert not bad, bad
+    for kind, names, norms in (("grad:", "dec_grad_names", "dec_grad_norms"), ("pgrad:", "pose_grad_names",
+                                                                                 "pose_grad_norms")):
+        for n, ref in zip(z[names], z[norms]):
+            got = float(res[f"{kind}{n}"].double().norm())
+            assert abs(got - ref) <= tol * ref + 1e-12, (n, got, ref)
+
+
+def test_decoders_match_reference_cpu():
+    z = gu.load_golden("decoders_resnet")
+    _check(_run(torch.device("cpu")), z, 1e-4)
+
+
+@pytest.mark.gpu
+def test_decoders_match_reference_gpu_fp32():
+    import __graft_entry__
+    __graft_entry__.build()
+    z = gu.load_golden("decoders_resnet")
+    _check(_run(torch.device("cuda:0")), z, 1e-3)
+
+
+@pytest.mark.gpu
+def test_decoders_bf16_fused_epilogues_as_close_as_the_reference_chain():
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.networks.layers import fused as FU
+    z = gu.load_golden("decoders_resnet")
+    dev = torch.device("cuda:0")
+    calls = {"bias": 0, "upcat": 0}
+    ob, ou = FU._BiasAct.apply, FU._UpCat.apply
+    prev = dict(FU.FUSE), FU.UPCAT
+
+    def count(kind, fn):
+        def wrapped(*a):
+            calls[kind] += 1
+            return fn(*a)
+        return wrapped
+    FU._BiasAct.apply, FU._UpCat.apply = count("bias", ob), count("upcat", ou)
+    try:
+        FU.FUSE.update(bias=True)
+        FU.UPCAT = True
+        fused = _run(dev, amp=True, channels_last=True)
+        assert calls["bias"] == 14 and calls["upcat"] == 5, calls   # 10 ConvBlocks + 4 heads, 5 up-stages
+        FU.FUSE.update(bias=False)
+        FU.UPCAT = False
+        plain = _run(dev, amp=True, channels_last=True)
+    finally:
+        FU._BiasAct.apply, FU._UpCat.apply = ob, ou
+        FU.FUSE.update(prev[0])
+        FU.UPCAT = prev[1]
+    worst = []
+    for k in _keys(z):
+        ef, ep = _err(fused[k], z[k]), _err(plain[k], z[k])
+        worst.append((ef, ep, k))
+        assert ef <= 2.0 * ep + 1e-2, (k, ef, ep)
+    worst.sort(reverse=True)
+    print("largest fused-vs-reference errors (fused, reference op chain in bf16):",
+          [(k, f"{a:.2e}", f"{b:.2e}") for a, b, k in worst[:4]])

@@ -303,3 +303,55 @@ def test_ddad_packnet_san_four_camera_step_matches_oracle_on_its_outputs():
     assert missing == ["depth_net.weight", "depth_net.bias"], missing[:5]
     bad = [n for n, p in model.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
     assert not bad, bad[:5]
+
+
+# -------------------------------------------------------------------------------------------------
+# per-element network-gradient parity: the golden's own upstream gradients
+# (dL/d inverse-depth outputs, dL/d pose vector: no min-reprojection flip can enter) fed into the
+# build's nets; every element of the pinned layers' gradients (inverse-depth heads, the first pack /
+# unpack Conv3d — the HIP pack3d kernels on the GPU — and the PoseNet head) vs the reference
+def _net_grads_vs_golden(depth, pose, z, dev, seed, tol):
+    g = torch.Generator().manual_seed(seed)
+    rgb = gu.smooth_texture(g, 1, 3, 64, 192).to(dev)
+    ctx = [gu.smooth_texture(g, 1, 3, 64, 192).to(dev) for _ in range(2)]
+    depth, pose = depth.to(dev).train(), pose.to(dev).train()
+    inv = depth(rgb)["inv_depths"]
+    vec = pose(rgb, ctx)
+    up = [torch.from_numpy(z[f"up_inv{i}"]).to(dev) for i in range(len(inv))]
+    assert [tuple(a.shape) for a in inv] == [tuple(u.shape) for u in up]
+    (sum((a * u).sum() for a, u in zip(inv, up)) + (vec * torch.from_numpy(z["up_vec"]).to(dev)).sum()).backward()
+    params = {f"depth_net.{n}": p for n, p in depth.named_parameters()}
+    params.update({f"pose_net.{n}": p for n, p in pose.named_parameters()})
+    names = [str(n) for n in z["full_grad_names"]]
+    assert any("conv3d" in n for n in names) and any("pose_pred" in n for n in names)
+    errs = {}
+    for n in names:
+        errs[n] = gu.rel_err(params[n].grad.detach().cpu(), z[f"full_grad:{n}"])
+    print("per-element gradient error / max:", {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if v > tol}
+    assert not bad, bad
+
+
+def test_packnet_layer_gradients_match_reference_cpu():
+    depth, pose = _packnet_model()
+    torch.set_num_threads(8)
+    _net_grads_vs_golden(depth, pose, gu.load_golden("step_packnet_tiny"), torch.device("cpu"), 77, 1e-4)
+
+
+def test_packnet_san_layer_gradients_match_reference_cpu():
+    depth, pose = _packnet_san_model()
+    torch.set_num_threads(8)
+    _net_grads_vs_golden(depth, pose, gu.load_golden("step_packnet_san_tiny"), torch.device("cpu"), 78, 1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["packnet", "packnet_san"])
+def test_packnet_layer_gradients_match_reference_gpu_fp32(which):
+    """fp32 on the GPU: MIOpen convolutions + the HIP pack / unpack Conv3d kernels, 1e-3 * max per
+    element of every pinned layer gradient."""
+    import __graft_entry__
+    __graft_entry__.build()
+    torch.backends.cudnn.benchmark = False
+    depth, pose = _packnet_model() if which == "packnet" else _packnet_san_model()
+    z = gu.load_golden("step_packnet_tiny" if which == "packnet" else "step_packnet_san_tiny")
+    _net_grads_vs_golden(depth, pose, z, torch.device("cuda:0"), 77 if which == "packnet" else 78, 1e-3)

@@ -286,6 +286,53 @@ def gen_kitti_1img():
     print(f"  loss_kitti_1img: loss={float(res['loss'][0]):.6f}")
 
 
+# per-element network-gradient parity: the gradient arriving at the depth net's
+# raw inverse-depth outputs and at the pose net's output vector, and the full gradients of a few
+# layers (inverse-depth heads, one pack / unpack Conv3d, the PoseNet head) — a test feeds the same
+# upstream gradients into the build's nets and compares these layers element by element
+FULL_GRAD_PATTERNS = ("disp1_layer.", "disp2_layer.", "disp3_layer.", "disp4_layer.", "pack1.conv3d.",
+                      "unpack1.conv3d.", "pose_pred.")
+
+
+def _retain_net_outputs(model):
+    kept = {}
+    d_fwd, p_fwd = model.depth_net.forward, model.pose_net.forward
+
+    def depth_fwd(*a, **k):
+        o = d_fwd(*a, **k)
+        if "inv" not in kept and o["inv_depths"][0].requires_grad:
+            # clones: the coarse maps are also used INSIDE the net (upsampled into the next decoder
+            # stage); the gradient of the clone is the one arriving from outside (the loss) only
+            o = dict(o, inv_depths=[t.clone() for t in o["inv_depths"]])
+            for t in o["inv_depths"]:
+                t.retain_grad()
+            kept["inv"] = o["inv_depths"]
+        return o
+
+    def pose_fwd(*a, **k):
+        v = p_fwd(*a, **k)
+        if "vec" not in kept and v.requires_grad:
+            v.retain_grad()
+            kept["vec"] = v
+        return v
+    model.depth_net.forward, model.pose_net.forward = depth_fwd, pose_fwd
+    return kept
+
+
+def _net_grad_fixture(model, kept):
+    res = {f"up_inv{i}": np32(t.grad) for i, t in enumerate(kept["inv"])}
+    res["up_vec"] = np32(kept["vec"].grad)
+    names = []
+    for net in ("depth_net", "pose_net"):
+        for n, p in getattr(model, net).named_parameters():
+            if p.grad is not None and any(k in n for k in FULL_GRAD_PATTERNS):
+                assert p.numel() <= 4096, (n, p.shape)
+                names.append(f"{net}.{n}")
+                res[f"full_grad:{net}.{n}"] = np32(p.grad)
+    res["full_grad_names"] = np.array(names)
+    return res
+
+
 def gen_step_packnet():
     """SelfSupModel(PackNet01 '1A' + PoseNet) forward+backward, B=1, 64x192."""
     from packnet_sfm.models.SelfSupModel import SelfSupModel
@@ -307,6 +354,7 @@ def gen_step_packnet():
     K = gu.kitti_K(B, H, W)
     batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx,
                  intrinsics=K, distortion_coeffs=K, mask=torch.ones(B, 1, H, W))
+    kept = _retain_net_outputs(model)
     out = model(batch, progress=0.0)
     out["loss"].sum().backward()
     names, norms = [], []
@@ -324,7 +372,8 @@ def gen_step_packnet():
                inv0_samples=np32(inv0.reshape(-1)[::997]),
                pose_mats=np32(torch.stack([p.mat for p in out["poses"]], 1)),
                grad_names=np.array([names[i] for i in sel]),
-               grad_norms=np.array([norms[i] for i in sel], dtype=np.float64))
+               grad_norms=np.array([norms[i] for i in sel], dtype=np.float64),
+               **_net_grad_fixture(model, kept))
     np.savez_compressed(os.path.join(OUT, "step_packnet_tiny.npz"), **res)
     print(f"  step_packnet_tiny: loss={float(res['loss'][0]):.6f}")
 
@@ -357,6 +406,7 @@ def gen_step_packnet_san():
     K = gu.kitti_K(B, H, W)
     batch = dict(rgb=rgb, rgb_context=ctx, rgb_original=rgb, rgb_context_original=ctx,
                  intrinsics=K, distortion_coeffs=K, mask=torch.ones(B, 1, H, W))
+    kept = _retain_net_outputs(model)
     out = model(batch, progress=0.0)
     out["loss"].sum().backward()
     names, norms = [], []
@@ -366,6 +416,7 @@ def gen_step_packnet_san():
                 names.append(f"{net}.{n}")
                 norms.append(float(p.grad.double().norm()))
     sel = list(range(0, len(names), max(1, len(names) // 16)))[:16]
+    grads_fixture = _net_grad_fixture(model, kept)
     inv = out["inv_depths"]
     model.depth_net.eval()
     with torch.no_grad():
@@ -381,7 +432,7 @@ def gen_step_packnet_san():
                param_names=np.array([n for n, _ in model.depth_net.named_parameters()]),
                param_count=np.int64(sum(p.numel() for p in model.depth_net.parameters())),
                grad_names=np.array([names[i] for i in sel]),
-               grad_norms=np.array([norms[i] for i in sel], dtype=np.float64))
+               grad_norms=np.array([norms[i] for i in sel], dtype=np.float64), **grads_fixture)
     np.savez_compressed(os.path.join(OUT, "step_packnet_san_tiny.npz"), **res)
     print(f"  step_packnet_san_tiny: loss={float(res['loss'][0]):.6f} params={int(res['param_count'])}")
 
@@ -428,6 +479,56 @@ def gen_fisheye():
     np.savez_compressed(os.path.join(OUT, "fisheye_small.npz"), **res)
 
 
+def gen_decoders():
+    """ResNet-side heads of BASELINE configs 1/2 that the reference can pin without torchvision:
+    DepthDecoder (networks/layers/resnet/depth_decoder.py:16-64: 5 up-stages, skips, sigmoid heads)
+    and PoseDecoder (pose_decoder.py:13-53) with det_init_ weights, fed seeded encoder features;
+    forward outputs and, for a seeded upstream gradient, the input-feature gradients, every bias
+    gradient and the full weight gradients of the small layers, plus all gradient norms."""
+    from packnet_sfm.networks.layers.resnet.depth_decoder import DepthDecoder
+    from packnet_sfm.networks.layers.resnet.layers import disp_to_depth
+    from packnet_sfm.networks.layers.resnet.pose_decoder import PoseDecoder
+    feats, up_disp, up_pose = gu.decoder_inputs()
+    res = {"seed": np.int64(91)}
+    dec = DepthDecoder(np.array([64, 64, 128, 256, 512]))
+    gu.det_init_(dec)
+    f = [t.clone().requires_grad_(True) for t in feats]
+    out = dec(f)
+    disps = [out[("disp", i)] for i in range(4)]
+    sum((d * u).sum() for d, u in zip(disps, up_disp)).backward()
+    for i, d in enumerate(disps):
+        res[f"disp{i}"] = np32(d)
+        sd, dd = disp_to_depth(d.detach(), 0.1, 100.0)
+        res[f"scaled_disp{i}"], res[f"depth{i}"] = np32(sd), np32(dd)
+    for i, t in enumerate(f):
+        res[f"grad_feat{i}"] = np32(t.grad)
+    names, norms = [], []
+    for n, p in dec.named_parameters():
+        names.append(n)
+        norms.append(float(p.grad.double().norm()))
+        if n.endswith("bias") or p.numel() <= 4096:
+            res[f"grad:{n}"] = np32(p.grad)
+    res["dec_grad_names"], res["dec_grad_norms"] = np.array(names), np.array(norms, dtype=np.float64)
+    pdec = PoseDecoder(np.array([64, 64, 128, 256, 512]), num_input_features=1, num_frames_to_predict_for=2)
+    gu.det_init_(pdec)
+    last = feats[-1].clone().requires_grad_(True)
+    axisangle, translation = pdec([[None, None, None, None, last]])
+    pose = torch.cat([axisangle, translation], -1)
+    (pose * up_pose).sum().backward()
+    res["axisangle"], res["translation"] = np32(axisangle), np32(translation)
+    res["grad_pose_feat"] = np32(last.grad)
+    names, norms = [], []
+    for n, p in pdec.named_parameters():
+        names.append(n)
+        norms.append(float(p.grad.double().norm()))
+        if n.endswith("bias") or p.numel() <= 4096:
+            res[f"pgrad:{n}"] = np32(p.grad)
+    res["pose_grad_names"], res["pose_grad_norms"] = np.array(names), np.array(norms, dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "decoders_resnet.npz"), **res)
+    print(f"  decoders_resnet: disp0 sum={float(disps[0].double().sum()):.6f} "
+          f"pose sum={float(pose.double().sum()):.6e}")
+
+
 def gen_depth_metrics():
     g = torch.Generator().manual_seed(31)
     B, H, W = 2, 192, 640
@@ -465,5 +566,5 @@ if __name__ == "__main__":
         with contextlib.redirect_stdout(quiet) if w == "metrics" else contextlib.nullcontext():
             {"geom": gen_geom, "ssim": gen_ssim, "losses": gen_losses, "kitti": gen_kitti_1img,
              "metrics": gen_depth_metrics, "step": gen_step_packnet, "fisheye": gen_fisheye,
-             "step_san": gen_step_packnet_san}[w]()
+             "step_san": gen_step_packnet_san, "decoders": gen_decoders}[w]()
     print("done")
