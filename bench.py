@@ -129,6 +129,21 @@ def parse(argv=None):
     return args
 
 
+def source_hash():
+    """sha256 (16 hex) of the HIP library's sources (csrc/*.hip, csrc/*.h, include/*.h, sorted): the
+    code revision a stamped PMC profile was taken on."""
+    import hashlib
+    h = hashlib.sha256()
+    for d, exts in ((os.path.join(ROOT, "packnet-sfm-resnet-san_amd", "csrc"), (".hip", ".h")),
+                    (os.path.join(ROOT, "include"), (".h",))):
+        for f in sorted(os.listdir(d)):
+            if f.endswith(exts):
+                h.update(f.encode())
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def config_key(args):
     """Identifies the workload of a stamped profile file (profiles/pmc/<key>.json)."""
     return (f"{args.depth_net}+{args.pose_net}_B{args.batch}x{args.cameras}_{args.height}x{args.width}_{args.amp}"
@@ -322,13 +337,18 @@ def time_photometric_kernels(args, trainer, batch, HP):
 
 def stamped_profile(args):
     """profiles/pmc/<config_key>.json written by tools/pmc_bench.py from rocprofv3 --pmc passes over
-    THIS command's workload; None when no file carries this config's key."""
+    THIS command's workload on THIS source revision; (None, path, why) when no file carries this
+    config's key or its source hash differs from the library built from the current sources."""
     path = os.path.join(ROOT, "profiles", "pmc", config_key(args) + ".json")
     if not os.path.exists(path):
-        return None, path
+        return None, path, "absent for this config"
     with open(path) as f:
         prof = json.load(f)
-    return (prof if prof.get("config_key") == config_key(args) else None), path
+    if prof.get("config_key") != config_key(args):
+        return None, path, "config key mismatch"
+    if prof.get("source_hash") != source_hash():
+        return None, path, f"stale: taken on sources {prof.get('source_hash')}, library built from {source_hash()}"
+    return prof, path, None
 
 
 def roofline(args, ktimes):
@@ -353,8 +373,9 @@ def roofline(args, ktimes):
                      "frac": round(bytes_step / (group_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
            "kernels_us_per_step": {k: round(v, 2) for k, v in ktimes.items()},
            "timing": "HIP events around graph replays of each recorded C-ABI call (replay stream)"}
-    prof, path = stamped_profile(args)
-    out["profile"] = os.path.relpath(path, ROOT) + ("" if prof else " (absent for this config: traffic null)")
+    prof, path, why = stamped_profile(args)
+    out["profile"] = os.path.relpath(path, ROOT) + ("" if prof else f" ({why}: traffic null)")
+    out["source_hash"] = source_hash()
     if prof:
         k = prof["kernels"].get(dom)
         if k and k.get("hbm_bytes") is not None:

@@ -124,3 +124,42 @@ def test_decoder_merge_cat_feeds_the_same_bf16_input():
     yr.backward(gy)
     for p, r in zip(parts, refs):
         assert p.grad.dtype == r.grad.dtype and torch.equal(p.grad, r.grad)
+
+
+@pytest.mark.parametrize("mode,d,shape", [(0, 8, (6, 64, 192, 640)), (0, 4, (4, 32, 384, 640)),
+                                          (1, 8, (6, 64, 96, 320)), (1, 4, (4, 64, 192, 320))])
+def test_real_layer_shapes_match_torch_chain(dev, mode, d, shape):
+    """The first pack layer of PackNet01 (d = 8, B = 6, 192x640) / PackNetSAN01 on DDAD (d = 4,
+    4 cameras, 384x640) and the last unpack layers, in the production storage (bf16, channels_last:
+    the grid-size-dependent XCD-aware dx mapping and the o-in-passes staging at their real sizes)
+    against the reference op chain in fp32 on the same device (packing / Conv3d / PixelShuffle,
+    layers01.py:213-286) on the same bf16-rounded inputs: outputs and input gradient 1e-2 * max
+    (one bf16 rounding), weight / bias gradients 2e-3 relative."""
+    from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
+    from packnet_sfm_amd.networks.layers.packnet.layers01 import packing
+    g = torch.Generator(device="cpu").manual_seed(7 + mode + d)
+    x = torch.randn(shape, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2).to(dev).to(torch.bfloat16).float()
+    b = (torch.randn(d, generator=g) * 0.1).to(dev)
+    xg, wg, bg = x.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = Pack3dFn.apply(xg, wg, bg, mode, 2)
+    gy = torch.randn(y.shape, generator=g).to(dev, torch.bfloat16)
+    y.backward(gy.contiguous(memory_format=torch.channels_last))
+    # reference chain in fp32 on the same device
+    xr = x.float().contiguous().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    v = packing(xr, 2) if mode == 0 else xr
+    yr = torch.nn.functional.conv3d(v.unsqueeze(1), wr, br, 1, 1)
+    B_, c, dd, h, ww = yr.shape
+    yr = yr.reshape(B_, c * dd, h, ww)
+    if mode == 1:
+        yr = torch.nn.functional.pixel_shuffle(yr, 2)
+    yr.backward(gy.float())
+    torch.cuda.synchronize()
+
+    def rel(a, r):
+        return float((a.float() - r.float()).abs().max() / r.float().abs().max())
+    errs = {"y": rel(y, yr), "dx": rel(xg.grad, xr.grad), "dW": rel(wg.grad, wr.grad), "db": rel(bg.grad, br.grad)}
+    print(f"mode {mode} d={d} {shape}: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert errs["y"] <= 1e-2 and errs["dx"] <= 1e-2, errs
+    assert errs["dW"] <= 2e-3 and errs["db"] <= 2e-3, errs

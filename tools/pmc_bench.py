@@ -10,6 +10,8 @@ in KiB and on gfx950 reports half the bytes of wide coalesced reads -> read byte
 uncalibrated); WRITE_SIZE is in KiB, exact for streaming stores -> 1024 * WRITE_SIZE.
 
 usage: pmc_bench.py CONFIG_KEY OUT.json PASS_DIR [PASS_DIR ...]
+The profile is stamped with bench.source_hash() (the library sources it was taken on): bench.py
+ignores a profile whose stamp differs from the current sources.
 """
 import collections
 import csv
@@ -21,7 +23,10 @@ import sys
 NAMES = {"k12_fwd_grad": "K12_photometric_fwd_grad", "k0_unwarped": "K0_unwarped", "k_sig_sum": "sig_sum",
          "k_grad_finish": "grad_finish", "k_finalize": "finalize", "k_pose_reduce": "pose_grad_reduce",
          "k1_forward": "K1_photometric_fwd", "k2_backward": "K2_photometric_bwd",
-         "k_p3d_fwd": "p3d_fwd", "k_p3d_bwd_x": "p3d_bwd_x", "k_p3d_bwd_w": "p3d_bwd_w", "k_adam": "adam"}
+         "k_p3d_fwd": "p3d_fwd", "k_p3d_bwd_x": "p3d_bwd_x", "k_p3d_bwd_w": "p3d_bwd_w", "k_adam": "adam",
+         "k_gn_fwd_stats": "gn_fwd_stats", "k_gn_fwd_apply": "gn_fwd_apply", "k_gn_bwd_stats": "gn_bwd_stats",
+         "k_gn_bwd_apply": "gn_bwd_apply", "k_bias_act_fwd": "bias_act_fwd", "k_bias_act_bwd": "bias_act_bwd",
+         "k_cols_finish": "cols_finish", "k_upcat_fwd": "upcat_fwd", "k_upcat_bwd": "upcat_bwd"}
 
 
 def label(kernel):
@@ -57,7 +62,9 @@ def main():
         wr = 1024 * k["WRITE_SIZE"] if "WRITE_SIZE" in k else None
         k["read_bytes"], k["write_bytes"] = rd, wr
         k["hbm_bytes"] = (rd + wr) if rd is not None and wr is not None else None
-    res = {"config_key": key,
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    res = {"config_key": key, "source_hash": bench.source_hash(),
            "source": "rocprofv3 --pmc over bench.py (one pass per counter group, tools/gpu_pmc_bench.sh)",
            "correction": "read = 2*1024*FETCH_SIZE (gfx950 half-count of wide reads), write = 1024*WRITE_SIZE",
            "kernels": kernels}
