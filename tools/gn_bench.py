@@ -25,6 +25,8 @@ ap.add_argument("--height", type=int, default=192)
 ap.add_argument("--width", type=int, default=640)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--lib", default=None)
+ap.add_argument("--net", default="depth", choices=["depth", "pose"], help="record the depth or the pose net's GN calls")
+ap.add_argument("--eager", action="store_true", help="time eager calls (default: HIP-graph replays of --iters calls)")
 args = ap.parse_args()
 import __graft_entry__  # noqa: E402
 
@@ -63,22 +65,34 @@ for mod in list(sys.modules.values()):
 FU.gn_act = rec
 b = bench.synthetic_batch(1, args.height, args.width, torch.device("cpu"), seed=0)
 with torch.no_grad():
-    model.depth_net(b["rgb"])
+    if args.net == "depth":
+        model.depth_net(b["rgb"])
+    else:
+        model.pose_net(b["rgb"], b["rgb_context"])
 print(f"{sum(calls.values())} gn_act calls, {len(calls)} shapes", flush=True)
 
 
 def timed(fn):
-    """HIP events around args.iters back-to-back eager calls (the launches queue ahead of the GPU
-    for the large shapes; small shapes are an upper bound — rocprofv3 kernel stats give the kernel
-    time alone)."""
+    """Per-call GPU time: a HIP graph of args.iters calls replayed between two HIP events (no host
+    launch gaps; --eager: back-to-back eager calls, an upper bound for small shapes)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.iters):
-        fn()
-    e1.record()
+    if args.eager:
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+    else:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(args.iters):
+                fn()
+        g.replay()
+        e0.record()
+        g.replay()
+        e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1e3 / args.iters
 
