@@ -20,9 +20,6 @@
  * needs in a fixed order (fp64) — the GroupNorm apply pass its sample's group rows in its
  * prologue, a small column-total kernel the parameter gradients.  The kernel boundary orders
  * the partial rows before their readers, so no device-scope arrival rounds are needed.
- * BatchNorm (bn_act, off by default: MIOpen's BN is faster on these nets) still reduces in
- * one launch with arrival counts in `counter`, an int array of PSFM_NETOPS_COUNTER_INTS
- * zeroed once by the caller and re-armed by the kernels.
  *
  * Conventions as include/psfm.h: device pointers, caller-owned buffers, stream-ordered,
  * graph-capturable; return 0 / <0 bad argument / >0 hipError_t, message from
@@ -37,8 +34,6 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-
-#define PSFM_NETOPS_COUNTER_INTS 256
 
 #define PSFM_ACT_NONE 0
 #define PSFM_ACT_RELU 1
@@ -62,17 +57,18 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
                       int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
+ * three launches each way (statistics rows, per-channel finish, apply),
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
  * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
-                    float* save_invstd, float* ws, int* counter, void* stream);
+                    float* save_invstd, float* ws, void* stream);
 
 /* Backward of psfm_bn_act_fwd: dx (bf16), dres (bf16, = ReLU-masked dy; may be NULL),
  * dgamma / dbeta (fp32 [C], written). */
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
-                    float* dbeta, float* ws, int* counter, void* stream);
+                    float* dbeta, float* ws, void* stream);
 
 /* y = act(GroupNorm(G)(x [+ res] + bias)) per sample (two launches: statistics rows, then apply with
  * the per-sample reduction in its prologue): x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]

@@ -110,8 +110,8 @@ def lib():
         "psfm_gn_ws_floats": ([c_int, c_int, c_int, c_int], c_size_t),
         "psfm_bias_act_fwd": ([V, V, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_bias_act_bwd": ([V, V, c_int, c_int, c_int, V, V, c_int, V, V], c_int),
-        "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
-        "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V, V], c_int),
+        "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V], c_int),
+        "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
         "psfm_gn_act_fwd": ([V, V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V],
                             c_int),
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,

@@ -6,14 +6,12 @@
 // row lane t / G (G = C/VEC; VEC = 8: one 16-byte load per thread, fully coalesced rows) and
 // walks its workgroup's row range in steps of U*TR rows with U independent loads in flight.
 //
-// Column reductions (batch statistics, bias gradients) are deterministic and single-launch:
-//   per-thread fp32 sums -> LDS tree over the row lanes -> one partial row per workgroup
-//   -> the last workgroup of each group of GS workgroups sums its group's rows (fp64)
-//   -> the last group sums the group rows (fp64) and finalises the per-channel results.
-// Arrival order is counted on device-scope int counters (re-armed by the last arrival, so
-// graph replays reuse them).  Partials are written with device-coherent (sc1) stores and read
-// back with coherent vector loads, all of a row block in flight at once — the tail is two
-// short dependent rounds, not a serial sweep over hundreds of partials.  No float atomics.
+// Column reductions (batch statistics, bias / affine gradients) are deterministic and need no
+// device-scope synchronisation: each workgroup writes its partial row (fp32 column sums of its
+// rows, LDS tree over its row lanes), and the NEXT launch sums the rows in a fixed order in fp64
+// (a small finish kernel, or — GroupNorm — the apply pass's prologue).  The kernel boundary is
+// the barrier: at these sizes it is cheaper than arrival counters through the non-coherent
+// per-XCD L2s (two device-scope rounds of 3-5 us each).  No float atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -41,7 +39,6 @@ int fail(int code, const char* msg) {
 constexpr int NT = 256;           // threads per workgroup
 constexpr int U = 4;              // row steps unrolled (independent loads in flight per thread)
 constexpr int TARGET_BLOCKS = 512;
-constexpr int GS = 16;     // workgroups per reduction group (ngroups)
 constexpr int MAX_KC = 1024;      // widest partial row (BN: 2*C, C <= 512)
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
@@ -159,14 +156,7 @@ inline Geo geometry(int M, int C, int vec, int target = TARGET_BLOCKS) {
     return g;
 }
 inline int pick_vec(int C) { return (C % 8 == 0 && C / 8 <= NT) ? 8 : 1; }
-__host__ __device__ inline int ngroups(int nblk) { return (nblk + GS - 1) / GS; }
-// floats of reduction workspace for nseg segments of nblk workgroups with KC-wide rows:
-// block rows [nseg*nblk][KC] fp32, then group rows [nseg*ngroups][KC] fp64.
 __host__ __device__ inline size_t align4(size_t n) { return (n + 3) / 4 * 4; }  // 16-byte alignment
-__host__ __device__ inline size_t tree_grp_off(int nseg, int nblk, int KC) { return align4((size_t)nseg * nblk * KC); }
-__host__ __device__ inline size_t tree_ws_floats(int nseg, int nblk, int KC) {
-    return tree_grp_off(nseg, nblk, KC) + 2 * (size_t)nseg * ngroups(nblk) * KC;
-}
 
 // Block column reduction of K per-thread vectors; afterwards row lane 0 holds the block sums.
 // red: LDS [K * NT * VEC] floats (TR * G <= NT).
@@ -197,132 +187,6 @@ __device__ __forceinline__ void block_colsum(float (&acc)[K][VEC], float* red, i
         for (int k = 0; k < K; ++k)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) acc[k][i] = red[(k * TR * G + cg) * VEC + i];
-    }
-}
-
-// ---- device-coherent partial traffic -------------------------------------------------------
-// The L2 of an XCD is not coherent with the others.  Partials are stored with agent-scope
-// relaxed atomic stores (global_store ... sc1) and read back with sc1 loads, so no cache-wide
-// writeback / invalidate fence is needed; completion is awaited (s_waitcnt) before the
-// arrival counter increment, which is a device-scope RMW.
-__device__ __forceinline__ void st_part(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_part(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_part(const float* p) {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_part(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr int CPOL_SC1 = 16;             // gfx94x/gfx950 cache policy: agent-scope coherent
-constexpr int RSRC_WORD3 = 0x00020000;   // raw buffer resource, gfx9 data format
-
-// coherent 16-byte load of base[off_bytes/4 ..] (buffer_load_dwordx4 ... sc1; the resource is
-// wave-uniform, set up once in SGPRs)
-__device__ __forceinline__ float4 ld4_part(const float* base, int nbytes, int off_bytes) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nbytes, RSRC_WORD3);
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off_bytes, 0, CPOL_SC1));
-}
-
-// true (in every thread) only in the last of n workgroups to arrive on *ctr; re-arms *ctr.
-__device__ __forceinline__ bool arrive(int* ctr, int n) {
-    __shared__ int is_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (prev == n - 1);
-        if (is_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    return is_last;
-}
-
-// fin[c] = sum over rows r in [0, nrows) of src[r*KC + c] in fixed row order (fp64), valid in
-// every thread on return.  All NT threads take part: thread = (row lane, column vector); each
-// issues all its (<= 32) loads before summing.  scratch: LDS [NT * 4] doubles.
-template <typename T>
-__device__ void sum_rows(const T* src, int nrows, int KC, double* fin, double* scratch) {
-    const int t = threadIdx.x;
-    constexpr bool F4 = sizeof(T) == 4;
-    const int W = (F4 && KC % 4 == 0) ? 4 : 1;
-    const int QW = KC / W;
-    const int LN = QW >= NT ? 1 : NT / QW;
-    const int l = t / QW, q = t % QW;
-    for (int qq = (QW >= NT ? t : q); qq < QW && l < LN; qq += (QW >= NT ? NT : QW)) {
-        double s[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int r0 = (QW >= NT ? 0 : l); r0 < nrows; r0 += 8 * LN) {
-            if (W == 4) {
-                float4 v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int rr = r0 + u * LN;
-                    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if constexpr (F4)
-                        if (rr < nrows) v[u] = ld4_part(src, nrows * KC * 4, (rr * KC + qq * 4) * 4);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    s[0] += (double)v[u].x;
-                    s[1] += (double)v[u].y;
-                    s[2] += (double)v[u].z;
-                    s[3] += (double)v[u].w;
-                }
-            } else {
-                T v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int rr = r0 + u * LN;
-                    v[u] = rr < nrows ? ld_part(src + (size_t)rr * KC + qq) : (T)0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) s[0] += (double)v[u];
-            }
-        }
-        if (QW >= NT) {  // one lane: the thread's sums are final
-            for (int i = 0; i < W; ++i) fin[qq * W + i] = s[i];
-        } else {
-            for (int i = 0; i < W; ++i) scratch[(l * QW + qq) * W + i] = s[i];
-        }
-    }
-    __syncthreads();
-    if (QW < NT) {
-        for (int c = t; c < KC; c += NT) {  // lanes combined in lane order
-            double a = 0.0;
-            for (int ll = 0; ll < LN; ++ll) a += scratch[ll * KC + c];
-            fin[c] = a;
-        }
-        __syncthreads();
-    }
-}
-
-// Two-level deterministic reduction of one segment's block rows.  rows: [nblk][KC] fp32
-// (this workgroup's row already stored), grp: [ngroups][KC] fp64, ctr: 1 + ngroups ints.
-// Returns true in the single workgroup that finishes the segment; fin = column totals.
-__device__ bool tree_reduce(float* rows, double* grp, int* ctr, int b, int nblk, int KC, double* fin,
-                            double* scratch) {
-    const int g = b / GS, ng = ngroups(nblk);
-    const int n_in = min(GS, nblk - g * GS);
-    if (!arrive(ctr + 1 + g, n_in)) return false;
-    sum_rows<float>(rows + (size_t)g * GS * KC, n_in, KC, fin, scratch);
-    if (ng == 1) return true;
-    for (int c = threadIdx.x; c < KC; c += NT) st_part(grp + (size_t)g * KC + c, fin[c]);
-    if (!arrive(ctr, ng)) return false;
-    sum_rows<double>(grp, ng, KC, fin, scratch);
-    return true;
-}
-
-// this workgroup's K x VEC column sums (row lane 0 threads) -> its partial row
-template <int VEC, int K>
-__device__ __forceinline__ void store_row(float* row, const float (&acc)[K][VEC], int C, int c0, int r) {
-    if (r == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) st_part(row + k * C + c0 + i, acc[k][i]);
     }
 }
 
@@ -509,23 +373,58 @@ struct BNArgs {
     uint16_t* dres;  // bwd
     float* dgamma;
     float* dbeta;
-    float* ws;       // reduction tree, then [3][C] coefficients
-    int* counter;
+    float* ws;       // partial rows [nblk][2C], then [3][C] coefficients
     float momentum, eps;
     int M, C, relu, G, TR, rpb, nblk;
 };
 
-__device__ __forceinline__ float* bn_coef(const BNArgs& a) {
-    return a.ws + tree_ws_floats(1, a.nblk, 2 * a.C);
+__host__ __device__ inline size_t bn_coef_off(int nblk, int C) { return align4((size_t)nblk * 2 * C); }
+__device__ __forceinline__ float* bn_coef(const BNArgs& a) { return a.ws + bn_coef_off(a.nblk, a.C); }
+
+// Column totals for the finish kernels: thread = (column c = 4 * blockIdx.x + t % 4, lane t / 4 of
+// 64); tot[k] = sum over rows of rows[r * stride + off[k] + c] (fp64: each lane its rows in order,
+// then a fixed tree over the lanes), valid in every thread of the column on return.
+template <int K>
+__device__ __forceinline__ void cols4_totals(const float* rows, int nrows, int stride, const int (&off)[K], int c,
+                                             bool valid, double (&tot)[K]) {
+    __shared__ double part[K][256];
+    const int t = threadIdx.x, cl = t & 3, lane = t >> 2;
+    double s[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[k] = 0.0;
+    if (valid) {
+        for (int r0 = lane; r0 < nrows; r0 += 4 * 64) {
+            float v[4][K];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int rr = r0 + u * 64;
+                    v[u][k] = rr < nrows ? rows[(size_t)rr * stride + off[k] + c] : 0.0f;
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) s[k] += (double)v[u][k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) part[k][t] = s[k];
+    __syncthreads();
+    for (int h = 32; h >= 1; h >>= 1) {
+        if (lane < h)
+#pragma unroll
+            for (int k = 0; k < K; ++k) part[k][t] += part[k][t + 4 * h];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) tot[k] = part[k][cl];
 }
 
-// pass 1: per-channel sum / sum of squares; the finishing workgroup -> mean, invstd, running
-// stats and the affine coefficients scale = gamma*invstd, shift = beta - mean*scale.
+// pass 1: per-channel sum / sum of squares of this workgroup's rows -> its partial row
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bn_fwd_stats(BNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[2][VEC];
@@ -550,27 +449,40 @@ __global__ __launch_bounds__(NT) void k_bn_fwd_stats(BNArgs a) {
         ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    const int KC = 2 * a.C;
-    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * KC, acc, a.C, c0, r);
-    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, KC));
-    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, KC, fin, scratch)) return;
+    if (r == 0) {   // this workgroup's partial row; k_bn_fwd_finish reduces the rows (next launch)
+        float* row = a.ws + (size_t)blockIdx.x * 2 * a.C;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            row[c0 + i] = acc[0][i];
+            row[a.C + c0 + i] = acc[1][i];
+        }
+    }
+}
+
+// pass 1b: per channel (4 channels x 64 lanes per workgroup) the column totals of the partial rows
+// -> mean, invstd, running stats and the affine coefficients scale = gamma*invstd,
+// shift = beta - mean*scale
+__global__ __launch_bounds__(256) void k_bn_fwd_finish(BNArgs a) {
+    const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+    const int off[2] = {0, a.C};
+    double fin[2];
+    cols4_totals<2>(a.ws, a.nblk, 2 * a.C, off, c, c < a.C, fin);
+    if (threadIdx.x >= 4 || c >= a.C) return;
     float* coef = bn_coef(a);  // [2][C]: scale, shift
     const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += NT) {
-        const double mean = fin[c] * inv_m;
-        const double var = fmax(fin[a.C + c] * inv_m - mean * mean, 0.0);
-        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        a.save_mean[c] = (float)mean;
-        a.save_invstd[c] = invstd;
-        if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
-            const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-            a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
-            a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-        }
-        const float scale = a.gamma[c] * invstd;
-        coef[c] = scale;
-        coef[a.C + c] = a.beta[c] - (float)mean * scale;
+    const double mean = fin[0] * inv_m;
+    const double var = fmax(fin[1] * inv_m - mean * mean, 0.0);
+    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+    a.save_mean[c] = (float)mean;
+    a.save_invstd[c] = invstd;
+    if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
+        const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
+        a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
+        a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
     }
+    const float scale = a.gamma[c] * invstd;
+    coef[c] = scale;
+    coef[a.C + c] = a.beta[c] - (float)mean * scale;
 }
 
 // pass 2: y = act(x*scale + shift [+ res])
@@ -608,13 +520,10 @@ __global__ __launch_bounds__(NT) void k_bn_fwd_apply(BNArgs a) {
     ROW_LOOP_END
 }
 
-// backward pass 1: per channel sum(dyr), sum(dyr * (x - mean)); finishing workgroup -> dgamma,
-// dbeta and dx coefficients k1 = gamma*invstd, k2 = sum(dyr)/M, k3 = sum(dyr*xc)*invstd^2/M.
+// backward pass 1: per channel sum(dyr), sum(dyr * (x - mean)) of this workgroup's rows
 template <int VEC>
 __global__ __launch_bounds__(NT) void k_bn_bwd_stats(BNArgs a) {
     __shared__ float red[2 * NT * VEC];
-    __shared__ double fin[MAX_KC];
-    __shared__ double scratch[NT * 4];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * VEC;
     float acc[2][VEC];
@@ -645,20 +554,32 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_stats(BNArgs a) {
         ROW_LOOP_END
     }
     block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    const int KC = 2 * a.C;
-    store_row<VEC, 2>(a.ws + (size_t)blockIdx.x * KC, acc, a.C, c0, r);
-    double* grp = reinterpret_cast<double*>(a.ws + tree_grp_off(1, a.nblk, KC));
-    if (!tree_reduce(a.ws, grp, a.counter, blockIdx.x, a.nblk, KC, fin, scratch)) return;
+    if (r == 0) {
+        float* row = a.ws + (size_t)blockIdx.x * 2 * a.C;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            row[c0 + i] = acc[0][i];
+            row[a.C + c0 + i] = acc[1][i];
+        }
+    }
+}
+
+// backward pass 1b: column totals -> dgamma, dbeta and the dx coefficients k1 = gamma*invstd,
+// k2 = sum(dyr)/M, k3 = sum(dyr*xc)*invstd^2/M
+__global__ __launch_bounds__(256) void k_bn_bwd_finish(BNArgs a) {
+    const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+    const int off[2] = {0, a.C};
+    double fin[2];
+    cols4_totals<2>(a.ws, a.nblk, 2 * a.C, off, c, c < a.C, fin);
+    if (threadIdx.x >= 4 || c >= a.C) return;
     float* coef = bn_coef(a);  // [3][C]
     const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += NT) {
-        const double is = a.save_invstd[c];
-        a.dbeta[c] = (float)fin[c];
-        a.dgamma[c] = (float)(fin[a.C + c] * is);
-        coef[c] = a.gamma[c] * (float)is;
-        coef[a.C + c] = (float)(fin[c] * inv_m);
-        coef[2 * a.C + c] = (float)(fin[a.C + c] * is * is * inv_m);
-    }
+    const double is = a.save_invstd[c];
+    a.dbeta[c] = (float)fin[0];
+    a.dgamma[c] = (float)(fin[1] * is);
+    coef[c] = a.gamma[c] * (float)is;
+    coef[a.C + c] = (float)(fin[0] * inv_m);
+    coef[2 * a.C + c] = (float)(fin[1] * is * is * inv_m);
 }
 
 // backward pass 2: dx = k1 * (dyr - k2 - (x - mean) * k3); dres = dyr
@@ -1229,9 +1150,9 @@ int psfm_upcat_bwd(const void* dout, int N, int h, int w, int C1, int C2, void* 
     return 0;
 }
 
-size_t psfm_netops_ws_floats(int M, int C) {
+size_t psfm_netops_ws_floats(int M, int C) {   // partial rows [nblk][2C] + coefficients [3][C]
     const Geo g = geometry(M, C, pick_vec(C));
-    return tree_ws_floats(1, g.nblk, 2 * C) + 3 * (size_t)C;
+    return bn_coef_off(g.nblk, C) + 3 * (size_t)C;
 }
 
 size_t psfm_gn_ws_floats(int N, int HW, int C, int G) {
@@ -1283,8 +1204,8 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
 
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
-                    float* save_invstd, float* ws, int* counter, void* stream) {
-    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || !counter || M < 1 || C < 1)
+                    float* save_invstd, float* ws, void* stream) {
+    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || M < 1 || C < 1)
         return fail(-1, "bn_act_fwd: bad arguments");
     if ((run_mean == nullptr) != (run_var == nullptr)) return fail(-1, "bn_act_fwd: running stats must pair");
     if (int e = check_vec(C, "bn_act_fwd")) return e;
@@ -1296,15 +1217,18 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
     a.save_mean = save_mean, a.save_invstd = save_invstd;
     a.out = static_cast<uint16_t*>(y);
-    a.ws = ws, a.counter = counter, a.momentum = momentum, a.eps = eps;
+    a.ws = ws, a.momentum = momentum, a.eps = eps;
     a.M = M, a.C = C, a.relu = relu, a.nblk = g.nblk;
     set_geo(a, g);
     hipStream_t st = (hipStream_t)stream;
+    const dim3 fin((C + 3) / 4);
     if (vec == 8) {
         hipLaunchKernelGGL(k_bn_fwd_stats<8>, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bn_fwd_finish, fin, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_bn_fwd_apply<8>, dim3(g.nblk), dim3(NT), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_bn_fwd_stats<1>, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bn_fwd_finish, fin, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_bn_fwd_apply<1>, dim3(g.nblk), dim3(NT), 0, st, a);
     }
     NETOPS_LAUNCH_CHECK();
@@ -1313,8 +1237,8 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
 
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
-                    float* dbeta, float* ws, int* counter, void* stream) {
-    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws || !counter ||
+                    float* dbeta, float* ws, void* stream) {
+    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws ||
         M < 1 || C < 1 || (relu && !y))
         return fail(-1, "bn_act_bwd: bad arguments");
     if (int e = check_vec(C, "bn_act_bwd")) return e;
@@ -1327,15 +1251,18 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
     a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
     a.out = static_cast<uint16_t*>(dx);
     a.dres = static_cast<uint16_t*>(dres);
-    a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws, a.counter = counter;
+    a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws;
     a.M = M, a.C = C, a.relu = relu, a.nblk = g.nblk;
     set_geo(a, g);
     hipStream_t st = (hipStream_t)stream;
+    const dim3 fin((C + 3) / 4);
     if (vec == 8) {
         hipLaunchKernelGGL(k_bn_bwd_stats<8>, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bn_bwd_finish, fin, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_bn_bwd_apply<8>, dim3(g.nblk), dim3(NT), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_bn_bwd_stats<1>, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bn_bwd_finish, fin, dim3(256), 0, st, a);
         hipLaunchKernelGGL(k_bn_bwd_apply<1>, dim3(g.nblk), dim3(NT), 0, st, a);
     }
     NETOPS_LAUNCH_CHECK();

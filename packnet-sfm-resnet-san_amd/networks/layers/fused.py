@@ -38,25 +38,6 @@ def _rows(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
-SLOT = 256  # PSFM_NETOPS_COUNTER_INTS (include/psfm_netops.h)
-FWD, BWD = 0, 1  # counter slots of the (opt-in) fused BatchNorm: forward | backward kernels
-
-
-def _counter(module, device):
-    """Arrival counters of the fused BatchNorm's single-launch reductions: zeroed once here and
-    re-armed by the kernels after every launch (graph replays reuse them).  GroupNorm and the
-    bias epilogues need none (partial rows + a next-launch reduction)."""
-    c = getattr(module, "_psfm_counter", None)
-    if c is None or c.device != device:
-        c = torch.zeros(3 * SLOT, dtype=torch.int32, device=device)
-        module._psfm_counter = c
-    return c
-
-
-def _slot(t, i):
-    return ctypes.c_void_p(t.data_ptr() + 4 * SLOT * i)
-
-
 # ----------------------------------------------------------------------------------------------
 class _BiasAct(torch.autograd.Function):
     @staticmethod
@@ -111,7 +92,7 @@ def conv_nobias(conv, x):
 # ----------------------------------------------------------------------------------------------
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, counter):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu):
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -125,10 +106,9 @@ class _BNAct(torch.autograd.Function):
         _hip.check(L.psfm_bn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(weight), _hip.ptr(bias),
                                      _hip.ptr(running_mean), _hip.ptr(running_var), ctypes.c_float(momentum),
                                      ctypes.c_float(eps), M, C, int(relu), _hip.ptr(y), _hip.ptr(mean),
-                                     _hip.ptr(invstd), _hip.ptr(ws), _slot(counter, FWD), _hip.stream(dev)),
-                   "psfm_bn_act_fwd")
+                                     _hip.ptr(invstd), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_fwd")
         ctx.save_for_backward(x, y, weight, mean, invstd)
-        ctx.relu, ctx.has_res, ctx.counter = relu, residual is not None, counter
+        ctx.relu, ctx.has_res = relu, residual is not None
         return y
 
     @staticmethod
@@ -146,9 +126,8 @@ class _BNAct(torch.autograd.Function):
         ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
         _hip.check(L.psfm_bn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(mean),
                                      _hip.ptr(invstd), M, C, int(ctx.relu), _hip.ptr(dx), _hip.ptr(dres),
-                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _slot(ctx.counter, BWD),
-                                     _hip.stream(dev)), "psfm_bn_act_bwd")
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None, None
+                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_bwd")
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None
 
 
 def bn_act(x, bn, relu=True, residual=None):
@@ -158,7 +137,7 @@ def bn_act(x, bn, relu=True, residual=None):
         if bn.num_batches_tracked is not None:  # the graph trainer keeps these off the step
             bn.num_batches_tracked.add_(1)
         return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, float(bn.momentum),
-                            float(bn.eps), bool(relu), _counter(bn, x.device))
+                            float(bn.eps), bool(relu))
     y = bn(x)
     if residual is not None:
         y = y + residual

@@ -166,8 +166,8 @@ def test_gn_act_matches_torch(dev, shape):
 
 @gpu
 def test_fused_reductions_are_deterministic_and_rearm(dev):
-    """Repeated launches reuse the device counters (re-armed by the last workgroup): results
-    stay bit-identical run to run."""
+    """Repeated fused BatchNorm launches (statistics rows -> per-channel finish -> apply): results
+    stay bit-identical run to run (fixed-order reductions, no atomics)."""
     g = torch.Generator(device="cpu").manual_seed(4)
     bn = nn.BatchNorm2d(64).to(dev).train()
     x = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
