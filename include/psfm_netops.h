@@ -105,6 +105,21 @@ int psfm_upcat_fwd(const void* x, const void* skip, int N, int h, int w, int C1,
  * dskip = dout[..., C1:] (NULL when C2 = 0). */
 int psfm_upcat_bwd(const void* dout, int N, int h, int w, int C1, int C2, void* dx, void* dskip, void* stream);
 
+/* The up-stage input with the stage's first ConvBlock folded in (layers.py:25-41 Conv3x3 + ReLU,
+ * depth_decoder.py:48-57): out = cat([nearest_up2(relu(x + bias)), skip], channels), x = that
+ * block's convolution WITHOUT its bias (bf16 NHWC [N, h, w, C1]), bias bf16 (bias_bf16 = 1) or fp32
+ * [C1].  The block's output is never materialised on its own.  C1 / 8 must divide 256. */
+int psfm_upcat_bias_relu_fwd(const void* x, const void* bias, int bias_bf16, const void* skip, int N, int h, int w,
+                             int C1, int C2, void* out, void* stream);
+
+/* Its backward: dx = (relu'(.) read from `out`, the forward output) * the 2x2 block sums of
+ * dout[..., :C1] (fp32, one bf16 rounding), dskip = dout[..., C1:], dbias = the column sums of the
+ * stored dx (bias dtype) — two launches (dx + partial rows, column totals); ws floats:
+ * psfm_upcat_ws_floats(N, h, w, C1). */
+int psfm_upcat_bias_relu_bwd(const void* dout, const void* out, int N, int h, int w, int C1, int C2, void* dx,
+                             void* dskip, void* dbias, int bias_bf16, float* ws, void* stream);
+size_t psfm_upcat_ws_floats(int N, int h, int w, int C1);
+
 #ifdef __cplusplus
 }
 #endif

@@ -119,6 +119,9 @@ def lib():
         "psfm_netops_last_error": ([], ctypes.c_char_p),
         "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_upcat_bwd": ([V, c_int, c_int, c_int, c_int, c_int, V, V, V], c_int),
+        "psfm_upcat_bias_relu_fwd": ([V, V, c_int, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
+        "psfm_upcat_bias_relu_bwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, c_int, V, V], c_int),
+        "psfm_upcat_ws_floats": ([c_int, c_int, c_int, c_int], c_size_t),
         # include/psfm_pack3d.h
         "psfm_p3d_fwd": ([V, V, V, V, V, V], c_int),
         "psfm_p3d_ws_floats": ([V], ctypes.c_int64),
@@ -153,7 +156,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
-            "psfm_upcat_fwd", "psfm_upcat_bwd",
+            "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",
+            "psfm_upcat_ws_floats",
             "psfm_depth_metrics", "psfm_metrics_last_error",
             "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
             "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error",

@@ -1054,10 +1054,33 @@ struct UpcatArgs {
     const uint4* dout;
     uint4* dx;
     uint4* dskip;
+    const void* bias;   // RELU variant: conv bias [C1] (bf16 / fp32)
+    float* rows;        // RELU backward: per-workgroup partial rows of the bias gradient [nbx][C1]
     int N, h, w, V1, V2;  // V = channels / 8
-    uint32_t nfwd, ndx, ndskip;
+    int bias_bf16;
+    uint32_t nfwd, ndx, ndskip, nbx;  // nbx: workgroups of the dx part (the dskip part follows)
 };
 
+__device__ __forceinline__ uint4 pack8(const float (&v)[8]) {
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    return o;
+}
+__device__ __forceinline__ void unpack8(uint4 q, float (&v)[8]) {
+    const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[2 * k] = __uint_as_float(u[k] << 16);
+        v[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+    }
+}
+
+// RELU = true: the x part is relu(x + bias) of the up-stage's first ConvBlock (layers.py:25-41:
+// Conv3x3 + ReLU), computed on the fly — the block's output is never written on its own.
+template <bool RELU>
 __global__ __launch_bounds__(256) void k_upcat_fwd(UpcatArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= a.nfwd) return;
@@ -1065,10 +1088,21 @@ __global__ __launch_bounds__(256) void k_upcat_fwd(UpcatArgs a) {
     const uint32_t pix = i / Vt, v = i - pix * Vt;   // output pixel (n, Y, X), vector in the row
     const uint32_t W2 = 2u * (uint32_t)a.w, H2 = 2u * (uint32_t)a.h;
     const uint32_t X = pix % W2, nY = pix / W2, Y = nY % H2, n = nY / H2;
-    if (v < (uint32_t)a.V1)
-        a.out[i] = a.x[(((size_t)n * a.h + (Y >> 1)) * a.w + (X >> 1)) * a.V1 + v];
-    else
+    if (v < (uint32_t)a.V1) {
+        const uint4 q = a.x[(((size_t)n * a.h + (Y >> 1)) * a.w + (X >> 1)) * a.V1 + v];
+        if constexpr (RELU) {
+            float f[8];
+            unpack8(q, f);
+            const Vec<8> b = ld_param<8>(a.bias, a.bias_bf16, (int)v * 8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k] + b.v[k], 0.0f);
+            a.out[i] = pack8(f);
+        } else {
+            a.out[i] = q;
+        }
+    } else {
         a.out[i] = a.skip[(size_t)pix * a.V2 + (v - a.V1)];
+    }
 }
 
 __device__ __forceinline__ void add8(float (&acc)[8], uint4 q) {
@@ -1080,31 +1114,53 @@ __device__ __forceinline__ void add8(float (&acc)[8], uint4 q) {
     }
 }
 
-// threads [0, ndx): one 8-channel vector of dx (sum of its 2x2 block, rows then columns, fp32,
-// one bf16 rounding); threads [ndx, ndx + ndskip): one vector of dskip (copy)
+// workgroups [0, nbx): one 8-channel vector of dx per thread (sum of its 2x2 block, rows then
+// columns, fp32, one bf16 rounding; RELU: masked where the block's output relu(x + bias) — read
+// back from the forward output — is 0, and the workgroup's column sums of the stored dx written as
+// its partial bias-gradient row); workgroups [nbx, ..): one vector of dskip per thread (copy)
+template <bool RELU>
 __global__ __launch_bounds__(256) void k_upcat_bwd(UpcatArgs a) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     const uint32_t Vt = (uint32_t)(a.V1 + a.V2);
-    if (i < a.ndx) {
-        const uint32_t pix = i / (uint32_t)a.V1, v = i - pix * (uint32_t)a.V1;  // input pixel (n, y, x)
-        const uint32_t x = pix % (uint32_t)a.w, ny = pix / (uint32_t)a.w;
-        const uint32_t y = ny % (uint32_t)a.h, n = ny / (uint32_t)a.h;
-        const uint32_t W2 = 2u * (uint32_t)a.w;
-        const size_t r0 = ((size_t)n * 2u * a.h + 2u * y) * W2 + 2u * x;  // top-left output pixel
+    if (blockIdx.x < a.nbx) {
+        const uint32_t i = blockIdx.x * 256u + threadIdx.x;
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        add8(acc, a.dout[r0 * Vt + v]);
-        add8(acc, a.dout[(r0 + 1) * Vt + v]);
-        add8(acc, a.dout[(r0 + W2) * Vt + v]);
-        add8(acc, a.dout[(r0 + W2 + 1) * Vt + v]);
-        uint4 o;
-        o.x = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
-        o.y = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
-        o.z = (uint32_t)f2bf(acc[4]) | ((uint32_t)f2bf(acc[5]) << 16);
-        o.w = (uint32_t)f2bf(acc[6]) | ((uint32_t)f2bf(acc[7]) << 16);
-        a.dx[i] = o;
+        if (i < a.ndx) {
+            const uint32_t pix = i / (uint32_t)a.V1, v = i - pix * (uint32_t)a.V1;  // input pixel (n, y, x)
+            const uint32_t x = pix % (uint32_t)a.w, ny = pix / (uint32_t)a.w;
+            const uint32_t y = ny % (uint32_t)a.h, n = ny / (uint32_t)a.h;
+            const uint32_t W2 = 2u * (uint32_t)a.w;
+            const size_t r0 = ((size_t)n * 2u * a.h + 2u * y) * W2 + 2u * x;  // top-left output pixel
+            add8(acc, a.dout[r0 * Vt + v]);
+            add8(acc, a.dout[(r0 + 1) * Vt + v]);
+            add8(acc, a.dout[(r0 + W2) * Vt + v]);
+            add8(acc, a.dout[(r0 + W2 + 1) * Vt + v]);
+            if constexpr (RELU) {
+                float y0[8];
+                unpack8(a.out[r0 * Vt + v], y0);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] = y0[k] > 0.0f ? bfround(acc[k]) : 0.0f;
+            }
+            a.dx[i] = pack8(acc);
+        }
+        if constexpr (RELU) {   // partial row: pixels of this workgroup summed per channel (fixed tree)
+            __shared__ float red[256][8];
+            const int t = threadIdx.x, V1 = a.V1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) red[t][k] = acc[k];
+            __syncthreads();
+            for (int st = (256 / V1) / 2; st >= 1; st >>= 1) {
+                if (t / V1 < st)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) red[t][k] += red[t + st * V1][k];
+                __syncthreads();
+            }
+            if (t < V1)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) a.rows[(size_t)blockIdx.x * V1 * 8 + t * 8 + k] = red[t][k];
+        }
         return;
     }
-    const uint32_t j = i - a.ndx;
+    const uint32_t j = (blockIdx.x - a.nbx) * 256u + threadIdx.x;
     if (j >= a.ndskip) return;
     const uint32_t pix = j / (uint32_t)a.V2, v = j - pix * (uint32_t)a.V2;
     a.dskip[j] = a.dout[(size_t)pix * Vt + a.V1 + v];
@@ -1120,16 +1176,24 @@ static int upcat_check(int N, int h, int w, int C1, int C2, const char* who) {
     return 0;
 }
 
+static UpcatArgs upcat_args(int N, int h, int w, int C1, int C2) {
+    UpcatArgs a{};
+    a.N = N, a.h = h, a.w = w, a.V1 = C1 / 8, a.V2 = C2 / 8;
+    a.nfwd = (uint32_t)((size_t)N * 4 * h * w * (a.V1 + a.V2));
+    a.ndx = (uint32_t)((size_t)N * h * w * a.V1);
+    a.ndskip = (uint32_t)((size_t)N * 4 * h * w * a.V2);
+    a.nbx = (a.ndx + 255) / 256;
+    return a;
+}
+
 int psfm_upcat_fwd(const void* x, const void* skip, int N, int h, int w, int C1, int C2, void* out, void* stream) {
     if (int e = upcat_check(N, h, w, C1, C2, "upcat_fwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)")) return e;
     if (!x || !out || (C2 > 0 && !skip)) return fail(-1, "upcat_fwd: null pointer");
-    UpcatArgs a{};
+    UpcatArgs a = upcat_args(N, h, w, C1, C2);
     a.x = static_cast<const uint4*>(x);
     a.skip = static_cast<const uint4*>(skip);
     a.out = static_cast<uint4*>(out);
-    a.N = N, a.h = h, a.w = w, a.V1 = C1 / 8, a.V2 = C2 / 8;
-    a.nfwd = (uint32_t)((size_t)N * 4 * h * w * (a.V1 + a.V2));
-    hipLaunchKernelGGL(k_upcat_fwd, dim3((a.nfwd + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_upcat_fwd<false>, dim3((a.nfwd + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
     NETOPS_LAUNCH_CHECK();
     return 0;
 }
@@ -1137,16 +1201,59 @@ int psfm_upcat_fwd(const void* x, const void* skip, int N, int h, int w, int C1,
 int psfm_upcat_bwd(const void* dout, int N, int h, int w, int C1, int C2, void* dx, void* dskip, void* stream) {
     if (int e = upcat_check(N, h, w, C1, C2, "upcat_bwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)")) return e;
     if (!dout || !dx || (C2 > 0 && !dskip)) return fail(-1, "upcat_bwd: null pointer");
-    UpcatArgs a{};
+    UpcatArgs a = upcat_args(N, h, w, C1, C2);
     a.dout = static_cast<const uint4*>(dout);
     a.dx = static_cast<uint4*>(dx);
     a.dskip = static_cast<uint4*>(dskip);
-    a.N = N, a.h = h, a.w = w, a.V1 = C1 / 8, a.V2 = C2 / 8;
-    a.ndx = (uint32_t)((size_t)N * h * w * a.V1);
-    a.ndskip = (uint32_t)((size_t)N * 4 * h * w * a.V2);
-    const uint32_t n = a.ndx + a.ndskip;
-    hipLaunchKernelGGL(k_upcat_bwd, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+    const uint32_t nb = a.nbx + (a.ndskip + 255) / 256;
+    hipLaunchKernelGGL(k_upcat_bwd<false>, dim3(nb), dim3(256), 0, (hipStream_t)stream, a);
     NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+static int upcat_relu_check(int C1, const char* who) {
+    if (256 % (C1 / 8) != 0) return fail(-2, (std::string(who) + ": C1 / 8 must divide 256").c_str());
+    return 0;
+}
+
+size_t psfm_upcat_ws_floats(int N, int h, int w, int C1) {
+    return (size_t)upcat_args(N, h, w, C1, 0).nbx * (size_t)C1;
+}
+
+int psfm_upcat_bias_relu_fwd(const void* x, const void* bias, int bias_bf16, const void* skip, int N, int h, int w,
+                             int C1, int C2, void* out, void* stream) {
+    if (int e = upcat_check(N, h, w, C1, C2, "upcat_bias_relu_fwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)"))
+        return e;
+    if (int e = upcat_relu_check(C1, "upcat_bias_relu_fwd")) return e;
+    if (!x || !bias || !out || (C2 > 0 && !skip)) return fail(-1, "upcat_bias_relu_fwd: null pointer");
+    UpcatArgs a = upcat_args(N, h, w, C1, C2);
+    a.x = static_cast<const uint4*>(x);
+    a.skip = static_cast<const uint4*>(skip);
+    a.out = static_cast<uint4*>(out);
+    a.bias = bias, a.bias_bf16 = bias_bf16;
+    hipLaunchKernelGGL(k_upcat_fwd<true>, dim3((a.nfwd + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_upcat_bias_relu_bwd(const void* dout, const void* out, int N, int h, int w, int C1, int C2, void* dx,
+                             void* dskip, void* dbias, int bias_bf16, float* ws, void* stream) {
+    if (int e = upcat_check(N, h, w, C1, C2, "upcat_bias_relu_bwd: bad shape (C1 >= 8, C1 and C2 multiples of 8)"))
+        return e;
+    if (int e = upcat_relu_check(C1, "upcat_bias_relu_bwd")) return e;
+    if (!dout || !out || !dx || !dbias || !ws || (C2 > 0 && !dskip)) return fail(-1, "upcat_bias_relu_bwd: null pointer");
+    UpcatArgs a = upcat_args(N, h, w, C1, C2);
+    a.dout = static_cast<const uint4*>(dout);
+    a.out = static_cast<uint4*>(const_cast<void*>(out));
+    a.dx = static_cast<uint4*>(dx);
+    a.dskip = static_cast<uint4*>(dskip);
+    a.rows = ws;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t nb = a.nbx + (a.ndskip + 255) / 256;
+    hipLaunchKernelGGL(k_upcat_bwd<true>, dim3(nb), dim3(256), 0, st, a);
+    NETOPS_LAUNCH_CHECK();
+    const ColJob job{ws, dbias, C1, 0, (int)a.nbx, C1, bias_bf16};
+    if (hipError_t e = launch_finish(&job, 1, st)) return fail((int)e, "upcat_bias_relu_bwd: finish launch");
     return 0;
 }
 

@@ -256,3 +256,60 @@ def up_cat(x, skip=None):
         return _UpCat.apply(x, skip)
     up = upsample_nearest(x, 2)
     return up if skip is None else torch.cat([up, skip.to(up.dtype)], 1)
+
+
+class _UpCatBiasReLU(torch.autograd.Function):
+    """cat([nearest_up2(relu(x + bias)), skip]): the up-stage's first ConvBlock epilogue folded into
+    the up-stage input (include/psfm_netops.h psfm_upcat_bias_relu_*).  The ReLU mask of the
+    backward is read from the output itself (its x part holds relu(x + bias) upsampled)."""
+
+    @staticmethod
+    def forward(ctx, x, bias, skip):
+        N, C1, h, w = x.shape
+        C2 = skip.shape[1] if skip is not None else 0
+        out = torch.empty((N, C1 + C2, 2 * h, 2 * w), device=x.device, dtype=x.dtype,
+                          memory_format=torch.channels_last)
+        bf = int(bias.dtype == torch.bfloat16)
+        _hip.check(_hip.lib().psfm_upcat_bias_relu_fwd(_hip.ptr(x), _hip.ptr(bias), bf, _hip.ptr(skip), N, h, w, C1,
+                                                       C2, _hip.ptr(out), _hip.stream(x.device)),
+                   "psfm_upcat_bias_relu_fwd")
+        ctx.save_for_backward(out)
+        ctx.dims, ctx.has_skip, ctx.bias_dtype = (N, C1, C2, h, w), skip is not None, bias.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        N, C1, C2, h, w = ctx.dims
+        dout = _rows(dout)
+        L = _hip.lib()
+        dx = torch.empty((N, C1, h, w), device=dout.device, dtype=dout.dtype, memory_format=torch.channels_last)
+        dskip = torch.empty((N, C2, 2 * h, 2 * w), device=dout.device, dtype=dout.dtype,
+                            memory_format=torch.channels_last) if ctx.has_skip else None
+        db = torch.empty(C1, device=dout.device, dtype=ctx.bias_dtype)
+        ws = torch.empty(max(L.psfm_upcat_ws_floats(N, h, w, C1), 1), device=dout.device, dtype=torch.float32)
+        _hip.check(L.psfm_upcat_bias_relu_bwd(_hip.ptr(dout), _hip.ptr(out), N, h, w, C1, C2, _hip.ptr(dx),
+                                              _hip.ptr(dskip), _hip.ptr(db), int(ctx.bias_dtype == torch.bfloat16),
+                                              _hip.ptr(ws), _hip.stream(dout.device)), "psfm_upcat_bias_relu_bwd")
+        return dx, db, dskip
+
+
+def conv_block_up_cat(block, x, skip=None):
+    """cat([upsample(ConvBlock(x)), skip]) — ConvBlock = Conv3x3 + ReLU (layers.py:25-41), the
+    DepthDecoder's upconv_i0 followed by its up-stage input (depth_decoder.py:48-57).  On bf16
+    channels_last activations: the convolution without its bias, then ONE HIP kernel each way for
+    bias + ReLU + upsample + cat (psfm_upcat_bias_relu); otherwise the block and up_cat."""
+    c = block.conv
+    xin = c.pad(x) if c.pad is not None else x
+    bias = c.conv.bias
+    if FUSE["bias"] and UPCAT and bias is not None:
+        y = conv_nobias(c.conv, xin)
+        C1 = y.shape[1]
+        if (_nhwc_bf16(y) and C1 % 8 == 0 and 256 % (C1 // 8) == 0 and
+                (skip is None or (_nhwc_bf16(skip) and skip.shape[1] % 8 == 0 and skip.device == y.device
+                                  and tuple(skip.shape[-2:]) == (2 * y.shape[2], 2 * y.shape[3])
+                                  and skip.shape[0] == y.shape[0]))):
+            return _UpCatBiasReLU.apply(y, bias, skip)
+        return up_cat(bias_act(y, bias, ACT_RELU), skip)
+    return up_cat(block(x), skip)
+

@@ -7,7 +7,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..fused import ACT_SIGMOID, bias_act, conv_nobias, up_cat
+from ..fused import ACT_SIGMOID, bias_act, conv_block_up_cat, conv_nobias
 from .layers import Conv3x3, ConvBlock
 
 
@@ -35,9 +35,10 @@ class DepthDecoder(nn.Module):
         out = {}
         x = input_features[-1]
         for i in range(4, -1, -1):
-            # cat([upsample(upconv_i0(x)), skip]) as one fused op (fused.up_cat)
+            # cat([upsample(upconv_i0(x)), skip]) with upconv_i0's bias + ReLU folded in: one fused
+            # op each way after the convolution (fused.conv_block_up_cat)
             skip = input_features[i - 1] if (self.use_skips and i > 0) else None
-            x = self.convs[("upconv", i, 1)](up_cat(self.convs[("upconv", i, 0)](x), skip))
+            x = self.convs[("upconv", i, 1)](conv_block_up_cat(self.convs[("upconv", i, 0)], x, skip))
             if i in self.scales:
                 head = self.convs[("dispconv", i)]  # Conv3x3 + sigmoid, fused epilogue (fp32 maps)
                 xin = head.pad(x) if head.pad is not None else x

@@ -93,8 +93,8 @@ def test_decoders_bf16_fused_epilogues_as_close_as_the_reference_chain():
     from packnet_sfm_amd.networks.layers import fused as FU
     z = gu.load_golden("decoders_resnet")
     dev = torch.device("cuda:0")
-    calls = {"bias": 0, "upcat": 0}
-    ob, ou = FU._BiasAct.apply, FU._UpCat.apply
+    calls = {"bias": 0, "upcat": 0, "block_upcat": 0}
+    ob, ou, oc = FU._BiasAct.apply, FU._UpCat.apply, FU._UpCatBiasReLU.apply
     prev = dict(FU.FUSE), FU.UPCAT
 
     def count(kind, fn):
@@ -103,16 +103,19 @@ def test_decoders_bf16_fused_epilogues_as_close_as_the_reference_chain():
             return fn(*a)
         return wrapped
     FU._BiasAct.apply, FU._UpCat.apply = count("bias", ob), count("upcat", ou)
+    FU._UpCatBiasReLU.apply = count("block_upcat", oc)
     try:
         FU.FUSE.update(bias=True)
         FU.UPCAT = True
         fused = _run(dev, amp=True, channels_last=True)
-        assert calls["bias"] == 14 and calls["upcat"] == 5, calls   # 10 ConvBlocks + 4 heads, 5 up-stages
+        # 5 upconv_i1 ConvBlocks + 4 heads on psfm_bias_act; 5 upconv_i0 ConvBlocks folded into the
+        # up-stage input (psfm_upcat_bias_relu)
+        assert calls == {"bias": 9, "upcat": 0, "block_upcat": 5}, calls
         FU.FUSE.update(bias=False)
         FU.UPCAT = False
         plain = _run(dev, amp=True, channels_last=True)
     finally:
-        FU._BiasAct.apply, FU._UpCat.apply = ob, ou
+        FU._BiasAct.apply, FU._UpCat.apply, FU._UpCatBiasReLU.apply = ob, ou, oc
         FU.FUSE.update(prev[0])
         FU.UPCAT = prev[1]
     worst = []

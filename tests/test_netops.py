@@ -365,3 +365,29 @@ def test_gn_and_bias_reductions_are_deterministic(dev):
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert torch.equal(a_, b_)
+
+
+@gpu
+@pytest.mark.parametrize("N,C1,C2,h,w,bias_bf16", [(4, 256, 256, 6, 20, True), (4, 16, 0, 96, 320, True),
+                                                  (2, 32, 64, 48, 160, False), (1, 128, 64, 3, 5, True)])
+def test_conv_block_up_cat_equals_the_unfused_chain(dev, N, C1, C2, h, w, bias_bf16):
+    """psfm_upcat_bias_relu (ConvBlock bias + ReLU folded into the up-stage input) == bias_act then
+    up_cat: output, dx and dskip bitwise; the bias gradient sums the same bf16 values in another
+    order (1e-6 of max)."""
+    g = torch.Generator(device="cpu").manual_seed(C1 + h)
+    x = _cl(torch.randn(N, C1, h, w, generator=g)).to(dev, torch.bfloat16)
+    b = torch.randn(C1, generator=g).to(dev, torch.bfloat16 if bias_bf16 else torch.float32)
+    skip = _cl(torch.randn(N, C2, 2 * h, 2 * w, generator=g)).to(dev, torch.bfloat16) if C2 else None
+    dout = _cl(torch.randn(N, C1 + C2, 2 * h, 2 * w, generator=g)).to(dev, torch.bfloat16)
+    res = []
+    for fused in (True, False):
+        xi, bi = x.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        si = skip.clone().requires_grad_(True) if skip is not None else None
+        y = FU._UpCatBiasReLU.apply(xi, bi, si) if fused else FU.up_cat(FU.bias_act(xi, bi, FU.ACT_RELU), si)
+        y.backward(dout)
+        res.append((y.detach(), xi.grad, bi.grad, si.grad if si is not None else None))
+    (yf, dxf, dbf, dsf), (yu, dxu, dbu, dsu) = res
+    assert torch.equal(yf, yu) and torch.equal(dxf, dxu)
+    assert (dsf is None and dsu is None) or torch.equal(dsf, dsu)
+    assert dbf.dtype == b.dtype
+    assert (dbf.float() - dbu.float()).abs().max() <= 1e-6 * dbu.float().abs().max() + (2 ** -8 if bias_bf16 else 0) * dbu.float().abs().max()
