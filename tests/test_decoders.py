@@ -6,8 +6,9 @@ stays parity-unpinned (torchvision is absent); these heads are not.
 
   * CPU (the reference op chain): outputs 1e-5, every pinned gradient element 1e-4 * max;
   * GPU fp32 (MIOpen convolutions): 1e-3 * max per element;
-  * GPU bf16 autocast, channels_last — the production path, where the decoder runs the HIP
-    epilogues psfm_upcat (upsample + skip cat) and psfm_bias_act (bias + ReLU / sigmoid): every
+  * GPU bf16 autocast, channels_last, bf16 encoder features — the production path, where the
+    decoder runs the HIP epilogues psfm_upcat_bias_relu (the first ConvBlock's bias + ReLU, the
+    upsample and the skip cat) and psfm_bias_act (bias + ReLU / sigmoid): every
     output / gradient within 2x the error of the reference's own op chain under the same autocast
     (+ 1e-2 of max), and the fused kernels must actually have run."""
 import numpy as np
@@ -35,7 +36,9 @@ def _run(dev, amp=False, channels_last=False):
     fmt = torch.channels_last if channels_last else torch.contiguous_format
     if channels_last:
         dec, pdec = dec.to(memory_format=fmt), pdec.to(memory_format=fmt)
-    f = [t.to(dev).contiguous(memory_format=fmt).requires_grad_(True) for t in feats]
+    # under autocast the encoder hands the decoder bf16 features (its convolutions' outputs)
+    dt = torch.bfloat16 if amp else torch.float32
+    f = [t.to(dev, dt).contiguous(memory_format=fmt).requires_grad_(True) for t in feats]
     ctx = torch.autocast("cuda", dtype=torch.bfloat16) if amp else torch.autocast("cpu", enabled=False)
     with ctx:
         out = dec(f)

@@ -108,7 +108,8 @@ for (shape, has_res, has_bias, ng, act), n in calls.items():
     xg = x.detach().requires_grad_(True)
     y = orig(xg, bias, gn, act=act, residual=r)
     dy = torch.randn_like(y)
-    fwd_us = timed(lambda: orig(x, bias, gn, act=act, residual=r))
+    with torch.no_grad():   # the forward-only call (eval), as a training step's forward costs the same
+        fwd_us = timed(lambda: orig(x, bias, gn, act=act, residual=r))
     bwd_us = timed(lambda: torch.autograd.grad(y, xg, dy, retain_graph=True))
     el = x.numel()
     rr = 1 if has_res else 0
