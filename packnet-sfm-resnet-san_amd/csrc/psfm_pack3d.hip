@@ -38,6 +38,9 @@ int fail(int code, const std::string& msg) {
 constexpr int NTH = 256;
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
+#ifndef MFMA_DW
+#define MFMA_DW 1   // weight gradient of bf16 channels_last pack layers on the matrix cores
+#endif
 // ND: Conv3d output features d — 8 (PackNet01) or 4 (PackNetSAN01, num_3d_feat = 4)
 
 struct P3 {
@@ -565,6 +568,130 @@ __device__ __forceinline__ void bwd_w_body(const P3& a) {
     }
 }
 
+// --------------------------------------------------------------------------------------------
+// dW on the matrix cores — bf16 channels_last PACK layers (every PackNet encoder pack layer; the
+// first one is 10 G MACs per pass).  For one pixel p and a 32-channel chunk, the contribution to
+// dW is a small GEMM: A = dy[o][k] (d rows x 32 k) times B = the pixel's packed neighbourhood
+// B[k][n] = V[k + dz - 1, p + (sdy, sdx) - 1] for the 27 taps n = dz*9 + sdy*3 + sdx, plus a column
+// of ones (n = 27: the bias gradient sum_k dy) — one v_mfma_f32_16x16x32_bf16 per 16 columns
+// (M = 16 rows, d real; N = 32 columns, 28 real), accumulated over the tile's pixels and the
+// workgroup's chunks in fp32.  Workgroup = 4 x 16 pixel tile, 4 waves (wave w: tile row w).
+// LDS: V halo tile sv[yy][xx][kk] = V[k0 - 1 + kk] (kk < 34, rows padded to 40: 16-B aligned), the
+// (pixel, o) dy runs sg[p][o][32].  A lane's B fragment (8 consecutive k of its column) starts
+// dz elements into an aligned 16-B run: one ds_read_b128 + one ds_read_b32, and a 0 / 1 / 2
+// element shift (the dword funnel of dz = 1 is v_alignbyte).  Staging: x is channels_last and
+// V[k = 4c + 2i + j, y, x] = x[b, 2y + i, 2x + j, c], so each (pixel, i, j) gives 8 channels of
+// the chunk as one 16-byte load (k = k0 + 4e + 2i + j); the chunk halo k0 - 1 / k0 + 32 is one
+// element each.  Fixed instruction order, no atomics: deterministic; products of bf16 values are
+// exact in fp32 (the VALU kernel's arithmetic up to the accumulation order).
+template <int ND>
+__global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
+    constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LKP = 40, NP = TY * TX;
+    typedef short bf8 __attribute__((ext_vector_type(8)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint16_t sv[LY * LX * LKP];
+    __shared__ __attribute__((aligned(16))) uint16_t sg[NP * ND * DC];
+    __shared__ float red[4][2][64][4];
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int m = lane & 15, kq = (lane >> 4) * 8;
+    // this lane's B columns in the two halves: kind 0 = tap (dz, sdy, sdx), 1 = ones, 2 = zero
+    int kind[2], dz[2], off[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int n = 16 * h + m;
+        kind[h] = n < 27 ? 0 : (n == 27 ? 1 : 2);
+        const int tap = n < 27 ? n : 0, s = tap % 9;
+        dz[h] = tap / 9;
+        off[h] = ((s / 3) * LX + (s % 3)) * LKP + kq;   // + (tile row, column) of the pixel
+    }
+    const uint16_t* xv = static_cast<const uint16_t*>(a.x);
+    const uint16_t* gy = static_cast<const uint16_t*>(a.dy);
+    f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        const int k0 = ch * DC, c0 = k0 >> 2;
+        __syncthreads();
+        // V tile: (yy, xx, i, j) -> 8 channels c0 .. c0+7 = k0 + 4e + 2i + j, kk = that - k0 + 1
+        for (int e = t; e < LY * LX * 4; e += NTH) {
+            const int ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, i = ij >> 1, j = ij & 1;
+            uint4 q = make_uint4(0u, 0u, 0u, 0u);
+            if (gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                q = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * c0 + ij, gyy, gxx));
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint16_t* row = sv + pix * LKP + 1 + 2 * i + j;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                row[8 * u] = (uint16_t)(w[u] & 0xffffu);
+                row[8 * u + 4] = (uint16_t)(w[u] >> 16);
+            }
+        }
+        // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
+        for (int e = t; e < LY * LX * 2; e += NTH) {
+            const int hi = e & 1, pix = e >> 1, xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? k0 + 32 : k0 - 1;
+            uint16_t v = 0;
+            if (k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                v = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
+            sv[pix * LKP + (hi ? 33 : 0)] = v;
+        }
+        // dy runs: (pixel, o) -> 32 channels o K + k0 .. of the channels_last output, 4 x 16 B
+        for (int e = t; e < NP * ND * 4; e += NTH) {
+            const int qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
+            const int gyy = y0 + p / TX, gxx = x0 + p % TX;
+            uint4 q = make_uint4(0u, 0u, 0u, 0u);
+            if (gyy < a.Hv && gxx < a.Wv)
+                q = reinterpret_cast<const uint4*>(gy + yaddr<PSFM_P3D_PACK>(a, b, o, k0, gyy, gxx))[qd];
+            reinterpret_cast<uint4*>(sg + (p * ND + o) * DC)[qd] = q;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int px = 0; px < TX; ++px) {
+            const int p = wv * TX + px;
+            bf8 A = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (m < ND) A = *reinterpret_cast<const bf8*>(sg + (p * ND + m) * DC + kq);
+            bf8 Bf[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t o4[4] = {0u, 0u, 0u, 0u};
+                if (kind[h] == 0) {
+                    const uint16_t* src = sv + (wv * LX + px) * LKP + off[h];
+                    const uint4 d = *reinterpret_cast<const uint4*>(src);
+                    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(src + 8);
+                    const uint32_t dd[5] = {d.x, d.y, d.z, d.w, d4};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        o4[q] = dz[h] == 0 ? dd[q]
+                              : dz[h] == 2 ? dd[q + 1]
+                                           : __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], 2);
+                } else if (kind[h] == 1) {
+                    o4[0] = o4[1] = o4[2] = o4[3] = 0x3f803f80u;   // bf16 1.0 pairs
+                }
+                Bf[h] = __builtin_bit_cast(bf8, make_uint4(o4[0], o4[1], o4[2], o4[3]));
+            }
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[1], acc1, 0, 0, 0);
+        }
+    }
+    // the 4 waves' accumulators in wave order -> partial row [tap][o] (taps 0..26), [27 ND + o] bias
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        red[wv][0][lane][r] = acc0[r];
+        red[wv][1][lane][r] = acc1[r];
+    }
+    __syncthreads();
+    const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    // C/D map of 16x16x32: column = lane & 15, row = (lane >> 4) * 4 + register
+    for (int e = t; e < 28 * ND; e += NTH) {
+        const int o = e % ND, n = e / ND, h = n >> 4, col = n & 15;
+        const int ln = (o >> 2) * 16 + col, r = o & 3;
+        const float v = ((red[0][h][ln][r] + red[1][h][ln][r]) + red[2][h][ln][r]) + red[3][h][ln][r];
+        a.ws[blk * (27 * ND + ND) + e] = v;   // e = n * ND + o: taps then the bias row
+    }
+}
+
 template <typename T, int MODE, int ND, bool CL>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w(P3 a) { bwd_w_body<T, MODE, ND, CL>(a); }
 
@@ -733,12 +860,20 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         aw.x = x;
         aw.dy = dy;
         aw.ws = ws;
-        const dim3 grid = grid_of(aw, 4, 16, 16);
+        dim3 grid = grid_of(aw, 4, 16, 16);
         // channels_last dy of a pack layer: 16-channel runs are contiguous and 16-byte aligned
         const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
         const bool cl = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 16 == 0 && a.ys[0] % vec == 0 &&
                         a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
-        if (cl) {
+        // the matrix-core form: bf16, r = 2, channels_last x (8-channel 16-byte runs) and 32-k chunks
+        const bool mfma = cl && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 &&
+                          t->C % 8 == 0 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 &&
+                          (reinterpret_cast<uintptr_t>(x) & 15) == 0 && MFMA_DW;
+        if (mfma) {
+            grid = grid_of(aw, 4, 16, 32);
+            if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_w_mfma<4>, grid, dim3(NTH), 0, st, aw);
+            else hipLaunchKernelGGL(k_p3d_bwd_w_mfma<8>, grid, dim3(NTH), 0, st, aw);
+        } else if (cl) {
             if (t->dtype == PSFM_P3D_BF16) {
                 if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_w<uint16_t, PSFM_P3D_PACK, 4, true>), grid, dim3(NTH), 0, st, aw);
                 else hipLaunchKernelGGL((k_p3d_bwd_w<uint16_t, PSFM_P3D_PACK, 8, true>), grid, dim3(NTH), 0, st, aw);

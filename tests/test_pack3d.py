@@ -42,9 +42,11 @@ def _ref(mode, x, w, b, r):
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape,cl", [((2, 5, 14, 38), True), ((1, 16, 24, 40), False), ((2, 3, 6, 70), True),
-                                      ((1, 40, 10, 36), True)])
+                                      ((1, 40, 10, 36), True), ((2, 16, 22, 70), True)])
 def test_matches_reference_chain(dev, mode, dtype, shape, cl, d):
-    """d = 8: PackNet01; d = 4: PackNetSAN01 (num_3d_feat = 4)."""
+    """d = 8: PackNet01; d = 4: PackNetSAN01 (num_3d_feat = 4).  bf16 channels_last pack layers with
+    C % 8 == 0 ((1, 40, 10, 36): one 32-k chunk per tile pass of 5; (2, 16, 22, 70): 2 chunks, partial
+    edge tiles) take the matrix-core weight gradient (k_p3d_bwd_w_mfma)."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
     g = torch.Generator().manual_seed(sum(shape) + mode + d)
     B, C, H, W = shape
