@@ -610,43 +610,64 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
     const uint16_t* xv = static_cast<const uint16_t*>(a.x);
     const uint16_t* gy = static_cast<const uint16_t*>(a.dy);
     f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int ch = c_lo; ch < c_hi; ++ch) {
+    // software pipeline: the next chunk's global loads are issued into registers right after this
+    // chunk's tiles are in LDS, so their latency runs under this chunk's MFMA loop
+    constexpr int NV = (LY * LX * 4 + NTH - 1) / NTH;   // 16-byte V runs per thread
+    static_assert(LY * LX * 2 <= NTH && (NP * ND * 4) % NTH == 0, "staging slots");
+    uint4 vq[NV], gq[ND];   // NP * ND * 4 / NTH = ND dy slots per thread
+    uint16_t hq;
+    auto load = [&](int ch) {
         const int k0 = ch * DC, c0 = k0 >> 2;
-        __syncthreads();
-        // V tile: (yy, xx, i, j) -> 8 channels c0 .. c0+7 = k0 + 4e + 2i + j, kk = that - k0 + 1
-        for (int e = t; e < LY * LX * 4; e += NTH) {
-            const int ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, i = ij >> 1, j = ij & 1;
-            uint4 q = make_uint4(0u, 0u, 0u, 0u);
-            if (gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                q = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * c0 + ij, gyy, gxx));
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-            uint16_t* row = sv + pix * LKP + 1 + 2 * i + j;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                row[8 * u] = (uint16_t)(w[u] & 0xffffu);
-                row[8 * u + 4] = (uint16_t)(w[u] >> 16);
+        for (int u = 0; u < NV; ++u) {   // (yy, xx, i, j) -> 8 channels c0 .. c0+7 = k0 + 4e + 2i + j
+            const int e = t + u * NTH, ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+            vq[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (e < LY * LX * 4 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                vq[u] = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * c0 + ij, gyy, gxx));
+        }
+        {   // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
+            const int hi = t & 1, pix = t >> 1, xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? k0 + 32 : k0 - 1;
+            hq = 0;
+            if (t < LY * LX * 2 && k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                hq = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
+        }
+#pragma unroll
+        for (int u = 0; u < ND; ++u) {   // dy runs: (pixel, o) -> 32 channels o K + k0 .., 4 x 16 B
+            const int e = t + u * NTH, qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
+            const int gyy = y0 + p / TX, gxx = x0 + p % TX;
+            gq[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (gyy < a.Hv && gxx < a.Wv)
+                gq[u] = reinterpret_cast<const uint4*>(gy + yaddr<PSFM_P3D_PACK>(a, b, o, k0, gyy, gxx))[qd];
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = t + u * NTH, ij = e & 3, pix = e >> 2;
+            if (e >= LY * LX * 4) continue;
+            const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
+            uint16_t* row = sv + pix * LKP + 1 + 2 * (ij >> 1) + (ij & 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                row[8 * q] = (uint16_t)(w[q] & 0xffffu);
+                row[8 * q + 4] = (uint16_t)(w[q] >> 16);
             }
         }
-        // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
-        for (int e = t; e < LY * LX * 2; e += NTH) {
-            const int hi = e & 1, pix = e >> 1, xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? k0 + 32 : k0 - 1;
-            uint16_t v = 0;
-            if (k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                v = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
-            sv[pix * LKP + (hi ? 33 : 0)] = v;
+        if (t < LY * LX * 2) sv[(t >> 1) * LKP + ((t & 1) ? 33 : 0)] = hq;
+#pragma unroll
+        for (int u = 0; u < ND; ++u) {
+            const int e = t + u * NTH, qd = e & 3, po = e >> 2;
+            reinterpret_cast<uint4*>(sg + po * DC)[qd] = gq[u];   // po = p * ND + o
         }
-        // dy runs: (pixel, o) -> 32 channels o K + k0 .. of the channels_last output, 4 x 16 B
-        for (int e = t; e < NP * ND * 4; e += NTH) {
-            const int qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
-            const int gyy = y0 + p / TX, gxx = x0 + p % TX;
-            uint4 q = make_uint4(0u, 0u, 0u, 0u);
-            if (gyy < a.Hv && gxx < a.Wv)
-                q = reinterpret_cast<const uint4*>(gy + yaddr<PSFM_P3D_PACK>(a, b, o, k0, gyy, gxx))[qd];
-            reinterpret_cast<uint4*>(sg + (p * ND + o) * DC)[qd] = q;
-        }
+    };
+    if (c_lo < c_hi) load(c_lo);
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        __syncthreads();   // the previous chunk's MFMA loop is done with the tiles
+        store();
         __syncthreads();
+        if (ch + 1 < c_hi) load(ch + 1);
 #pragma unroll 4
         for (int px = 0; px < TX; ++px) {
             const int p = wv * TX + px;

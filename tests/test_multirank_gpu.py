@@ -114,9 +114,9 @@ def test_two_ranks_bf16_fused_split_path_keep_identical_masters():
 
 def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
     """Each rank's packed gradient equals one process's eager gradient of the same samples (every
-    tensor within 1e-4 of its largest entry, floored at 1e-3 of the largest gradient overall: the
-    graph replay and the eager pass run the same kernels, but two processes share the device
-    here), the buffer the optimizer graph reads is EXACTLY the average of the two
+    tensor within 1e-4 of its largest entry + 1e-6 of the largest gradient overall: the graph
+    replay and the eager pass run the same kernels, but two processes share the device here), the
+    buffer the optimizer graph reads is EXACTLY the average of the two
     ranks' gradients ((g0 + g1) * 0.5, bitwise), and stepping torch Adam on that average in one
     process gives both ranks' weights bit for bit after 3 steps."""
     r = _run("fp32det")
@@ -152,8 +152,8 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
                 assert float(out["loss"]) == float(r[k]["losses"][step]), (step, k)
                 out["loss"].sum().backward()
                 got, ref = r[k]["own"][step], flat([p.grad for p in params])
-                # per parameter tensor: |diff| <= 1e-4 * max(max|grad| of the tensor, 1e-3 * max|grad|
-                # overall) — MIOpen's "deterministic" solvers still reorder some fp32 backward
+                # per parameter tensor: |diff| <= 1e-4 * max|grad of that tensor| + 1e-6 * max|grad|
+                # overall — MIOpen's "deterministic" solvers still reorder some fp32 backward
                 # reductions when two processes share the device (profiles/r03/diag_bf16_spread.log),
                 # and a few tensors are pure rounding noise (PoseNet's first conv bias feeds a
                 # 1-channel-per-group GroupNorm: its exact gradient is 0)
@@ -163,13 +163,13 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
                     if p.grad is None:
                         continue
                     n = p.numel()
-                    scale = max(float(ref[off:off + n].abs().max()), 1e-3 * G)
-                    e = float((got[off:off + n] - ref[off:off + n]).abs().max()) / scale
+                    allow = 1e-4 * float(ref[off:off + n].abs().max()) + 1e-6 * G
+                    e = float((got[off:off + n] - ref[off:off + n]).abs().max()) / allow
                     worst_t = max(worst_t, (e, pnames[id(p)]))
                     off += n
                 print(f"step {step} rank {k}: packed gradient vs eager: bitwise {torch.equal(got, ref)}, worst "
-                      f"tensor {worst_t[1]} at {worst_t[0]:.1e} of its scale")
-                assert worst_t[0] <= 1e-4, (step, k, worst_t)
+                      f"tensor {worst_t[1]} at {worst_t[0]:.2f} of its allowance")
+                assert worst_t[0] <= 1.0, (step, k, worst_t)
             avg = (r[0]["own"][step] + r[1]["own"][step]) * 0.5
             assert torch.equal(r[0]["avg"][step], avg) and torch.equal(r[1]["avg"][step], avg), step
             off = 0
