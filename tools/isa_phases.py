@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Per-phase VALU instruction counts of K12's main sweep loop, from the gfx950 ISA.
+
+Compiles csrc/psfm_photometric.hip to device assembly, takes k12_fwd_grad<2, true, PINHOLE>
+(the training default), finds its main loop (the longest backward branch: 4 unrolled sweep steps)
+and splits it at the sched_barrier markers (PSFM_PHASE between issue | p-eval | q-eval | resolve,
+PSFM_CHAN between the SSIM channels).  Prints VALU / packed / DPP / memory counts per phase.
+  python tools/isa_phases.py [--kernel NAME]
+"""
+import argparse
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ap = argparse.ArgumentParser()
+ap.add_argument("--kernel", default="_ZN4psfm5fused12k12_fwd_gradILi2ELb1ELi0EEEvNS0_4ArgsE")
+a = ap.parse_args()
+with tempfile.TemporaryDirectory() as d:
+    s = os.path.join(d, "k.s")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S", "--cuda-device-only",
+                    "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "packnet-sfm-resnet-san_amd", "csrc", "psfm_photometric.hip"), "-o", s],
+                   check=True, capture_output=True)
+    lines = open(s).read().split("\n")
+start = next(i for i, ln in enumerate(lines) if ln.startswith(a.kernel + ":"))
+end = next(i for i in range(start + 1, len(lines)) if lines[i].startswith(".Lfunc_end"))
+body = lines[start:end]
+lab = {m.group(1): i for i, ln in enumerate(body) if (m := re.match(r"^(\.LBB\d+_\d+):", ln))}
+loops = []
+for i, ln in enumerate(body):
+    m = re.search(r"s_(cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", ln)
+    if m and m.group(2) in lab and lab[m.group(2)] < i:
+        loops.append((i - lab[m.group(2)], lab[m.group(2)], i))
+_, lo, hi = max(loops)
+phases, cur = [], []
+for ln in body[lo:hi + 1]:
+    if "sched_barrier" in ln:
+        phases.append(cur)
+        cur = []
+    else:
+        cur.append(ln.strip())
+phases.append(cur)
+tot = 0
+print(f"{a.kernel}: main loop {hi - lo + 1} lines, {len(phases)} segments between sched_barriers (4 sweep steps)")
+for k, ph in enumerate(phases):
+    if len(ph) < 4:
+        continue
+    v = sum(ln.startswith("v_") and not ln.startswith(("v_readlane", "v_writelane")) for ln in ph)
+    pk = sum(ln.startswith("v_pk_") for ln in ph)
+    dpp = sum(("row_" in ln or "quad_perm" in ln) for ln in ph)
+    mem = sum(ln.startswith(("global_load", "buffer_load", "ds_", "s_load", "global_store")) for ln in ph)
+    tot += v
+    print(f"  segment {k:2d}: VALU {v:4d} (v_pk {pk:3d}, DPP {dpp:3d})  memory {mem:3d}")
+print(f"  loop total VALU {tot} = {tot / 4:.0f} per sweep step (one issued row of 64 lanes)")
