@@ -68,7 +68,7 @@ def _worker(rank, world, init_file, out_dir, mode):
             own.append(t.detach().cpu().clone())
         return real(t, *a, **k)
     dist.all_reduce = spy
-    losses = []
+    losses, after = [], []
     try:
         for i in range(STEPS):
             if i:
@@ -78,12 +78,14 @@ def _worker(rank, world, init_file, out_dir, mode):
             losses.append(float(tr.train_step(batch)["loss"]))
             torch.cuda.synchronize()
             avg.append(tr.flat_grad.detach().cpu().clone())
+            if not bf16:   # the weights each optimizer graph replay left
+                after.append(torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()]))
     finally:
         dist.all_reduce = real
     assert len(tr.graphs) == 2   # split: step graph | all_reduce | optimizer graph
     assert len(own) == STEPS, len(own)
     out = {"seen": torch.tensor(seen), "losses": torch.tensor(losses), "own": torch.stack(own),
-           "avg": torch.stack(avg), "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()}}
+           "avg": torch.stack(avg), "after": torch.stack(after) if after else torch.zeros(0), "params": {n: p.detach().float().cpu() for n, p in model.named_parameters()}}
     if tr.fused is not None:
         out["master"] = tr.fused.master.cpu()
         assert int(tr.fused.step_count) == STEPS
@@ -113,12 +115,15 @@ def test_two_ranks_bf16_fused_split_path_keep_identical_masters():
 
 
 def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
-    """Each rank's packed gradient equals one process's eager gradient of the same samples (every
-    tensor within 1e-4 of its largest entry + 1e-6 of the largest gradient overall: the graph
-    replay and the eager pass run the same kernels, but two processes share the device here), the
-    buffer the optimizer graph reads is EXACTLY the average of the two
-    ranks' gradients ((g0 + g1) * 0.5, bitwise), and stepping torch Adam on that average in one
-    process gives both ranks' weights bit for bit after 3 steps."""
+    """Both ranks end with bit-identical weights; the buffer the optimizer graph reads is EXACTLY
+    the average of the two ranks' gradients ((g0 + g1) * 0.5, bitwise); and stepping torch Adam on
+    that average in one process reproduces the weights every optimizer replay left, bit for bit,
+    step by step.  Each rank's own packed gradient against one process's eager gradient of the
+    same samples and weights: bitwise at step 0 (same kernels, same inputs); at later steps
+    within 5e-3 relative L2 overall and 5e-2 per tensor — the photometric loss is non-smooth
+    (minimum reprojection, bilinear cells) and an ulp-level forward difference between the
+    replayed and the eager pass flips a few pixels' choices, which moves a disparity head's
+    gradient by ~6e-3 of its max (measured: depth_net.decoder.decoder.12 at step 1, rank 1)."""
     r = _run("fp32det")
     for n, p in r[0]["params"].items():
         assert torch.equal(p, r[1]["params"][n]), n
@@ -152,24 +157,25 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
                 assert float(out["loss"]) == float(r[k]["losses"][step]), (step, k)
                 out["loss"].sum().backward()
                 got, ref = r[k]["own"][step], flat([p.grad for p in params])
-                # per parameter tensor: |diff| <= 1e-4 * max|grad of that tensor| + 1e-6 * max|grad|
-                # overall — MIOpen's "deterministic" solvers still reorder some fp32 backward
-                # reductions when two processes share the device (profiles/r03/diag_bf16_spread.log),
-                # and a few tensors are pure rounding noise (PoseNet's first conv bias feeds a
-                # 1-channel-per-group GroupNorm: its exact gradient is 0)
                 G = float(ref.abs().max())
-                off, worst_t = 0, (0.0, "")
+                off, worst_t, worst_l2 = 0, (0.0, ""), (0.0, "")
                 for p in params:
                     if p.grad is None:
                         continue
                     n = p.numel()
-                    allow = 1e-4 * float(ref[off:off + n].abs().max()) + 1e-6 * G
-                    e = float((got[off:off + n] - ref[off:off + n]).abs().max()) / allow
-                    worst_t = max(worst_t, (e, pnames[id(p)]))
+                    a, b = got[off:off + n].double(), ref[off:off + n].double()
+                    allow = 1e-4 * float(b.abs().max()) + 1e-6 * G
+                    worst_t = max(worst_t, (float((a - b).abs().max()) / allow, pnames[id(p)]))
+                    worst_l2 = max(worst_l2, (float((a - b).norm() / b.norm().clamp_min(1e-6 * G)), pnames[id(p)]))
                     off += n
-                print(f"step {step} rank {k}: packed gradient vs eager: bitwise {torch.equal(got, ref)}, worst "
-                      f"tensor {worst_t[1]} at {worst_t[0]:.2f} of its allowance")
-                assert worst_t[0] <= 1.0, (step, k, worst_t)
+                tot = float((got.double() - ref.double()).norm() / ref.double().norm())
+                print(f"step {step} rank {k}: packed gradient vs eager: bitwise {torch.equal(got, ref)}, rel L2 "
+                      f"{tot:.2e}, worst tensor L2 {worst_l2[1]} {worst_l2[0]:.2e}, worst element "
+                      f"{worst_t[1]} at {worst_t[0]:.2f} x (1e-4 max_t + 1e-6 max)")
+                if step == 0:
+                    assert torch.equal(got, ref), (step, k, worst_t)
+                else:
+                    assert tot <= 5e-3 and worst_l2[0] <= 5e-2, (step, k, tot, worst_l2)
             avg = (r[0]["own"][step] + r[1]["own"][step]) * 0.5
             assert torch.equal(r[0]["avg"][step], avg) and torch.equal(r[1]["avg"][step], avg), step
             off = 0
@@ -179,6 +185,8 @@ def test_two_ranks_fp32_split_path_equal_one_process_on_the_averaged_gradient():
                         memory_format=torch.channels_last if p.dim() == 4 else torch.contiguous_format)
                     off += p.numel()
             opt.step()
+            now = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
+            assert torch.equal(now, r[0]["after"][step]), (step, float((now - r[0]["after"][step]).abs().max()))
         torch.cuda.synchronize()
     finally:
         torch.backends.cudnn.deterministic = False
