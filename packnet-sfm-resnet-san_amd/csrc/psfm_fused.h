@@ -61,15 +61,16 @@ using sweep::work_item;
 // scheduler triple the live temporaries (~40 VGPRs each)
 #define PSFM_CHAN() __builtin_amdgcn_sched_barrier(0)
 constexpr int WAVES = 2;         // waves per SIMD the register budget is sized for (<= 256 VGPRs)
-constexpr int RB = 20;           // q (output) rows per band (20 beats 16 / 24: 1760 waves on 2048 slots)
+// q (output) rows per band: chosen per launch among RB_LO / RB_HI by rb_for() (psfm_photometric.hip)
+// from the wave count against the device's wave slots — a wave costs RB + 5 sweep steps
+constexpr int RB_LO = 18, RB_HI = 28;
 constexpr int OW = 60;           // output columns per stripe
 constexpr int SIGCH = 16;        // chunks of the per-(scale, image) sigmoid sum pre-pass
 constexpr int GTS = 28;          // per-lane dL/dT row: 12 entries x 2 contexts, padded to 28 dwords
                                  // (the 16 lanes of a b128 access start on distinct bank groups)
-static_assert(RB % 4 == 0, "K12 band height must be a multiple of 4 (4-slot pipeline)");
 
 __host__ __device__ inline int stripes(int W) { return (W + OW - 1) / OW; }
-__host__ __device__ inline int units(int H, int W) { return stripes(W) * ((H + RB - 1) / RB); }
+__host__ __device__ inline int units(int H, int W, int rb) { return stripes(W) * ((H + rb - 1) / rb); }
 // wave-private LDS (each lane touches only its own column: no barriers):
 //   [3 row slots][6][64] f2  d warp / d(ix, iy) of both contexts | [64][GTS] dL/dT accumulators
 __host__ __device__ inline size_t lds_bytes(int NC) {
@@ -297,7 +298,7 @@ struct State {
     float acc_photo, acc_ax, acc_ay, acc_m;
 };
 
-template <int NC, bool FAST, int MODEL>
+template <int NC, bool FAST, int MODEL, int RB>
 struct K12 {
     static_assert(NC == 1 || NC == 2, "K12: one context pair (N <= 2, fused_ok)");
     static constexpr bool PAIR_CAM = MODEL == PSFM_CAM_PINHOLE;  // packed pinhole projection
@@ -333,11 +334,11 @@ struct K12 {
         c.load(reinterpret_cast<cfloat*>(rp), B, H, W);
         return c;
     }
+    // the context-paired pinhole record is NOT laundered: the compiler may keep it in SGPRs across
+    // the phases (105.2 vs 107.5 us per K12 call, profiles/r03/k12ab/kbench_variants_1.log)
     __device__ __forceinline__ CamPair load_pair() const {
-        uint64_t rp = reinterpret_cast<uint64_t>(campair);
-        asm volatile("" : "+s"(rp));
         CamPair c;
-        c.load(reinterpret_cast<cf2*>(rp), H, W);
+        c.load(reinterpret_cast<cf2*>(reinterpret_cast<uint64_t>(campair)), H, W);
         return c;
     }
 
@@ -419,7 +420,7 @@ struct K12 {
     }
 
     template <int I, bool LOAD, bool PEVAL, bool QEVAL>
-    __device__ __forceinline__ void step(State<NC>& S, int k) const {
+    __device__ __forceinline__ void step(State<NC>& S, int k, bool issue) const {
         constexpr int IA = (I + 1) & 3, IB = (I + 2) & 3, IC = (I + 3) & 3;
         const int v = y0 - 2 + k;
         Pend pd[NC];
@@ -434,7 +435,7 @@ struct K12 {
                 S.un[j] = (cfg.automask() && pin) ? a.ws.unwarp[((size_t)j * B + b) * plane + ppix] : 0.0f;
             S.mv = (mask && pin) ? mask[ppix] : 1.0f;
         }
-        if (LOAD) {
+        if (LOAD && issue) {
             const float sg = S.sg_next;
             S.sg_next = load_sig(v + 1);
             S.template SG<I>() = sg;
@@ -476,7 +477,7 @@ struct K12 {
                 S.D1[0][c] = S.D2[0][c];
             }
         }
-        if (LOAD) resolve_row<I>(S, k, pd);
+        if (LOAD && issue) resolve_row<I>(S, k, pd);
     }
 
     // the bilinear samples of the issued row (the duplicate context of NC = 1 is computed in the
@@ -685,10 +686,11 @@ struct K12 {
     }
 };
 
-template <int NC, bool FAST, int MODEL>
+template <int NC, bool FAST, int MODEL, int RB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) void k12_fwd_grad(Args a) {
+    static_assert(RB >= 4, "K12 band height");
     extern __shared__ __attribute__((aligned(16))) float k12_lds[];
-    const K12<NC, FAST, MODEL> K(a, k12_lds);
+    const K12<NC, FAST, MODEL, RB> K(a, k12_lds);
     State<NC> S;
     S.acc_photo = S.acc_ax = S.acc_ay = S.acc_m = 0.0f;
     S.h_p = S.h_n = S.t_pp = S.t_p = S.t_n = 0.0f;
@@ -697,23 +699,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
 #pragma unroll
     for (int m = 0; m < 24; ++m) K.gt[m] = 0.0f;
     // rows y0-2 .. y0+RB+1 issued at k = 0 .. RB+3; p-rows y0-1 .. y0+RB at k = 3 .. RB+4;
-    // q-rows y0 .. y0+RB-1 at k = 5 .. RB+4 (the last step's issue is a harmless extra row)
+    // q-rows y0 .. y0+RB-1 at k = 5 .. RB+4.  Step k uses row slot k & 3; the loop leaves after
+    // step RB+4 (wave-uniform branches, any RB), which issues nothing: no row after y0+RB+1 is read
+    constexpr int KE = RB + 4;
     S.sg_next = K.load_sig(K.y0 - 2);
-    K.template step<0, true, false, false>(S, 0);
-    K.template step<1, true, false, false>(S, 1);
-    K.template step<2, true, false, false>(S, 2);
-    K.template step<3, true, true, false>(S, 3);
-    K.template step<0, true, true, false>(S, 4);
+    K.template step<0, true, false, false>(S, 0, true);
+    K.template step<1, true, false, false>(S, 1, true);
+    K.template step<2, true, false, false>(S, 2, true);
+    K.template step<3, true, true, false>(S, 3, true);
+    K.template step<0, true, true, false>(S, 4, true);
 #pragma unroll 1
-    for (int k = 5; k < RB + 5; k += 4) {
-        K.template step<1, true, true, true>(S, k);
-        K.template step<2, true, true, true>(S, k + 1);
-        K.template step<3, true, true, true>(S, k + 2);
-        K.template step<0, true, true, true>(S, k + 3);
+    for (int k0 = 5;; k0 += 4) {
+        // opaque step index: no loop-carried strength-reduced addresses (each one an SGPR that the
+        // sweep's register peak spills to VGPR lanes and re-loads every step)
+        int k = k0;
+        asm volatile("" : "+s"(k));
+        K.template step<1, true, true, true>(S, k, k < KE);
+        if (k == KE) break;
+        K.template step<2, true, true, true>(S, k + 1, k + 1 < KE);
+        if (k + 1 == KE) break;
+        K.template step<3, true, true, true>(S, k + 2, k + 2 < KE);
+        if (k + 2 == KE) break;
+        K.template step<0, true, true, true>(S, k + 3, k + 3 < KE);
+        if (k + 3 == KE) break;
     }
     // per-wave partial sums (fixed-order wave butterflies)
     const psfm_params& p = a.p;
-    const int nu = units(p.H, p.W);
+    const int nu = units(p.H, p.W, RB);
     const float ph = wave_sum64(S.acc_photo);
     const float ax = wave_sum64(S.acc_ax), ay = wave_sum64(S.acc_ay), m = wave_sum64(S.acc_m);
     if (threadIdx.x == 0) {

@@ -17,6 +17,7 @@
 // them (reflect-aware weights) per pixel, then back-propagates through bilinear sampling and
 // the projection; dL/d[R|t] is reduced per tile (wave butterfly + fixed-order wave sum).
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <string>
 
@@ -1024,12 +1025,34 @@ bool use_sweep(const psfm_params* p) { return !p->l1_only; }
 // partial-sum units of the clip-statistics pass (always K1 / v1 tiles)
 int stats_units(const psfm_params* p) { return use_sweep(p) ? sweep::k1_units(p->H, p->W) : tiles_img(p->H, p->W); }
 bool fused_ok(const psfm_params* p) { return use_sweep(p) && p->N <= 2; }
+// K12 band height for this launch.  K12 is issue-bound with at most WAVES waves resident per SIMD,
+// and every wave of a launch costs RB + 5 sweep steps (4 halo rows + the pipeline tail), so the
+// launch time follows the busiest SIMD: waves per SIMD n -> about n / 2 two-wave rounds, a lone
+// wave running ~0.6 of a shared one.  Pick the candidate with the smallest steps x rounds on this
+// device's CU count (B = 4 at 192 x 640: RB 18 -> 1936 waves, one round; B = 6: RB 28 -> 1848
+// waves beat RB 18's 2904 = three waves on some SIMDs).
+int rb_for(const psfm_params* p) {
+    static int simds[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!simds[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        simds[dev] = 4 * cus;
+    }
+    auto cost = [&](int rb) {
+        const double waves = (double)fused::units(p->H, p->W, rb) * p->B * p->S;
+        const int n = (int)std::ceil(waves / simds[dev]);
+        return (double)(rb + 5) * ((n / 2) + ((n & 1) ? 0.6 : 0.0));
+    };
+    return cost(fused::RB_HI) < cost(fused::RB_LO) ? fused::RB_HI : fused::RB_LO;
+}
 int fwd_units(const psfm_params* p) {
-    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W);
+    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W, rb_for(p));
     return stats_units(p);
 }
 int bwd_units(const psfm_params* p) {
-    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W);
+    if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W, rb_for(p));
     return use_sweep(p) ? sweep::k2_units(p->H, p->W) : tiles_img(p->H, p->W);
 }
 
@@ -1083,6 +1106,26 @@ void launch_k1(const psfm_params* p, const sweep::SweepArgs& a, hipStream_t st) 
         launch_k1_t<STATS, false>(p, a, st);
 }
 
+template <int RB>
+void launch_k12(const psfm_params* p, bool fast, dim3 grid, size_t lds, hipStream_t st, const fused::Args& fa) {
+    constexpr int PIN = PSFM_CAM_PINHOLE, FISH = PSFM_CAM_FISHEYE;
+    if (p->cam_model == FISH) {
+        if (p->N == 1) {
+            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, FISH, RB>), grid, dim3(64), lds, st, fa);
+            else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, FISH, RB>), grid, dim3(64), lds, st, fa);
+        } else {
+            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, FISH, RB>), grid, dim3(64), lds, st, fa);
+            else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, FISH, RB>), grid, dim3(64), lds, st, fa);
+        }
+    } else if (p->N == 1) {
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, PIN, RB>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, PIN, RB>), grid, dim3(64), lds, st, fa);
+    } else {
+        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, PIN, RB>), grid, dim3(64), lds, st, fa);
+        else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, PIN, RB>), grid, dim3(64), lds, st, fa);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1093,7 +1136,7 @@ int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, s
                           size_t* clip_thr, size_t* pose, size_t* argmin_bytes, size_t* unwarp,
                           size_t* sig_part, size_t* cam_pairs) {
     if (!p) return fail(-1, "null params");
-    const int u = std::max(std::max(tiles_img(p->H, p->W), fused::units(p->H, p->W)),
+    const int u = std::max(std::max(tiles_img(p->H, p->W), fused::units(p->H, p->W, fused::RB_LO)),
                            std::max(sweep::k1_units(p->H, p->W), sweep::k2_units(p->H, p->W)));
     const size_t t = (size_t)u * p->B;
     const size_t ns = (size_t)n_src(*p);
@@ -1364,25 +1407,12 @@ int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const
         fa.grad_sig[s] = grad_sig[s];
     }
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid(fused::units(p->H, p->W), p->B, p->S);
+    const int rb = rb_for(p);
+    const dim3 grid(fused::units(p->H, p->W, rb), p->B, p->S);
     const size_t lds = fused::lds_bytes(p->N);
     const bool fast = fast_cfg(p, in);
-    constexpr int PIN = PSFM_CAM_PINHOLE, FISH = PSFM_CAM_FISHEYE;
-    if (p->cam_model == FISH) {
-        if (p->N == 1) {
-            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, FISH>), grid, dim3(64), lds, st, fa);
-            else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, FISH>), grid, dim3(64), lds, st, fa);
-        } else {
-            if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, FISH>), grid, dim3(64), lds, st, fa);
-            else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, FISH>), grid, dim3(64), lds, st, fa);
-        }
-    } else if (p->N == 1) {
-        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<1, true, PIN>), grid, dim3(64), lds, st, fa);
-        else hipLaunchKernelGGL((fused::k12_fwd_grad<1, false, PIN>), grid, dim3(64), lds, st, fa);
-    } else {
-        if (fast) hipLaunchKernelGGL((fused::k12_fwd_grad<2, true, PIN>), grid, dim3(64), lds, st, fa);
-        else hipLaunchKernelGGL((fused::k12_fwd_grad<2, false, PIN>), grid, dim3(64), lds, st, fa);
-    }
+    if (rb == fused::RB_HI) launch_k12<fused::RB_HI>(p, fast, grid, lds, st, fa);
+    else launch_k12<fused::RB_LO>(p, fast, grid, lds, st, fa);
     PSFM_LAUNCH_CHECK();
     return 0;
 }

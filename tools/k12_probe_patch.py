@@ -1,0 +1,44 @@
+"""Timing probes for K12 (tools/build_k12_variant.sh name:WAVES:RB:probe): edits a COPY of csrc/.
+Probe builds are for kbench timing only — their results are wrong by construction.
+
+  coal   : every bilinear gather reads the lane's own column of rows 0/1 (perfect locality):
+           how much of K12's time is gather latency / cache misses
+  sgcam  : camera records kept in SGPRs across the sweep (no per-use s_load re-read)
+  nogath : gathers replaced by constants (no vector-memory gathers at all)
+  launder: the pinhole camera pair re-read through a laundered pointer at every use (s_load)
+  noopq  : the sweep step index visible to the compiler (strength-reduced addresses)
+  rb20   : band height 20 for every launch (the round-2 shape)
+  rb40   : band height 40 for every launch (one wave per SIMD at B = 4, 192 x 640)
+"""
+import sys
+
+path, probe = sys.argv[1], sys.argv[2]
+src = open(path).read()
+if probe == "coal":
+    old = "    const TapAddr t = tap_addr(ix, iy, H, W);\n#pragma unroll\n    for (int c = 0; c < 3; ++c) {\n        g.q[c][0]"
+    new = ("    TapAddr t = tap_addr(ix, iy, H, W);\n    t.nw = threadIdx.x * 4u; t.ne = t.nw + 4u; t.sw = t.nw + (uint32_t)W * 4u; t.se = t.sw + 4u;\n"
+           "#pragma unroll\n    for (int c = 0; c < 3; ++c) {\n        g.q[c][0]")
+elif probe == "sgcam":
+    old = "        uint64_t rp = reinterpret_cast<uint64_t>(campair);\n        asm volatile(\"\" : \"+s\"(rp));"
+    new = "        uint64_t rp = reinterpret_cast<uint64_t>(campair);"
+elif probe == "nogath":
+    old = "        g.q[c][0] = ldg(img, c * pb + t.nw);\n        g.q[c][1] = ldg(img, c * pb + t.ne);\n        g.q[c][2] = ldg(img, c * pb + t.sw);\n        g.q[c][3] = ldg(img, c * pb + t.se);"
+    new = ("        g.q[c][0] = __uint_as_float(t.nw) * 1e-30f;\n        g.q[c][1] = __uint_as_float(t.ne) * 1e-30f;\n"
+           "        g.q[c][2] = __uint_as_float(t.sw) * 1e-30f;\n        g.q[c][3] = __uint_as_float(t.se) * 1e-30f;")
+elif probe == "launder":
+    old = "        CamPair c;\n        c.load(reinterpret_cast<cf2*>(reinterpret_cast<uint64_t>(campair)), H, W);"
+    new = ("        uint64_t rp = reinterpret_cast<uint64_t>(campair);\n        asm volatile(\"\" : \"+s\"(rp));\n"
+           "        CamPair c;\n        c.load(reinterpret_cast<cf2*>(rp), H, W);")
+elif probe == "noopq":
+    old = '        asm volatile("" : "+s"(k));\n'
+    new = ""
+elif probe == "rb20":
+    old = "constexpr int RB_LO = 18, RB_HI = 28;"
+    new = "constexpr int RB_LO = 20, RB_HI = 20;"
+elif probe == "rb40":
+    old = "constexpr int RB_LO = 18, RB_HI = 28;"
+    new = "constexpr int RB_LO = 40, RB_HI = 40;"
+else:
+    sys.exit("unknown probe " + probe)
+assert src.count(old) == 1, (probe, src.count(old))
+open(path, "w").write(src.replace(old, new))

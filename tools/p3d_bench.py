@@ -18,6 +18,7 @@ ap.add_argument("--lib", action="append", default=[])
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--net", default="packnet", choices=["packnet", "packnet-san"],
                 help="packnet: PackNet01 (d=8, n1=64); packnet-san: PackNetSAN01 (d=4, n1=32)")
+ap.add_argument("--only", default="", help="run only the case with this key (e.g. pack64x192x640)")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -62,6 +63,8 @@ for lib in (args.lib or [None]):
         _hip._lib = None
     res, tot = {}, [0.0, 0.0, 0.0]
     for mode, (C, H, W) in cases:
+        if args.only and args.only != f"{'pack' if mode == 0 else 'unpack'}{C}x{H}x{W}":
+            continue
         x = torch.randn(B, C, H, W, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
         b = torch.randn(D, device=dev) * 0.1
