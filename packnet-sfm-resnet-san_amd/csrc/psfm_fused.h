@@ -420,22 +420,37 @@ struct K12 {
     }
 
     template <int I, bool LOAD, bool PEVAL, bool QEVAL>
-    __device__ __forceinline__ void step(State<NC>& S, int k, bool issue) const {
+    __device__ __forceinline__ void step(State<NC>& S, int k) const {
         constexpr int IA = (I + 1) & 3, IB = (I + 2) & 3, IC = (I + 3) & 3;
         const int v = y0 - 2 + k;
         Pend pd[NC];
         if (PEVAL) {
             // the p-row's K0 candidates / mask FIRST: vmcnt retires in issue order, so loads issued
             // after the gathers would make the p-eval wait for the gathers too
+            // unconditional loads from a clamped address, the selection after: a load under a
+            // lane-divergent branch makes the wait-count pass merge its paths pessimistically, and
+            // the p-eval then waited for every gather of the step (s_waitcnt vmcnt(0))
             const int pv = v - 2;
             const bool pin = pcol && pv >= 0 && pv < H;
-            const uint32_t ppix = (uint32_t)(pv * W + col);
+            const uint32_t ppix = (uint32_t)(min(max(pv, 0), H - 1) * W + min(max(col, 0), W - 1));
+            if (cfg.automask()) {
 #pragma unroll
-            for (int j = 0; j < NC; ++j)
-                S.un[j] = (cfg.automask() && pin) ? a.ws.unwarp[((size_t)j * B + b) * plane + ppix] : 0.0f;
-            S.mv = (mask && pin) ? mask[ppix] : 1.0f;
+                for (int j = 0; j < NC; ++j) {
+                    const float u = a.ws.unwarp[((size_t)j * B + b) * plane + ppix];
+                    S.un[j] = pin ? u : 0.0f;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NC; ++j) S.un[j] = 0.0f;
+            }
+            if (mask) {
+                const float mv = mask[ppix];
+                S.mv = pin ? mv : 1.0f;
+            } else {
+                S.mv = 1.0f;
+            }
         }
-        if (LOAD && issue) {
+        if (LOAD) {
             const float sg = S.sg_next;
             S.sg_next = load_sig(v + 1);
             S.template SG<I>() = sg;
@@ -477,7 +492,7 @@ struct K12 {
                 S.D1[0][c] = S.D2[0][c];
             }
         }
-        if (LOAD && issue) resolve_row<I>(S, k, pd);
+        if (LOAD) resolve_row<I>(S, k, pd);
     }
 
     // the bilinear samples of the issued row (the duplicate context of NC = 1 is computed in the
@@ -700,27 +715,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
     for (int m = 0; m < 24; ++m) K.gt[m] = 0.0f;
     // rows y0-2 .. y0+RB+1 issued at k = 0 .. RB+3; p-rows y0-1 .. y0+RB at k = 3 .. RB+4;
     // q-rows y0 .. y0+RB-1 at k = 5 .. RB+4.  Step k uses row slot k & 3; the loop leaves after
-    // step RB+4 (wave-uniform branches, any RB), which issues nothing: no row after y0+RB+1 is read
+    // step RB+4 (wave-uniform branches, any RB).  That step's issue is a harmless extra row (reflect-
+    // clamped reads): skipping it behind a branch made the wait-count pass merge a path without the
+    // gathers, and every p-eval then waited for all of its step's gathers (s_waitcnt vmcnt(0))
     constexpr int KE = RB + 4;
     S.sg_next = K.load_sig(K.y0 - 2);
-    K.template step<0, true, false, false>(S, 0, true);
-    K.template step<1, true, false, false>(S, 1, true);
-    K.template step<2, true, false, false>(S, 2, true);
-    K.template step<3, true, true, false>(S, 3, true);
-    K.template step<0, true, true, false>(S, 4, true);
+    K.template step<0, true, false, false>(S, 0);
+    K.template step<1, true, false, false>(S, 1);
+    K.template step<2, true, false, false>(S, 2);
+    K.template step<3, true, true, false>(S, 3);
+    K.template step<0, true, true, false>(S, 4);
 #pragma unroll 1
     for (int k0 = 5;; k0 += 4) {
         // opaque step index: no loop-carried strength-reduced addresses (each one an SGPR that the
         // sweep's register peak spills to VGPR lanes and re-loads every step)
         int k = k0;
         asm volatile("" : "+s"(k));
-        K.template step<1, true, true, true>(S, k, k < KE);
+        K.template step<1, true, true, true>(S, k);
         if (k == KE) break;
-        K.template step<2, true, true, true>(S, k + 1, k + 1 < KE);
+        K.template step<2, true, true, true>(S, k + 1);
         if (k + 1 == KE) break;
-        K.template step<3, true, true, true>(S, k + 2, k + 2 < KE);
+        K.template step<3, true, true, true>(S, k + 2);
         if (k + 2 == KE) break;
-        K.template step<0, true, true, true>(S, k + 3, k + 3 < KE);
+        K.template step<0, true, true, true>(S, k + 3);
         if (k + 3 == KE) break;
     }
     // per-wave partial sums (fixed-order wave butterflies)

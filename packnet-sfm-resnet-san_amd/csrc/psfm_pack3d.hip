@@ -44,7 +44,8 @@ constexpr int P3D_WAVES = 2;
 // ND: Conv3d output features d — 8 (PackNet01) or 4 (PackNetSAN01, num_3d_feat = 4)
 
 struct P3 {
-    int B, C, Hv, Wv, r, K, KG;  // K volume channels, KG chunks of channels per workgroup
+    int B, C, Hv, Wv, r, K, KG;  // K volume channels, KG channel groups (workgroups per pixel tile)
+    int lin, gxn, gyn;           // lin: 1-D XCD-grouped grid over gxn x gyn tiles (wg_coords)
     int dy32;                    // every in-image element offset of dy fits int32 (host-checked)
     int64_t xs[4], ys[4];
     const void* x;
@@ -118,6 +119,24 @@ __device__ __forceinline__ int64_t yaddr(const P3& a, int b, int o, int k, int y
     return b * a.ys[0] + c * a.ys[1] + (int64_t)(y * a.r + i) * a.ys[2] + (int64_t)(x * a.r + j) * a.ys[3];
 }
 
+// (tile x, tile y, b * KG + kg) of this workgroup.  lin = 0: the 3-D grid.  lin = 1: a 1-D grid
+// dealt round-robin to the 8 XCDs (workgroup w -> XCD w % 8); the logical index runs contiguously
+// within each XCD with the channel group fastest, so the KG workgroups of one pixel tile run side
+// by side on ONE XCD: the x lines they all read (each group uses 16-32 bytes of a pixel's 128-byte
+// channels_last line) and the dy lines shared by neighbouring groups are fetched into that XCD's
+// L2 once instead of once per group (profiles/r03/p3d: the 3-D grid fetched 7.6x / 3.2x the
+// forward / weight-gradient operand bytes).
+struct WG {
+    int bx, by, bz;
+};
+__device__ __forceinline__ WG wg_coords(const P3& a) {
+    if (!a.lin) return WG{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const int n = gridDim.x, w = blockIdx.x, q = n / 8, rm = n % 8, xcd = w % 8, idx = w / 8;
+    const int L = xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
+    const int kg = L % a.KG, rest = L / a.KG, nt = a.gxn * a.gyn, tile = rest % nt, b = rest / nt;
+    return WG{tile % a.gxn, tile / a.gxn, b * a.KG + kg};
+}
+
 template <int ND>
 __device__ __forceinline__ void load_weights(const P3& a, float* sw) {
     // sw[tap * 8 + o] = w[o][tap]; sw[216 + o] = bias[o]
@@ -139,8 +158,9 @@ __device__ __forceinline__ void fwd_body(const P3& a) {
     __shared__ __attribute__((aligned(16))) float sv[LY * LX * LK];
     __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
     load_weights<ND>(a, sw);
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const WG g = wg_coords(a);
+    const int x0 = g.bx * TX, y0 = g.by * TY;
+    const int b = g.bz / a.KG, kg = g.bz - b * a.KG;
     const int nch = (a.K + DC - 1) / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
     const int kq = threadIdx.x % (DC / KB), p = threadIdx.x / (DC / KB), py = p / TX, px = p % TX;
     const int gy = y0 + py, gx = x0 + px;
@@ -219,6 +239,135 @@ template <typename T, int MODE, int ND>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_fwd(P3 a) {
     fwd_body<T, MODE, ND>(a);
 }
+// Forward of a PACK layer with channels_last x AND y (every PackNet encoder pack layer).  Same
+// arithmetic per output as fwd_body (the same 27 fp32 FMAs per (o, k, pixel) in the same order),
+// three changes measured against it (profiles/r03/p3d):
+//  * staging by 16-byte loads: V[k = 4c + 2i + j, y, x] = x[b, 2y + i, 2x + j, c], so one (pixel,
+//    i, j) gives 8 (bf16) / 4 (fp32) consecutive c of the chunk at once (fwd_body: one 2-byte load
+//    and a 64-bit address per element); the chunk halo k0 - 1 / k0 + 32 is one element each;
+//  * thread = (wave = 8-k group, lane = pixel): a 16-lane quarter of a b128 LDS read covers 16
+//    consecutive pixels of one tile row, whose 144-byte (LK = 36) runs start on 16 distinct 4-bank
+//    groups — conflict-free (fwd_body's (pixel, k-group) lanes hit 2-way conflicts);
+//  * CPW chunks per workgroup, the next chunk's loads in flight (registers) during this one's FMAs.
+template <typename T, int ND>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3 : 4))) void k_p3d_fwd_cl(P3 a) {
+    constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LK = DC + 4, KB = 8;
+    constexpr int VEC = 16 / sizeof(T);               // channels c per 16-byte load
+    constexpr int NQ = LY * LX * 4 * (8 / VEC);       // 16-byte loads per chunk: (pixel, i, j, c half)
+    constexpr int NV = (NQ + NTH - 1) / NTH;
+    static_assert(LY * LX * 2 <= NTH, "halo staging slots");
+    __shared__ __attribute__((aligned(16))) float sv[LY * LX * LK];
+    __shared__ __attribute__((aligned(16))) float sw[27 * ND + ND];
+    load_weights<ND>(a, sw);
+    const WG g = wg_coords(a);
+    const int x0 = g.bx * TX, y0 = g.by * TY;
+    const int b = g.bz / a.KG, kg = g.bz - b * a.KG;
+    const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int t = threadIdx.x, kq = t >> 6, lane = t & 63, py = lane >> 4, px = lane & 15;
+    const int gy = y0 + py, gx = x0 + px;
+    const T* xv = static_cast<const T*>(a.x);
+    uint4 vq[NV];
+    float hq;
+    auto load = [&](int ch) {
+        const int c0 = ch * (DC / 4);
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {   // e -> (pixel, i, j, half): c0 + VEC*half .. + VEC - 1
+            const int e = t + u * NTH, hf = (8 / VEC == 2) ? (e & 1) : 0, ij = (8 / VEC == 2) ? ((e >> 1) & 3) : (e & 3);
+            const int pix = (8 / VEC == 2) ? (e >> 3) : (e >> 2), xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+            vq[u] = make_uint4(0u, 0u, 0u, 0u);
+            if (e < NQ && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                vq[u] = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * (c0 + VEC * hf) + ij, gyy, gxx));
+        }
+        {   // kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, i = 0, j = 0)
+            const int hi = t & 1, pix = t >> 1, xx = pix % LX, yy = pix / LX;
+            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? 4 * c0 + 32 : 4 * c0 - 1;
+            hq = 0.0f;
+            if (t < LY * LX * 2 && k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
+                hq = ld<T>(a.x, vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx));
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = t + u * NTH;
+            if (e >= NQ) continue;
+            const int hf = (8 / VEC == 2) ? (e & 1) : 0, ij = (8 / VEC == 2) ? ((e >> 1) & 3) : (e & 3);
+            const int pix = (8 / VEC == 2) ? (e >> 3) : (e >> 2);
+            float* row = sv + pix * LK + 1 + 4 * VEC * hf + ij;   // kk = 1 + 4 c' + ij
+            const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
+            if constexpr (sizeof(T) == 2) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    row[8 * q] = __uint_as_float(w[q] << 16);
+                    row[8 * q + 4] = __uint_as_float(w[q] & 0xffff0000u);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) row[4 * q] = __uint_as_float(w[q]);
+            }
+        }
+        if (t < LY * LX * 2) sv[(t >> 1) * LK + ((t & 1) ? DC + 1 : 0)] = hq;
+    };
+    if (c_lo < c_hi) load(c_lo);
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        __syncthreads();   // the previous chunk's FMAs are done with the tile
+        store();
+        __syncthreads();
+        if (ch + 1 < c_hi) load(ch + 1);
+        if (gy >= a.Hv || gx >= a.Wv) continue;
+        const int kb = ch * DC + kq * KB;
+        float acc[ND][KB];
+#pragma unroll
+        for (int o = 0; o < ND; ++o)
+#pragma unroll
+            for (int j = 0; j < KB; ++j) acc[o][j] = sw[27 * ND + o];
+#pragma unroll 1   // one shift at a time: the accumulators + 12 V values + 24 weights live (3-4 waves/SIMD)
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll 1
+            for (int dx = 0; dx < 3; ++dx) {
+                const float4* vr = reinterpret_cast<const float4*>(sv + ((py + dy) * LX + (px + dx)) * LK + kq * KB);
+                float v[KB + 4];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const float4 q = vr[i];
+                    v[4 * i] = q.x, v[4 * i + 1] = q.y, v[4 * i + 2] = q.z, v[4 * i + 3] = q.w;
+                }
+#pragma unroll
+                for (int dz = 0; dz < 3; ++dz) {
+                    const float4* w4 = reinterpret_cast<const float4*>(sw + ((dz * 3 + dy) * 3 + dx) * ND);
+#pragma unroll
+                    for (int h = 0; h < ND / 4; ++h) {
+                        const float4 wv = w4[h];
+                        const float wo[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int j = 0; j < KB; ++j) acc[4 * h + u][j] += wo[u] * v[j + dz];
+                    }
+                }
+            }
+#pragma unroll
+        for (int o = 0; o < ND; ++o) {
+            T* dst = static_cast<T*>(a.y) + yaddr<PSFM_P3D_PACK>(a, b, o, kb, gy, gx);
+            if constexpr (sizeof(T) == 2) {
+                uint32_t w[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t lo = __float_as_uint(acc[o][2 * i]), hi = __float_as_uint(acc[o][2 * i + 1]);
+                    lo += 0x7fffu + ((lo >> 16) & 1u);
+                    hi += 0x7fffu + ((hi >> 16) & 1u);
+                    w[i] = (lo >> 16) | (hi & 0xffff0000u);
+                }
+                *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+            } else {
+                reinterpret_cast<float4*>(dst)[0] = make_float4(acc[o][0], acc[o][1], acc[o][2], acc[o][3]);
+                reinterpret_cast<float4*>(dst)[1] = make_float4(acc[o][4], acc[o][5], acc[o][6], acc[o][7]);
+            }
+        }
+    }
+}
+
 // other layouts (unpack layers, NCHW): thread = (k, pixel), element stores through yaddr
 template <typename T, int MODE, int ND>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(P3D_WAVES))) void k_p3d_fwd_generic(P3 a) {
@@ -592,8 +741,9 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
     __shared__ __attribute__((aligned(16))) uint16_t sv[LY * LX * LKP];
     __shared__ __attribute__((aligned(16))) uint16_t sg[NP * ND * DC];
     __shared__ float red[4][2][64][4];
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-    const int b = blockIdx.z / a.KG, kg = blockIdx.z - b * a.KG;
+    const WG g = wg_coords(a);
+    const int x0 = g.bx * TX, y0 = g.by * TY;
+    const int b = g.bz / a.KG, kg = g.bz - b * a.KG;
     const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int m = lane & 15, kq = (lane >> 4) * 8;
@@ -703,7 +853,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         red[wv][1][lane][r] = acc1[r];
     }
     __syncthreads();
-    const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;   // any 1-1 map
     // C/D map of 16x16x32: column = lane & 15, row = (lane >> 4) * 4 + register
     for (int e = t; e < 28 * ND; e += NTH) {
         const int o = e % ND, n = e / ND, h = n >> 4, col = n & 15;
@@ -796,8 +946,19 @@ P3 make(const psfm_p3d_desc* t) {
 dim3 grid_of(P3& a, int TY, int TX, int DC) {
     const int gx = (a.Wv + TX - 1) / TX, gy = (a.Hv + TY - 1) / TY;
     a.KG = k_groups(a.K, DC, gx * gy * a.B);
+    a.lin = 0;
     return dim3(gx, gy, a.B * a.KG);
 }
+// the XCD-grouped 1-D grid (wg_coords): kg_chunks channel chunks of DC per workgroup
+dim3 grid_lin(P3& a, int TY, int TX, int DC, int kg_chunks) {
+    a.gxn = (a.Wv + TX - 1) / TX;
+    a.gyn = (a.Hv + TY - 1) / TY;
+    a.KG = std::max(1, ((a.K + DC - 1) / DC) / kg_chunks);
+    a.lin = 1;
+    return dim3((unsigned)((int64_t)a.gxn * a.gyn * a.B * a.KG));
+}
+constexpr int P3D_FWD_CPW = 2;   // channel chunks per workgroup, channels_last pack forward
+constexpr int P3D_DW_CPW = 2;    // and MFMA weight gradient (the next chunk's loads overlap the MFMAs)
 
 }  // namespace
 
@@ -811,13 +972,26 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
     a.y = y;
     a.w = w;
     a.bias = bias;
-    const dim3 grid = grid_of(a, 4, 16, 32);
+    dim3 grid = grid_of(a, 4, 16, 32);
     hipStream_t st = (hipStream_t)stream;
     // channels_last pack output: each thread's 8 folded channels are one aligned 16-byte run
     const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
     const bool vst = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 8 == 0 && a.ys[0] % vec == 0 &&
                      a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-    if (vst) {
+    // channels_last x with r = 2 as well: 16-byte staging loads (k_p3d_fwd_cl)
+    const bool xcl = vst && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 && a.xs[0] % vec == 0 &&
+                     a.xs[2] % vec == 0 && a.xs[3] % vec == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (xcl) {
+        grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);
+        if (t->dtype == PSFM_P3D_BF16) {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd_cl<uint16_t, 4>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd_cl<uint16_t, 8>), grid, dim3(NTH), 0, st, a);
+        } else {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd_cl<float, 4>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd_cl<float, 8>), grid, dim3(NTH), 0, st, a);
+        }
+    } else if (vst) {
+        grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);
         if (t->dtype == PSFM_P3D_BF16) {
             if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd<uint16_t, PSFM_P3D_PACK, 4>), grid, dim3(NTH), 0, st, a);
             else hipLaunchKernelGGL((k_p3d_fwd<uint16_t, PSFM_P3D_PACK, 8>), grid, dim3(NTH), 0, st, a);
@@ -836,7 +1010,8 @@ int64_t psfm_p3d_ws_floats(const psfm_p3d_desc* t) {
     if (check_desc(t)) return -1;
     P3 a = make(t);
     const dim3 g = grid_of(a, 4, 16, 16);
-    return (int64_t)g.x * g.y * g.z * 28 * t->d;
+    const dim3 gl = grid_lin(a, 4, 16, 32, P3D_DW_CPW);
+    return std::max((int64_t)g.x * g.y * g.z, (int64_t)gl.x) * 28 * t->d;
 }
 
 int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const void* dy, void* dx, float* dw,
@@ -891,7 +1066,7 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
                           t->C % 8 == 0 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 &&
                           (reinterpret_cast<uintptr_t>(x) & 15) == 0 && MFMA_DW;
         if (mfma) {
-            grid = grid_of(aw, 4, 16, 32);
+            grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);
             if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_w_mfma<4>, grid, dim3(NTH), 0, st, aw);
             else hipLaunchKernelGGL(k_p3d_bwd_w_mfma<8>, grid, dim3(NTH), 0, st, aw);
         } else if (cl) {

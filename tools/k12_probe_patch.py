@@ -1,5 +1,6 @@
-"""Timing probes for K12 (tools/build_k12_variant.sh name:WAVES:RB:probe): edits a COPY of csrc/.
-Probe builds are for kbench timing only — their results are wrong by construction.
+"""Timing probes / A-B variants (tools/build_k12_variant.sh name:WAVES:probe[+probe]): edits a COPY
+of csrc/ (argument: that copy's psfm_fused.h; pack3d probes edit psfm_pack3d.hip beside it).
+coal / nogath builds are for kbench timing only — their results are wrong by construction.
 
   coal   : every bilinear gather reads the lane's own column of rows 0/1 (perfect locality):
            how much of K12's time is gather latency / cache misses
@@ -9,10 +10,15 @@ Probe builds are for kbench timing only — their results are wrong by construct
   noopq  : the sweep step index visible to the compiler (strength-reduced addresses)
   rb20   : band height 20 for every launch (the round-2 shape)
   rb40   : band height 40 for every launch (one wave per SIMD at B = 4, 192 x 640)
+  p3dold : pack3d forward / MFMA dW on the round-3 3-D grids (no XCD grouping)
+  fcpw2 / wcpwN : two / N 32-k chunks per workgroup in the pack3d forward / MFMA dW
 """
+import os
 import sys
 
 path, probe = sys.argv[1], sys.argv[2]
+if probe in ("p3dold", "fcpw2", "wcpw2", "wcpw4", "wcpw1"):
+    path = os.path.join(os.path.dirname(path), "psfm_pack3d.hip")
 src = open(path).read()
 if probe == "coal":
     old = "    const TapAddr t = tap_addr(ix, iy, H, W);\n#pragma unroll\n    for (int c = 0; c < 3; ++c) {\n        g.q[c][0]"
@@ -38,6 +44,16 @@ elif probe == "rb20":
 elif probe == "rb40":
     old = "constexpr int RB_LO = 18, RB_HI = 28;"
     new = "constexpr int RB_LO = 40, RB_HI = 40;"
+elif probe == "p3dold":
+    src = src.replace("grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);", "")
+    old = "grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);"
+    new = "grid = grid_of(aw, 4, 16, 32);"
+elif probe == "fcpw2":
+    old = "constexpr int P3D_FWD_CPW = 1;"
+    new = "constexpr int P3D_FWD_CPW = 2;"
+elif probe in ("wcpw1", "wcpw2", "wcpw4"):
+    old = "constexpr int P3D_DW_CPW = 2;"
+    new = "constexpr int P3D_DW_CPW = %s;" % probe[-1]
 else:
     sys.exit("unknown probe " + probe)
 assert src.count(old) == 1, (probe, src.count(old))
