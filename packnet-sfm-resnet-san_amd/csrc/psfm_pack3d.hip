@@ -267,7 +267,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
     const int gy = y0 + py, gx = x0 + px;
     const T* xv = static_cast<const T*>(a.x);
     uint4 vq[NV];
-    float hq;
+    T hq;   // raw: converted in store() (a conversion here would wait for the loads)
     auto load = [&](int ch) {
         const int c0 = ch * (DC / 4);
 #pragma unroll
@@ -282,9 +282,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
         {   // kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, i = 0, j = 0)
             const int hi = t & 1, pix = t >> 1, xx = pix % LX, yy = pix / LX;
             const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? 4 * c0 + 32 : 4 * c0 - 1;
-            hq = 0.0f;
+            hq = (T)0;
             if (t < LY * LX * 2 && k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                hq = ld<T>(a.x, vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx));
+                hq = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
         }
     };
     auto store = [&]() {
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
                 for (int q = 0; q < 4; ++q) row[4 * q] = __uint_as_float(w[q]);
             }
         }
-        if (t < LY * LX * 2) sv[(t >> 1) * LK + ((t & 1) ? DC + 1 : 0)] = hq;
+        if (t < LY * LX * 2) sv[(t >> 1) * LK + ((t & 1) ? DC + 1 : 0)] = ldi<T>(&hq, 0);
     };
     if (c_lo < c_hi) load(c_lo);
     for (int ch = c_lo; ch < c_hi; ++ch) {
@@ -506,9 +506,11 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
     const T* dyb = static_cast<const T*>(a.dy) + b * a.ys[0];
     const int ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
     f2 acc[4] = {f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
-    for (int o0 = 0; o0 < ND; o0 += OP) {
-        uint4 v[ITER][DC / VEC];
-        float e0[ITER], e1[ITER];
+    // the next o pass's dy runs are loaded into registers while this pass computes (raw words:
+    // any conversion here would make the loads complete before the compute starts)
+    uint4 v[ITER][DC / VEC];
+    T e0[ITER], e1[ITER];
+    auto load = [&](int o0) {
 #pragma unroll
         for (int i = 0; i < ITER; ++i) {
             const int u = t + i * NT2;
@@ -519,9 +521,12 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
 #pragma unroll
             for (int j = 0; j < DC / VEC; ++j)
                 v[i][j] = in ? reinterpret_cast<const uint4*>(src)[j] : make_uint4(0, 0, 0, 0);
-            e0[i] = in && k0 > 0 ? ldi<T>(src, -1) : 0.0f;
-            e1[i] = in && k0 + DC < a.K ? ldi<T>(src, DC) : 0.0f;
+            e0[i] = in && k0 > 0 ? src[-1] : (T)0;
+            e1[i] = in && k0 + DC < a.K ? src[DC] : (T)0;
         }
+    };
+    load(0);
+    for (int o0 = 0; o0 < ND; o0 += OP) {
         __syncthreads();   // the previous pass's reads of sg are done
 #pragma unroll
         for (int i = 0; i < ITER; ++i) {
@@ -544,12 +549,13 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
                     for (int q = 0; q < 4; ++q) f[j * 4 + q] = __uint_as_float(w4[q]);
                 }
             }
-            d2[0] = make_float2(e0[i], f[0]);
+            d2[0] = make_float2(ldi<T>(&e0[i], 0), f[0]);
 #pragma unroll
             for (int j = 1; j < DC / 2; ++j) d2[j] = make_float2(f[2 * j - 1], f[2 * j]);
-            d2[DC / 2] = make_float2(f[DC - 1], e1[i]);
+            d2[DC / 2] = make_float2(f[DC - 1], ldi<T>(&e1[i], 0));
         }
         __syncthreads();
+        if (o0 + OP < ND) load(o0 + OP);
 #pragma unroll 1
         for (int o = 0; o < OP; ++o)
 #pragma unroll
@@ -573,7 +579,11 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
                         const f2 c0 = dz == 0 ? pb[q + 2] : dz == 1 ? pm[q + 2] : pa[q + 2];
                         const f2 c1 = dz == 0 ? pb[q + 1] : dz == 1 ? pm[q + 1] : pa[q + 1];
                         const f2 c2 = dz == 0 ? pb[q] : dz == 1 ? pm[q] : pa[q];
-                        acc[q] += w0 * c0 + w1 * c1 + w2 * c2;
+                        // one fused multiply-add chain per pair (3 v_pk_fma_f32; the sum-then-add
+                        // form took 4 packed ops per 3 MAC pairs)
+                        acc[q] = w0 * c0 + acc[q];
+                        acc[q] = w1 * c1 + acc[q];
+                        acc[q] = w2 * c2 + acc[q];
                     }
                 }
             }
@@ -764,40 +774,57 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
     // chunk's tiles are in LDS, so their latency runs under this chunk's MFMA loop
     constexpr int NV = (LY * LX * 4 + NTH - 1) / NTH;   // 16-byte V runs per thread
     static_assert(LY * LX * 2 <= NTH && (NP * ND * 4) % NTH == 0, "staging slots");
+    // chunk-independent element offsets (int32: host-checked), computed once: a chunk adds c0 = k0 / 4
+    // (x) or k0 (dy); out-of-image / out-of-range slots read offset 0 and are zeroed by a select
+    // (no exec-mask branches around the loads)
+    int vo[NV], go[ND], ho;
+    uint32_t vok = 0u, gok = 0u;
+    bool hok;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {   // (yy, xx, i, j) -> 8 channels c0 .. c0+7 = k0 + 4e + 2i + j
+        const int e = t + u * NTH, ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
+        const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        const bool ok = e < LY * LX * 4 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        vo[u] = ok ? (int)vaddr<PSFM_P3D_PACK>(a, b, ij, gyy, gxx) : 0;
+        vok |= ok ? 1u << u : 0u;
+    }
+    const int hi = t & 1;
+    {   // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
+        const int pix = t >> 1, xx = pix % LX, yy = pix / LX, gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        hok = t < LY * LX * 2 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        ho = hok ? (int)vaddr<PSFM_P3D_PACK>(a, b, hi ? 32 : -1, gyy, gxx) : 0;   // + 4 c0 - ... below
+    }
+#pragma unroll
+    for (int u = 0; u < ND; ++u) {   // dy runs: (pixel, o) -> 32 channels o K + k0 .., 4 x 16 B
+        const int e = t + u * NTH, qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
+        const int gyy = y0 + p / TX, gxx = x0 + p % TX;
+        const bool ok = gyy < a.Hv && gxx < a.Wv;
+        go[u] = ok ? (int)yaddr<PSFM_P3D_PACK>(a, b, o, 0, gyy, gxx) + 8 * qd : 0;
+        gok |= ok ? 1u << u : 0u;
+    }
     uint4 vq[NV], gq[ND];   // NP * ND * 4 / NTH = ND dy slots per thread
     uint16_t hq;
+    // load(): loads only (the validity selects sit in store(): a select here would make the
+    // loads of the NEXT chunk complete before this chunk's MFMA loop starts)
+    bool hin = false;
     auto load = [&](int ch) {
         const int k0 = ch * DC, c0 = k0 >> 2;
 #pragma unroll
-        for (int u = 0; u < NV; ++u) {   // (yy, xx, i, j) -> 8 channels c0 .. c0+7 = k0 + 4e + 2i + j
-            const int e = t + u * NTH, ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
-            vq[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (e < LY * LX * 4 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                vq[u] = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * c0 + ij, gyy, gxx));
-        }
-        {   // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
-            const int hi = t & 1, pix = t >> 1, xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? k0 + 32 : k0 - 1;
-            hq = 0;
-            if (t < LY * LX * 2 && k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                hq = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
-        }
+        for (int u = 0; u < NV; ++u) vq[u] = *reinterpret_cast<const uint4*>(xv + ((vok >> u) & 1u ? vo[u] + c0 : 0));
+        // k = k0 - 1 -> channel c0 - 1 (i = j = 1); k = k0 + 32 -> channel c0 + 8 (i = j = 0): the
+        // offset ho holds the pixel part with channel -1 (i = j = 1) or 8 (i = j = 0)
+        hin = hok && (hi ? k0 + 32 < a.K : k0 > 0);
+        hq = xv[hin ? ho + c0 : 0];
 #pragma unroll
-        for (int u = 0; u < ND; ++u) {   // dy runs: (pixel, o) -> 32 channels o K + k0 .., 4 x 16 B
-            const int e = t + u * NTH, qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
-            const int gyy = y0 + p / TX, gxx = x0 + p % TX;
-            gq[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (gyy < a.Hv && gxx < a.Wv)
-                gq[u] = reinterpret_cast<const uint4*>(gy + yaddr<PSFM_P3D_PACK>(a, b, o, k0, gyy, gxx))[qd];
-        }
+        for (int u = 0; u < ND; ++u) gq[u] = *reinterpret_cast<const uint4*>(gy + ((gok >> u) & 1u ? go[u] + k0 : 0));
     };
     auto store = [&]() {
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
             const int e = t + u * NTH, ij = e & 3, pix = e >> 2;
             if (e >= LY * LX * 4) continue;
-            const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
+            const uint4 vv = (vok >> u) & 1u ? vq[u] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
             uint16_t* row = sv + pix * LKP + 1 + 2 * (ij >> 1) + (ij & 1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -805,11 +832,11 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
                 row[8 * q + 4] = (uint16_t)(w[q] >> 16);
             }
         }
-        if (t < LY * LX * 2) sv[(t >> 1) * LKP + ((t & 1) ? 33 : 0)] = hq;
+        if (t < LY * LX * 2) sv[(t >> 1) * LKP + ((t & 1) ? 33 : 0)] = hin ? hq : (uint16_t)0;
 #pragma unroll
         for (int u = 0; u < ND; ++u) {
             const int e = t + u * NTH, qd = e & 3, po = e >> 2;
-            reinterpret_cast<uint4*>(sg + po * DC)[qd] = gq[u];   // po = p * ND + o
+            reinterpret_cast<uint4*>(sg + po * DC)[qd] = (gok >> u) & 1u ? gq[u] : make_uint4(0u, 0u, 0u, 0u);   // po = p * ND + o
         }
     };
     if (c_lo < c_hi) load(c_lo);
@@ -820,25 +847,27 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         if (ch + 1 < c_hi) load(ch + 1);
 #pragma unroll 4
         for (int px = 0; px < TX; ++px) {
+            // branch-free fragments: every lane loads (rows m >= ND and the ones / zero columns
+            // read a valid run and are replaced by selects), so the loop carries no exec-mask
+            // branches around its LDS reads
             const int p = wv * TX + px;
-            bf8 A = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (m < ND) A = *reinterpret_cast<const bf8*>(sg + (p * ND + m) * DC + kq);
+            const uint4 ar = *reinterpret_cast<const uint4*>(sg + (p * ND + (m < ND ? m : 0)) * DC + kq);
+            const bf8 A = __builtin_bit_cast(bf8, m < ND ? ar : make_uint4(0u, 0u, 0u, 0u));
             bf8 Bf[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                uint32_t o4[4] = {0u, 0u, 0u, 0u};
-                if (kind[h] == 0) {
-                    const uint16_t* src = sv + (wv * LX + px) * LKP + off[h];
-                    const uint4 d = *reinterpret_cast<const uint4*>(src);
-                    const uint32_t d4 = *reinterpret_cast<const uint32_t*>(src + 8);
-                    const uint32_t dd[5] = {d.x, d.y, d.z, d.w, d4};
+                const uint16_t* src = sv + (wv * LX + px) * LKP + off[h];
+                const uint4 d = *reinterpret_cast<const uint4*>(src);
+                const uint32_t d4 = *reinterpret_cast<const uint32_t*>(src + 8);
+                const uint32_t dd[5] = {d.x, d.y, d.z, d.w, d4};
+                const uint32_t fill = kind[h] == 1 ? 0x3f803f80u : 0u;   // bf16 1.0 pairs | zero column
+                uint32_t o4[4];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        o4[q] = dz[h] == 0 ? dd[q]
-                              : dz[h] == 2 ? dd[q + 1]
-                                           : __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], 2);
-                } else if (kind[h] == 1) {
-                    o4[0] = o4[1] = o4[2] = o4[3] = 0x3f803f80u;   // bf16 1.0 pairs
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t v = dz[h] == 0 ? dd[q]
+                                     : dz[h] == 2 ? dd[q + 1]
+                                                  : __builtin_amdgcn_alignbyte(dd[q + 1], dd[q], 2);
+                    o4[q] = kind[h] == 0 ? v : fill;
                 }
                 Bf[h] = __builtin_bit_cast(bf8, make_uint4(o4[0], o4[1], o4[2], o4[3]));
             }
@@ -1062,9 +1091,15 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         const bool cl = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 16 == 0 && a.ys[0] % vec == 0 &&
                         a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
         // the matrix-core form: bf16, r = 2, channels_last x (8-channel 16-byte runs) and 32-k chunks
+        // (and every element offset of x and dy below 2^31: the kernel's staging offsets are int32)
+        const int64_t xmax = (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(t->C - 1) * a.xs[1] +
+                             (int64_t)(2 * a.Hv - 1) * a.xs[2] + (int64_t)(2 * a.Wv - 1) * a.xs[3];
+        const int64_t ymax = (int64_t)(t->B - 1) * a.ys[0] + (int64_t)(t->d * a.K - 1) * a.ys[1] +
+                             (int64_t)(a.Hv - 1) * a.ys[2] + (int64_t)(a.Wv - 1) * a.ys[3];
         const bool mfma = cl && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 &&
                           t->C % 8 == 0 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 &&
-                          (reinterpret_cast<uintptr_t>(x) & 15) == 0 && MFMA_DW;
+                          a.xs[0] >= 0 && a.xs[2] >= 0 && a.xs[3] >= 0 && a.ys[0] >= 0 && xmax < INT32_MAX - 64 &&
+                          ymax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && MFMA_DW;
         if (mfma) {
             grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);
             if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_w_mfma<4>, grid, dim3(NTH), 0, st, aw);

@@ -5,10 +5,10 @@
 # usage: tools/gpu_pmc_bench.sh [bench.py args...]
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$ROOT/gpurun_out/pmc
-rm -rf "$OUT"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 KEY=$(cd "$ROOT" && python3 -c "import sys, bench; print(bench.config_key(bench.parse(sys.argv[1:])))" "$@")
+OUT=$ROOT/gpurun_out/pmc/$KEY
+rm -rf "$OUT"; mkdir -p "$OUT"
 echo "[pmc] config $KEY"
 crash() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 i=0
@@ -21,4 +21,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   crash $rc && exit $rc
   [ $rc -ne 0 ] && exit $rc
 done
-python3 "$ROOT/tools/pmc_bench.py" "$KEY" "$OUT/$KEY.json" "$OUT"/p1 "$OUT"/p2 "$OUT"/p3
+python3 "$ROOT/tools/pmc_bench.py" "$KEY" "$OUT/$KEY.json" "$OUT"/p1 "$OUT"/p2 "$OUT"/p3 && rm -rf "$OUT"/p1 "$OUT"/p2 "$OUT"/p3

@@ -23,7 +23,8 @@ import sys
 NAMES = {"k12_fwd_grad": "K12_photometric_fwd_grad", "k0_unwarped": "K0_unwarped", "k_sig_sum": "sig_sum",
          "k_grad_finish": "grad_finish", "k_finalize": "finalize", "k_pose_reduce": "pose_grad_reduce",
          "k1_forward": "K1_photometric_fwd", "k2_backward": "K2_photometric_bwd",
-         "k_p3d_fwd": "p3d_fwd", "k_p3d_bwd_x": "p3d_bwd_x", "k_p3d_bwd_w": "p3d_bwd_w", "k_adam": "adam",
+         "k_p3d_fwd_cl": "p3d_fwd_cl", "k_p3d_bwd_x_cl": "p3d_bwd_x_cl", "k_p3d_bwd_w_mfma": "p3d_bwd_w_mfma",
+         "k_p3d_reduce_w": "p3d_reduce_w", "k_p3d_fwd": "p3d_fwd", "k_p3d_bwd_x": "p3d_bwd_x", "k_p3d_bwd_w": "p3d_bwd_w", "k_adam": "adam",
          "k_gn_fwd_stats": "gn_fwd_stats", "k_gn_fwd_apply": "gn_fwd_apply", "k_gn_bwd_stats": "gn_bwd_stats",
          "k_gn_bwd_apply": "gn_bwd_apply", "k_bias_act_fwd": "bias_act_fwd", "k_bias_act_bwd": "bias_act_bwd",
          "k_cols_finish": "cols_finish", "k_upcat_fwd": "upcat_fwd", "k_upcat_bwd": "upcat_bwd"}
