@@ -266,26 +266,35 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
     const int t = threadIdx.x, kq = t >> 6, lane = t & 63, py = lane >> 4, px = lane & 15;
     const int gy = y0 + py, gx = x0 + px;
     const T* xv = static_cast<const T*>(a.x);
+    // chunk-independent element offsets (int32, host-checked), computed once: a chunk adds c0;
+    // invalid slots read offset 0 and are zeroed at the LDS store (selects here would wait)
+    int vo[NV], ho;
+    uint32_t vok = 0u;
+    bool hok;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {   // e -> (pixel, i, j, half): c0 + VEC*half .. + VEC - 1
+        const int e = t + u * NTH, hf = (8 / VEC == 2) ? (e & 1) : 0, ij = (8 / VEC == 2) ? ((e >> 1) & 3) : (e & 3);
+        const int pix = (8 / VEC == 2) ? (e >> 3) : (e >> 2), xx = pix % LX, yy = pix / LX;
+        const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        const bool ok = e < NQ && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        vo[u] = ok ? (int)vaddr<PSFM_P3D_PACK>(a, b, 4 * VEC * hf + ij, gyy, gxx) : 0;
+        vok |= ok ? 1u << u : 0u;
+    }
+    const int hi = t & 1;
+    {   // kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, i = 0, j = 0)
+        const int pix = t >> 1, xx = pix % LX, yy = pix / LX, gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        hok = t < LY * LX * 2 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        ho = hok ? (int)vaddr<PSFM_P3D_PACK>(a, b, hi ? 32 : -1, gyy, gxx) : 0;   // + c0 per chunk
+    }
     uint4 vq[NV];
     T hq;   // raw: converted in store() (a conversion here would wait for the loads)
+    bool hin = false;
     auto load = [&](int ch) {
         const int c0 = ch * (DC / 4);
 #pragma unroll
-        for (int u = 0; u < NV; ++u) {   // e -> (pixel, i, j, half): c0 + VEC*half .. + VEC - 1
-            const int e = t + u * NTH, hf = (8 / VEC == 2) ? (e & 1) : 0, ij = (8 / VEC == 2) ? ((e >> 1) & 3) : (e & 3);
-            const int pix = (8 / VEC == 2) ? (e >> 3) : (e >> 2), xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
-            vq[u] = make_uint4(0u, 0u, 0u, 0u);
-            if (e < NQ && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                vq[u] = *reinterpret_cast<const uint4*>(xv + vaddr<PSFM_P3D_PACK>(a, b, 4 * (c0 + VEC * hf) + ij, gyy, gxx));
-        }
-        {   // kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, i = 0, j = 0)
-            const int hi = t & 1, pix = t >> 1, xx = pix % LX, yy = pix / LX;
-            const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx, k = hi ? 4 * c0 + 32 : 4 * c0 - 1;
-            hq = (T)0;
-            if (t < LY * LX * 2 && k >= 0 && k < a.K && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv)
-                hq = xv[vaddr<PSFM_P3D_PACK>(a, b, k, gyy, gxx)];
-        }
+        for (int u = 0; u < NV; ++u) vq[u] = *reinterpret_cast<const uint4*>(xv + ((vok >> u) & 1u ? vo[u] + c0 : 0));
+        hin = hok && (hi ? 4 * c0 + 32 < a.K : c0 > 0);
+        hq = xv[hin ? ho + c0 : 0];
     };
     auto store = [&]() {
 #pragma unroll
@@ -295,7 +304,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
             const int hf = (8 / VEC == 2) ? (e & 1) : 0, ij = (8 / VEC == 2) ? ((e >> 1) & 3) : (e & 3);
             const int pix = (8 / VEC == 2) ? (e >> 3) : (e >> 2);
             float* row = sv + pix * LK + 1 + 4 * VEC * hf + ij;   // kk = 1 + 4 c' + ij
-            const uint32_t w[4] = {vq[u].x, vq[u].y, vq[u].z, vq[u].w};
+            const uint4 vv = (vok >> u) & 1u ? vq[u] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
             if constexpr (sizeof(T) == 2) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -307,8 +317,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
                 for (int q = 0; q < 4; ++q) row[4 * q] = __uint_as_float(w[q]);
             }
         }
-        if (t < LY * LX * 2) sv[(t >> 1) * LK + ((t & 1) ? DC + 1 : 0)] = ldi<T>(&hq, 0);
+        if (t < LY * LX * 2) sv[(t >> 1) * LK + ((t & 1) ? DC + 1 : 0)] = hin ? ldi<T>(&hq, 0) : 0.0f;
     };
+    T* ydst = static_cast<T*>(a.y) + (gy < a.Hv && gx < a.Wv ? yaddr<PSFM_P3D_PACK>(a, b, 0, 0, gy, gx) : 0);
     if (c_lo < c_hi) load(c_lo);
     for (int ch = c_lo; ch < c_hi; ++ch) {
         __syncthreads();   // the previous chunk's FMAs are done with the tile
@@ -349,7 +360,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(ND == 8 ? 3
             }
 #pragma unroll
         for (int o = 0; o < ND; ++o) {
-            T* dst = static_cast<T*>(a.y) + yaddr<PSFM_P3D_PACK>(a, b, o, kb, gy, gx);
+            T* dst = ydst + o * a.K + kb;   // channels_last y: the folded channel o K + k is innermost
             if constexpr (sizeof(T) == 2) {
                 uint32_t w[4];
 #pragma unroll
@@ -746,11 +757,18 @@ __device__ __forceinline__ void bwd_w_body(const P3& a) {
 template <int ND>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
     constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LKP = 40, NP = TY * TX;
+    // LDS strides in 16-byte units: a pixel's V run 5, a tile row 97 (= 18 x 5 + 7), a (pixel, o)
+    // dy run 5.  The 9 spatial shifts a 16-lane MFMA fragment read touches sit at 5 sx + 97 sy
+    // = 5 sx + sy (mod 16): 9 distinct 4-bank groups; the A rows m = 0..7 at 5 m (mod 16): distinct
+    // (rows of 40 / 32 elements had 2-way conflicts: 13.6 % of the kernel's CU cycles, PMC)
+    constexpr int ROWS = LX * LKP + 56, DCP = 40;
     typedef short bf8 __attribute__((ext_vector_type(8)));
     typedef float f4 __attribute__((ext_vector_type(4)));
-    __shared__ __attribute__((aligned(16))) uint16_t sv[LY * LX * LKP];
-    __shared__ __attribute__((aligned(16))) uint16_t sg[NP * ND * DC];
-    __shared__ float red[4][2][64][4];
+    __shared__ __attribute__((aligned(16))) uint16_t sv[LY * ROWS];
+    __shared__ __attribute__((aligned(16))) uint16_t sg[NP * ND * DCP];
+    // the 4 waves' accumulators at the end reuse the dy tile's LDS (3 workgroups per CU stay)
+    typedef float RedT[2][64][4];
+    static_assert(sizeof(float) * 4 * 2 * 64 * 4 <= sizeof(uint16_t) * NP * ND * DCP, "red fits in sg");
     const WG g = wg_coords(a);
     const int x0 = g.bx * TX, y0 = g.by * TY;
     const int b = g.bz / a.KG, kg = g.bz - b * a.KG;
@@ -765,7 +783,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         kind[h] = n < 27 ? 0 : (n == 27 ? 1 : 2);
         const int tap = n < 27 ? n : 0, s = tap % 9;
         dz[h] = tap / 9;
-        off[h] = ((s / 3) * LX + (s % 3)) * LKP + kq;   // + (tile row, column) of the pixel
+        off[h] = (s / 3) * ROWS + (s % 3) * LKP + kq;   // + (tile row, column) of the pixel
     }
     const uint16_t* xv = static_cast<const uint16_t*>(a.x);
     const uint16_t* gy = static_cast<const uint16_t*>(a.dy);
@@ -825,18 +843,18 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
             if (e >= LY * LX * 4) continue;
             const uint4 vv = (vok >> u) & 1u ? vq[u] : make_uint4(0u, 0u, 0u, 0u);
             const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-            uint16_t* row = sv + pix * LKP + 1 + 2 * (ij >> 1) + (ij & 1);
+            uint16_t* row = sv + (pix / LX) * ROWS + (pix % LX) * LKP + 1 + 2 * (ij >> 1) + (ij & 1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 row[8 * q] = (uint16_t)(w[q] & 0xffffu);
                 row[8 * q + 4] = (uint16_t)(w[q] >> 16);
             }
         }
-        if (t < LY * LX * 2) sv[(t >> 1) * LKP + ((t & 1) ? 33 : 0)] = hin ? hq : (uint16_t)0;
+        if (t < LY * LX * 2) sv[((t >> 1) / LX) * ROWS + ((t >> 1) % LX) * LKP + ((t & 1) ? 33 : 0)] = hin ? hq : (uint16_t)0;
 #pragma unroll
         for (int u = 0; u < ND; ++u) {
             const int e = t + u * NTH, qd = e & 3, po = e >> 2;
-            reinterpret_cast<uint4*>(sg + po * DC)[qd] = (gok >> u) & 1u ? gq[u] : make_uint4(0u, 0u, 0u, 0u);   // po = p * ND + o
+            reinterpret_cast<uint4*>(sg + po * DCP)[qd] = (gok >> u) & 1u ? gq[u] : make_uint4(0u, 0u, 0u, 0u);   // po = p * ND + o
         }
     };
     if (c_lo < c_hi) load(c_lo);
@@ -851,12 +869,12 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
             // read a valid run and are replaced by selects), so the loop carries no exec-mask
             // branches around its LDS reads
             const int p = wv * TX + px;
-            const uint4 ar = *reinterpret_cast<const uint4*>(sg + (p * ND + (m < ND ? m : 0)) * DC + kq);
+            const uint4 ar = *reinterpret_cast<const uint4*>(sg + (p * ND + (m < ND ? m : 0)) * DCP + kq);
             const bf8 A = __builtin_bit_cast(bf8, m < ND ? ar : make_uint4(0u, 0u, 0u, 0u));
             bf8 Bf[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const uint16_t* src = sv + (wv * LX + px) * LKP + off[h];
+                const uint16_t* src = sv + wv * ROWS + px * LKP + off[h];
                 const uint4 d = *reinterpret_cast<const uint4*>(src);
                 const uint32_t d4 = *reinterpret_cast<const uint32_t*>(src + 8);
                 const uint32_t dd[5] = {d.x, d.y, d.z, d.w, d4};
@@ -876,6 +894,8 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         }
     }
     // the 4 waves' accumulators in wave order -> partial row [tap][o] (taps 0..26), [27 ND + o] bias
+    __syncthreads();   // every wave is done with the dy tile that red reuses
+    RedT* red = reinterpret_cast<RedT*>(sg);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         red[wv][0][lane][r] = acc0[r];
@@ -1008,8 +1028,11 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
     const bool vst = t->mode == PSFM_P3D_PACK && a.ys[1] == 1 && a.K % 8 == 0 && a.ys[0] % vec == 0 &&
                      a.ys[2] % vec == 0 && a.ys[3] % vec == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
     // channels_last x with r = 2 as well: 16-byte staging loads (k_p3d_fwd_cl)
+    const int64_t xmax = (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(t->C - 1) * a.xs[1] +
+                         (int64_t)(2 * a.Hv - 1) * a.xs[2] + (int64_t)(2 * a.Wv - 1) * a.xs[3];   // int32 staging offsets
     const bool xcl = vst && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 && a.xs[0] % vec == 0 &&
-                     a.xs[2] % vec == 0 && a.xs[3] % vec == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+                     a.xs[2] % vec == 0 && a.xs[3] % vec == 0 && a.xs[0] >= 0 && a.xs[2] >= 0 && a.xs[3] >= 0 &&
+                     xmax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (xcl) {
         grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);
         if (t->dtype == PSFM_P3D_BF16) {
