@@ -75,8 +75,14 @@ print(f"{sum(calls.values())} gn_act calls, {len(calls)} shapes", flush=True)
 def timed(fn):
     """Per-call GPU time: a HIP graph of args.iters calls replayed between two HIP events (no host
     launch gaps; --eager: back-to-back eager calls, an upper bound for small shapes)."""
-    for _ in range(3):
-        fn()
+    # warm-up on a side stream, then capture (torch.cuda.graph's documented pattern: the warm-up
+    # calls on the default stream followed by a capture crashed in capture_end, r3 session 2)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if args.eager:

@@ -12,6 +12,7 @@ coal / nogath builds are for kbench timing only — their results are wrong by c
   rb40   : band height 40 for every launch (one wave per SIMD at B = 4, 192 x 640)
   p3dold : pack3d forward / MFMA dW on the round-3 3-D grids (no XCD grouping)
   fcpw2 / wcpwN : two / N 32-k chunks per workgroup in the pack3d forward / MFMA dW
+  u8 / t1024 : netops row steps in flight per thread 8 / 1024 target workgroups
 """
 import os
 import sys
@@ -19,6 +20,8 @@ import sys
 path, probe = sys.argv[1], sys.argv[2]
 if probe in ("p3dold", "fcpw2", "wcpw2", "wcpw4", "wcpw1"):
     path = os.path.join(os.path.dirname(path), "psfm_pack3d.hip")
+if probe in ("u8", "t1024"):
+    path = os.path.join(os.path.dirname(path), "psfm_netops.hip")
 src = open(path).read()
 if probe == "coal":
     old = "    const TapAddr t = tap_addr(ix, iy, H, W);\n#pragma unroll\n    for (int c = 0; c < 3; ++c) {\n        g.q[c][0]"
@@ -54,6 +57,12 @@ elif probe == "fcpw2":
 elif probe in ("wcpw1", "wcpw2", "wcpw4"):
     old = "constexpr int P3D_DW_CPW = 2;"
     new = "constexpr int P3D_DW_CPW = %s;" % probe[-1]
+elif probe == "u8":
+    old = "constexpr int U = 4;"
+    new = "constexpr int U = 8;"
+elif probe == "t1024":
+    old = "constexpr int TARGET_BLOCKS = 512;"
+    new = "constexpr int TARGET_BLOCKS = 1024;"
 else:
     sys.exit("unknown probe " + probe)
 assert src.count(old) == 1, (probe, src.count(old))
