@@ -2,7 +2,7 @@
 # Round-3 measurement of the final library, per bench config: the bench line, a rocprofv3
 # kernel-trace step summary of the same command, and the stamped PMC profile (3 passes,
 # tools/gpu_pmc_bench.sh -> gpurun_out/pmc/<key>/<key>.json, copied by hand to profiles/pmc/).
-#   tools/r3_final.sh <tag> config [config ...]      (CPU baseline only for kitti-resnet-san; SKIP_PMC=1)
+#   tools/r3_final.sh <tag> config [config ...]      (CPU baseline only for kitti-resnet-san; SKIP_PMC=1, SKIP_BENCH=1)
 set -u
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -14,6 +14,7 @@ trap 'kill $hb 2>/dev/null' EXIT
 cd "$ROOT"
 for cfg in "$@"; do
   cb=--no-cpu-baseline; [ "$cfg" = kitti-resnet-san ] && cb=""
+  if [ "${SKIP_BENCH:-0}" != 1 ]; then
   timeout -k 10 400 python -u bench.py --config $cfg $cb > "$OUT/bench_$cfg.json" 2> "$OUT/bench_$cfg.err"; rc=$?
   echo "[bench $cfg] rc=$rc"; cut -c1-240 "$OUT/bench_$cfg.json"; [ $rc -ne 0 ] && { tail -5 "$OUT/bench_$cfg.err"; exit $rc; }
   (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$cfg" -o run --output-format csv \
@@ -23,8 +24,9 @@ for cfg in "$@"; do
   python3 tools/summarize_trace.py "$(find "$OUT/prof_$cfg" -name '*kernel_trace.csv' | head -1)" "$OUT/step_summary_$cfg.txt" \
     && head -3 "$OUT/step_summary_$cfg.txt" | cut -c1-160
   rm -rf "$OUT/prof_$cfg"
+  fi
   if [ "${SKIP_PMC:-0}" != 1 ]; then
-    bash tools/gpu_pmc_bench.sh --config $cfg; rc=$?
+    PMC_EXTRA=--no-miopen-find bash tools/gpu_pmc_bench.sh --config $cfg; rc=$?
     echo "[pmc $cfg] rc=$rc"; [ $rc -ne 0 ] && exit $rc
   fi
 done
