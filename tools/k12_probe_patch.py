@@ -13,6 +13,8 @@ coal / nogath builds are for kbench timing only — their results are wrong by c
   p3dold : pack3d forward / MFMA dW on the round-3 3-D grids (no XCD grouping)
   fcpw2 / wcpwN : two / N 32-k chunks per workgroup in the pack3d forward / MFMA dW
   u8 / t1024 : netops row steps in flight per thread 8 / 1024 target workgroups
+  prio   : K12 wave priority raised (s_setprio 2) over the issue phase, so its gathers go out first
+  prioq  : ... and over the q-eval phase (LDS read-modify-write chain)
 """
 import os
 import sys
@@ -63,6 +65,18 @@ elif probe == "u8":
 elif probe == "t1024":
     old = "constexpr int TARGET_BLOCKS = 512;"
     new = "constexpr int TARGET_BLOCKS = 1024;"
+elif probe in ("prio", "prioq"):
+    old = "        if (LOAD) {\n            const float sg = S.sg_next;"
+    new = "        __builtin_amdgcn_s_setprio(2);\n        if (LOAD) {\n            const float sg = S.sg_next;"
+    assert src.count(old) == 1
+    src = src.replace(old, new)
+    old = "        PSFM_PHASE();\n        if (PEVAL) peval<IA, IB, IC>(S, v - 2);"
+    new = "        __builtin_amdgcn_s_setprio(0);\n        PSFM_PHASE();\n        if (PEVAL) peval<IA, IB, IC>(S, v - 2);"
+    if probe == "prioq":
+        assert src.count(old) == 1
+        src = src.replace(old, new)
+        old = "        PSFM_PHASE();\n        if (QEVAL) qeval<IA>(S, v - 3, k);\n        PSFM_PHASE();"
+        new = "        PSFM_PHASE();\n        __builtin_amdgcn_s_setprio(2);\n        if (QEVAL) qeval<IA>(S, v - 3, k);\n        __builtin_amdgcn_s_setprio(0);\n        PSFM_PHASE();"
 else:
     sys.exit("unknown probe " + probe)
 assert src.count(old) == 1, (probe, src.count(old))
