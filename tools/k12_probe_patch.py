@@ -14,7 +14,9 @@ coal / nogath builds are for kbench timing only — their results are wrong by c
   fcpw2 / wcpwN : two / N 32-k chunks per workgroup in the pack3d forward / MFMA dW
   u8 / t1024 : netops row steps in flight per thread 8 / 1024 target workgroups
   prio   : K12 wave priority raised (s_setprio 2) over the issue phase, so its gathers go out first
-  prioq  : ... and over the q-eval phase (LDS read-modify-write chain)
+  prioq  : ... and over the q-eval phase (LDS read-modify-write chain)   [adopted in the source]
+  prior  : (on the adopted source) priority 2 also over the rotate + resolve of the step
+  noprio : (on the adopted source) no wave priorities
 """
 import os
 import sys
@@ -77,6 +79,14 @@ elif probe in ("prio", "prioq"):
         src = src.replace(old, new)
         old = "        PSFM_PHASE();\n        if (QEVAL) qeval<IA>(S, v - 3, k);\n        PSFM_PHASE();"
         new = "        PSFM_PHASE();\n        __builtin_amdgcn_s_setprio(2);\n        if (QEVAL) qeval<IA>(S, v - 3, k);\n        __builtin_amdgcn_s_setprio(0);\n        PSFM_PHASE();"
+elif probe == "prior":
+    old = "        if (QEVAL) qeval<IA>(S, v - 3, k);\n        __builtin_amdgcn_s_setprio(0);"
+    new = "        if (QEVAL) qeval<IA>(S, v - 3, k);"
+elif probe == "noprio":
+    src = src.replace("        __builtin_amdgcn_s_setprio(2);\n", "").replace("        __builtin_amdgcn_s_setprio(0);\n", "")
+    old = new = "__builtin_amdgcn_s_setprio"   # none left: count 0 -> assert below skipped
+    open(path, "w").write(src)
+    sys.exit(0)
 else:
     sys.exit("unknown probe " + probe)
 assert src.count(old) == 1, (probe, src.count(old))
