@@ -450,9 +450,10 @@ struct K12 {
                 S.mv = 1.0f;
             }
         }
-        // wave priority (two waves share a SIMD): the issue phase (its gathers go out first) and the
-        // q-eval (an LDS read-modify-write chain) run at priority 2, the long p-eval at 0 — the
-        // other wave's p-eval fills the latency (104.7-106.4 -> 99.3-99.4 us, profiles/r03/k12ab)
+        // wave priority (two waves share a SIMD): everything but the long p-eval — the q-eval (an
+        // LDS read-modify-write chain), the resolve and the next issue (its gathers go out first) —
+        // runs at priority 2, the p-eval at 0, so the other wave's p-eval fills the latency
+        // (kbench B=4 104.7-105.8 -> 98.4 us, B=6 146-147 -> 138 us; profiles/r03/k12ab)
         __builtin_amdgcn_s_setprio(2);
         if (LOAD) {
             const float sg = S.sg_next;
@@ -487,7 +488,6 @@ struct K12 {
         PSFM_PHASE();
         __builtin_amdgcn_s_setprio(2);
         if (QEVAL) qeval<IA>(S, v - 3, k);
-        __builtin_amdgcn_s_setprio(0);
         PSFM_PHASE();
         if (PEVAL) {  // rotate the carried per-row terms
             S.t_pp = S.t_p;
