@@ -130,18 +130,10 @@ def parse(argv=None):
 
 
 def source_hash():
-    """sha256 (16 hex) of the HIP library's sources (csrc/*.hip, csrc/*.h, include/*.h, sorted): the
-    code revision a stamped PMC profile was taken on."""
-    import hashlib
-    h = hashlib.sha256()
-    for d, exts in ((os.path.join(ROOT, "packnet-sfm-resnet-san_amd", "csrc"), (".hip", ".h")),
-                    (os.path.join(ROOT, "include"), (".h",))):
-        for f in sorted(os.listdir(d)):
-            if f.endswith(exts):
-                h.update(f.encode())
-                with open(os.path.join(d, f), "rb") as fh:
-                    h.update(fh.read())
-    return h.hexdigest()[:16]
+    """sha256 (16 hex) of the HIP library's sources — the hash build() compiles into the library
+    (psfm_version()) and the code revision a stamped profile was taken on."""
+    import __graft_entry__
+    return __graft_entry__.source_hash()
 
 
 def config_key(args):
@@ -335,6 +327,43 @@ def time_photometric_kernels(args, trainer, batch, HP):
     return HP.graph_replay_times_us(rec, sigs[0].device, reps=10, iters=args.kernel_iters)
 
 
+def k12_in_step(trainer, next_batch, device, reps=10):
+    """K12's duration INSIDE the training step: `reps` more step replays (after the timed region)
+    with the library's per-wave stamps on (psfm_k12_stamps: each K12 wave writes the constant
+    100 MHz clock at its start and end); the launch span = last end - first start.  This is the
+    kernel as it runs in the step graph — beside the pose branch, after the depth net — not an
+    isolated replay of it."""
+    from packnet_sfm_amd import _hip
+    L = _hip.lib()
+    cap = 1 << 16
+    buf = torch.zeros(cap, 2, dtype=torch.int64, device=device)
+    st = _hip.stream(device)
+    _hip.check(L.psfm_k12_stamps(_hip.ptr(buf), cap, st), "psfm_k12_stamps")
+    spans, wave_mean, wave_max, nwaves = [], [], [], 0
+    try:
+        for _ in range(reps):
+            buf.zero_()
+            trainer.train_step(next_batch())
+            torch.cuda.synchronize()
+            b = buf.cpu()
+            used = b[:, 0] > 0
+            if not bool(used.any()):   # this step does not run the K12 path
+                return None
+            s0, e1 = b[used, 0], b[used, 1]
+            spans.append(float(e1.max() - s0.min()) * 0.01)   # 100 MHz ticks -> us
+            d = (e1 - s0).double() * 0.01
+            wave_mean.append(float(d.mean()))
+            wave_max.append(float(d.max()))
+            nwaves = int(used.sum())
+    finally:
+        _hip.check(L.psfm_k12_stamps(None, 0, st), "psfm_k12_stamps")
+    return {"us_mean": round(statistics.mean(spans), 2), "us_median": round(statistics.median(spans), 2),
+            "us_min": round(min(spans), 2), "us_max": round(max(spans), 2), "reps": reps, "waves": nwaves,
+            "wave_us_mean": round(statistics.mean(wave_mean), 2), "wave_us_max": round(max(wave_max), 2),
+            "timing": "per-wave s_memrealtime stamps (100 MHz) of K12 inside the replayed step graph: "
+                      "last wave end - first wave start, mean over reps extra steps after the timed region"}
+
+
 def stamped_profile(args):
     """profiles/pmc/<config_key>.json written by tools/pmc_bench.py from rocprofv3 --pmc passes over
     THIS command's workload on THIS source revision; (None, path, why) when no file carries this
@@ -351,15 +380,17 @@ def stamped_profile(args):
     return prof, path, None
 
 
-def roofline(args, ktimes):
+def roofline(args, ktimes, instep=None):
     """Dominant kernel K12 (the fused warp + SSIM + min + smoothness fwd/bwd sweep) against
-    SURVEY §8(d)'s algorithmic bytes of the photometric fwd+bwd per image; the whole photometric
+    SURVEY §8(d)'s algorithmic bytes of the photometric fwd+bwd per image, timed IN the step
+    (k12_in_step) when available, the isolated graph replay beside it; the whole photometric
     group beside it; HBM traffic and VALU occupancy from the stamped PMC profile of this config."""
     images = args.batch * args.cameras
     bytes_step = algorithmic_bytes_per_image(args.height, args.width) * images
     group_us = sum(v for k, v in ktimes.items() if k != "clip_stats")
     dom = "K12_photometric_fwd_grad" if "K12_photometric_fwd_grad" in ktimes else "K2_photometric_bwd"
-    dom_us = ktimes[dom]
+    iso_us = ktimes[dom]
+    dom_us = instep["us_mean"] if (instep and dom == "K12_photometric_fwd_grad") else iso_us
     achieved = bytes_step / (dom_us * 1e-6) / 1e9
     out = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
@@ -367,12 +398,17 @@ def roofline(args, ktimes):
            "algorithmic_bytes_note": "SURVEY §8(d): H*W*(2*12*(1+N) + 12*S) B per image (120 B/px), x images "
                                      "per launch",
            "dominant_us_per_launch": round(dom_us, 2),
+           "dominant_timing": ("in step (k12_in_step: per-wave clock stamps inside the step graph)"
+                               if dom_us is not iso_us else "isolated graph replay"),
+           "isolated_us_per_launch": round(iso_us, 2),
+           "in_step": instep,
            "group": {"kernels": "prepass (K0 automask + sigmoid sums) + K12 + finalize + grad finish + pose reduce",
                      "us_per_step": round(group_us, 2),
                      "achieved": round(bytes_step / (group_us * 1e-6) / 1e9, 1),
                      "frac": round(bytes_step / (group_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
            "kernels_us_per_step": {k: round(v, 2) for k, v in ktimes.items()},
-           "timing": "HIP events around graph replays of each recorded C-ABI call (replay stream)"}
+           "timing": "kernels_us_per_step / group / isolated_us_per_launch: HIP events around graph replays "
+                     "of each recorded C-ABI call (replay stream)"}
     prof, path, why = stamped_profile(args)
     out["profile"] = os.path.relpath(path, ROOT) + ("" if prof else f" ({why}: traffic null)")
     out["source_hash"] = source_hash()
@@ -497,6 +533,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     trainer.check_finite()
+    instep = k12_in_step(trainer, next_batch, device)
     batch_now = trainer.static_batch if trainer.graphs else batch
     ktimes = {} if args.no_kernel_timing else time_photometric_kernels(args, trainer, batch_now, HP)
     if world > 1:
@@ -539,8 +576,11 @@ def main():
                                             f"op chain (MIOpen BN)" if args.fused_nets != "none" else "reference op chain"),
                           "decoder_upcat": "torch op chain" if args.no_upcat else "HIP (psfm_upcat)",
                           "weights": "random init (no network / checkpoints)", "config_key": config_key(args)}}
+        out["library"] = __graft_entry__.library_hash()
         if ktimes:
-            out["roofline"] = roofline(args, ktimes)
+            out["roofline"] = roofline(args, ktimes, instep)
+        elif instep:
+            out["k12_in_step"] = instep
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

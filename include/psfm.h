@@ -195,7 +195,15 @@ int psfm_view_synthesis_bwd(int cam_model, int B, int H, int W, const float* ref
 int psfm_tiles_per_image(int H, int W);
 
 const char* psfm_last_error(void);
+/* "psfm-gfx950 <ver> src=<16 hex>": the sha256 of the sources the library was built from */
 const char* psfm_version(void);
+
+/* Measurement hook (no reference counterpart): when buf != NULL, every later K12 launch
+ * (psfm_photometric_fwd_grad) writes each wave's start / end time on the constant 100 MHz clock
+ * (s_memrealtime) to buf[2 L], buf[2 L + 1] for workgroup L < capacity; buf = NULL, capacity = 0
+ * turns it off.  A device global, so launches inside an already-captured HIP graph are timed in
+ * place.  Synchronises `stream`; not for use during capture. */
+int psfm_k12_stamps(unsigned long long* buf, int capacity, void* stream);
 
 #ifdef __cplusplus
 }

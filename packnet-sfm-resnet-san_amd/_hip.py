@@ -66,6 +66,22 @@ class AugmentParams(ctypes.Structure):
 
 
 _lib = None
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _graft_entry():
+    """The repo's __graft_entry__ module (source_hash / library_hash), by path."""
+    import importlib.util
+    import sys
+    mod = sys.modules.get("__graft_entry__")
+    if mod is None:
+        spec = importlib.util.spec_from_file_location("__graft_entry__", os.path.join(REPO_ROOT, "__graft_entry__.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.modules["__graft_entry__"] = mod
+    return mod
+
+
 POSE_MAX_CTX = 8  # include/psfm_pose.h PSFM_POSE_MAX_CTX
 
 
@@ -77,6 +93,11 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"HIP extension {LIB_PATH} is not built: run `python -c 'import "
                            f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+    G = _graft_entry()
+    have, want = G.library_hash(LIB_PATH), G.source_hash()
+    if have != want:
+        raise RuntimeError(f"{LIB_PATH} was built from sources {have}, the tree holds {want}: rebuild "
+                           f"(__graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
     P, PP, V = ctypes.POINTER(Params), ctypes.POINTER(ctypes.POINTER(Params)), c_void_p
     WS, WSP, IN = ctypes.POINTER(Workspace), ctypes.POINTER(ctypes.POINTER(Workspace)), ctypes.POINTER(Inputs)
@@ -99,6 +120,7 @@ def lib():
         "psfm_tiles_per_image": ([c_int, c_int], c_int),
         "psfm_last_error": ([], ctypes.c_char_p),
         "psfm_version": ([], ctypes.c_char_p),
+        "psfm_k12_stamps": ([V, c_int, V], c_int),
         # include/psfm_optim.h
         "psfm_optim_plan_chunks": ([c_int, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32), c_int],
                                    c_int),
@@ -152,7 +174,7 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_smoothness_fwd", "psfm_finalize", "psfm_photometric_bwd", "psfm_smoothness_bwd",
             "psfm_pose_grad_reduce", "psfm_photometric_prepass", "psfm_photometric_fwd_grad", "psfm_photometric_grad_finish",
             "psfm_pose_grad_reduce_scaled", "psfm_view_synthesis_fwd", "psfm_view_synthesis_bwd",
-            "psfm_tiles_per_image", "psfm_last_error", "psfm_version",
+            "psfm_tiles_per_image", "psfm_last_error", "psfm_version", "psfm_k12_stamps",
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",

@@ -78,6 +78,24 @@ __host__ __device__ inline size_t lds_bytes(int NC) {
     return ((size_t)3 * 6 * 64 * 2 + (size_t)GTS * 64) * sizeof(float);
 }
 
+// Optional per-wave timestamps (psfm_k12_stamps): when set, lane 0 of every wave writes the
+// constant 100 MHz real-time clock at its start and its end to p[2 L], p[2 L + 1] (L = linear
+// workgroup id < cap) with vector stores.  A device global, not a kernel argument, so a captured
+// step graph can be timed in place: bench.py reads K12's in-step span from it.
+struct StampBuf {
+    unsigned long long* p;
+    int cap;
+};
+__device__ StampBuf g_k12_stamp;
+
+__device__ __forceinline__ void k12_stamp(int slot) {
+    const StampBuf sb = g_k12_stamp;
+    if (sb.p == nullptr) return;  // wave-uniform
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    if (L < sb.cap && threadIdx.x == 0) sb.p[2 * L + slot] = t;
+}
+
 struct Args {
     psfm_params p;
     psfm_inputs in;
@@ -711,6 +729,7 @@ struct K12 {
 template <int NC, bool FAST, int MODEL, int RB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) void k12_fwd_grad(Args a) {
     static_assert(RB >= 4, "K12 band height");
+    k12_stamp(0);
     extern __shared__ __attribute__((aligned(16))) float k12_lds[];
     const K12<NC, FAST, MODEL, RB> K(a, k12_lds);
     State<NC> S;
@@ -771,6 +790,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
             if (threadIdx.x == 0) o[mm] = t;
         }
     }
+    k12_stamp(1);
 }
 
 }  // namespace fused

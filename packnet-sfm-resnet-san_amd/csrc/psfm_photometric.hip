@@ -1472,6 +1472,22 @@ int psfm_pose_grad_reduce_scaled(int ncalls, const psfm_params* const* calls,
 }
 
 const char* psfm_last_error(void) { return g_err.c_str(); }
-const char* psfm_version(void) { return "psfm-gfx950 0.1"; }
+// the source hash is passed by __graft_entry__.build() (sha256 of csrc/ + include/): a run can
+// prove which sources the library it mapped was built from (build() rebuilds on a mismatch)
+#ifndef PSFM_SRC_HASH
+#define PSFM_SRC_HASH "unstamped-build!"
+#endif
+const char* psfm_version(void) { return "psfm-gfx950 0.2 src=" PSFM_SRC_HASH; }
+
+int psfm_k12_stamps(unsigned long long* buf, int capacity, void* stream) {
+    if (capacity < 0 || (buf == nullptr) != (capacity == 0)) return fail(-1, "bad stamp buffer");
+    const fused::StampBuf sb{buf, capacity};
+    const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(fused::g_k12_stamp), &sb, sizeof(sb), 0,
+                                                hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) return fail((int)e, "psfm_k12_stamps: hipMemcpyToSymbolAsync failed");
+    // the host struct is pageable: the async copy is staged before this returns, but keep the
+    // call synchronous with the stream so the next launch surely sees the new pointer
+    return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? 0 : fail(-3, "stream sync failed");
+}
 
 }  // extern "C"

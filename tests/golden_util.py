@@ -224,3 +224,18 @@ def decoder_inputs(B=1, H=32, W=96, seed=91):
     up_disp = [torch.randn(B, 1, H >> i, W >> i, generator=g) for i in range(4)]
     up_pose = torch.randn(B, 2, 1, 6, generator=g)
     return feats, up_disp, up_pose
+
+
+def seeded_inputs(seed, B, H, W, nctx=2):
+    """(image, contexts, K, pose vectors, 4 sigmoid maps) of the kink-free parity tests."""
+    g = torch.Generator().manual_seed(seed)
+    image = smooth_texture(g, B, 3, H, W)
+    ctx = [smooth_texture(g, B, 3, H, W) for _ in range(nctx)]
+    return image, ctx, kitti_K(B, H, W), pose_vecs(g, B, nctx), [sigmoid_maps(g, B, H, W) for _ in range(4)]
+
+
+# Seeds whose seeded_inputs have NO pixel oracle.sensitive_pixels flags (2e-4 px kink band, 5e-5 min /
+# 1e-4 L1 near-ties, 4 scales x 2 contexts), found offline with the CPU oracle
+# (tools/find_kink_free_seed.py: (1, 5, 130) has ~31 flagged pixels on average, 6 kink-free seeds in
+# 200k) and committed so the GPU test never searches or skips.
+KINK_FREE_SEEDS = {(1, 8, 40): 177, (1, 6, 70): 321, (1, 5, 130): 9324}

@@ -134,3 +134,12 @@ def test_depth_metrics_refuses_cpu_tensors(hip):
     cfg = types.SimpleNamespace(min_depth=0.0, max_depth=80.0, crop="garg", scale_output="top-center")
     with pytest.raises(RuntimeError, match="ROCm"):
         compute_depth_metrics(cfg, torch.ones(1, 1, 8, 8), torch.ones(1, 1, 8, 8))
+
+
+def test_library_carries_the_source_hash():
+    """build() compiles the sources' sha256 into the library (psfm_version): the built .so must be
+    the one the current sources produce (a stale library would make every GPU result unattributable)."""
+    import __graft_entry__ as G
+    assert G.library_hash() == G.source_hash(), "libpsfm_hip.so is stale: run __graft_entry__.build()"
+    from packnet_sfm_amd import _hip
+    assert _hip.lib().psfm_version().decode().endswith("src=" + G.source_hash())

@@ -154,3 +154,14 @@ def test_progressive_scaling_reproduces_reference():
         assert int(z["n_used"]) == ProgressiveScaling(0.25, 4)(float(z["progress"])) == 4
     doc = ProgressiveScaling(0.25, 4, reference_quirk=False)
     assert [doc(p) for p in (0.1, 0.3, 0.6, 0.9)] == [4, 3, 2, 1]
+
+
+def test_kink_free_seeds_are_kink_free():
+    """The committed seeds of test_hip_photometric.py::test_kink_free_inputs_match_oracle_tightly still
+    give inputs without a single flagged pixel (a change of the oracle's bands or of the generators
+    fails here, on the CPU, instead of silently weakening the GPU test)."""
+    for (B, H, W), seed in gu.KINK_FREE_SEEDS.items():
+        image, ctx, K, vec, sigs = gu.seeded_inputs(seed, B, H, W)
+        mats = [O.pose_vec_to_mat(vec[:, j]) for j in range(2)]
+        n = sum(int(m.sum()) for m in O.sensitive_pixels(image, ctx, sigs, K, mats, 0.5, 80.0))
+        assert n == 0, f"seed {seed} for {(B, H, W)} has {n} flagged pixels"
