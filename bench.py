@@ -118,6 +118,10 @@ def parse(argv=None):
                     help="net epilogues as fused HIP kernels (psfm_netops): none | all | a comma list of "
                          "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU), gn (GroupNorm + ReLU); "
                          "default: the measured winners (networks/layers/fused.py FUSE)")
+    ap.add_argument("--no-add-relu", action="store_true",
+                    help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
+    ap.add_argument("--no-hip-gather", action="store_true",
+                    help="resident batch gather as index_select + layout copies instead of psfm_gather_frames")
     ap.add_argument("--no-upcat", action="store_true",
                     help="DepthDecoder upsample + cat as the torch op chain instead of psfm_upcat")
     args = ap.parse_args(argv)
@@ -355,6 +359,9 @@ def k12_in_step(trainer, next_batch, device, reps=10):
             wave_mean.append(float(d.mean()))
             wave_max.append(float(d.max()))
             nwaves = int(used.sum())
+        if os.environ.get("PSFM_STAMP_DUMP"):   # the last step's per-wave stamps, for tools/k12_stamps.py
+            import numpy as np
+            np.save(os.environ["PSFM_STAMP_DUMP"], b[: int(used.nonzero().max()) + 1].numpy())
     finally:
         _hip.check(L.psfm_k12_stamps(None, 0, st), "psfm_k12_stamps")
     return {"us_mean": round(statistics.mean(spans), 2), "us_median": round(statistics.median(spans), 2),
@@ -476,6 +483,7 @@ def main():
     kinds = {"none": set(), "all": {"bias", "bn", "gn"}}.get(args.fused_nets, set(args.fused_nets.split(",")))
     fused.FUSE.update(bias="bias" in kinds, bn="bn" in kinds, gn="gn" in kinds)
     fused.UPCAT = not args.no_upcat
+    fused.ADD_RELU = not args.no_add_relu
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     torch.backends.cudnn.deterministic = args.deterministic != "none"
@@ -493,6 +501,8 @@ def main():
     if args.data_path == "sampler":
         dataset = SyntheticSfmDataset(8 * args.batch * world, args.height, args.width, N_CTX, args.cameras, seed=0)
         loader = ResidentLoader(dataset, args.batch, get_datasampler(dataset, "train"), device)
+        if args.no_hip_gather:
+            loader._gather_hip = lambda idx, dst: False
         batch = loader.next_into(None)
         if not args.nchw:
             net_layout(batch)

@@ -72,6 +72,19 @@ size_t psfm_augment_ws_bytes(const psfm_augment_params* p);
 int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const int32_t* plan,
                        const psfm_jitter* jitter, void* ws, float* rgb_original, float* rgb, void* stream);
 
+/* Batch gather of the HBM-resident training set (the build's DataLoader stand-in,
+ * datasets/synthetic.py ResidentLoader.next_into; the reference collates samples on the host,
+ * models/model_wrapper.py:1147-1216 DataLoader + trainers/base_trainer.py:8-39 sample_to_cuda).
+ * For each of `ntensor` (<= PSFM_GATHER_MAX) fp32 image stores src[t] [n*cams, 3, H, W] (NCHW), image
+ * b < B*cams of the batch is row idx[b / cams] * cams + b % cams; it is written to dst_nchw[t]
+ * [B*cams, 3, H, W] (NCHW, or NULL) and dst_nhwc[t] (the same tensor in channels_last storage, or
+ * NULL).  intr_src [n*cams][3][3] -> intr_dst [B*cams][3][3] the same way (both NULL to skip).
+ * idx: device int64 [B].  HW = H*W a multiple of 4, buffers 16-byte aligned.  One launch. */
+#define PSFM_GATHER_MAX 4
+int psfm_gather_frames(int ntensor, const float* const* src, float* const* dst_nchw, float* const* dst_nhwc,
+                       const int64_t* idx, int B, int cams, int HW, const float* intr_src, float* intr_dst,
+                       void* stream);
+
 const char* psfm_augment_last_error(void);
 
 #ifdef __cplusplus

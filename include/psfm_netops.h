@@ -70,26 +70,41 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, void* stream);
 
-/* y = act(GroupNorm(G)(x [+ res] + bias)) per sample (two launches: statistics rows, then apply with
- * the per-sample reduction in its prologue): x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
+/* y = act(GroupNorm(G)(x [+ res] + bias)) per sample: x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
  * or NULL, gamma/beta fp32 [C], act PSFM_ACT_NONE / RELU / ELU.  PoseNet conv_gn (conv + GN + ReLU,
  * PoseNet.py:15-19); PackNet Conv2D (conv + GN(16) + ELU, layers01.py:10-37) and ResidualConv's
  * GN(conv2 + shortcut) + ELU (res = the conv2 branch, layers01.py:40-61).  save_mean / save_invstd
- * [N*G]. */
+ * [N*G].  Layers whose (sample, whole-group channel block) fits one workgroup's registers (HW <= 12288
+ * row vectors, 8192 with res, at C / G <= 8; PackNet below 96x320) run ONE launch (statistics and
+ * apply in the workgroup); larger ones two (statistics rows, then apply with the per-sample reduction
+ * in its prologue).  Environment PSFM_GN_PATH=twopass forces the two-pass kernels. */
 int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
                     const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
                     float* save_invstd, float* ws, void* stream);
 
 /* Backward of psfm_gn_act_fwd: dx (bf16) and, with res, dres (a second copy: both inputs are summed),
- * dbias (bias dtype; the column sum of the stored dx, as autograd forms a conv bias gradient; NULL
- * with bias NULL), dgamma / dbeta (fp32 [C]).  The activation's derivative is taken at its input,
- * recomputed from x (+ res + bias), save_mean / save_invstd and gamma / beta — the forward output is
- * not read back (one activation-sized read less per pass).  Three launches: statistics rows, apply
- * (dx + conv-bias rows), parameter-gradient column totals. */
+ * dgamma / dbeta (fp32 [C]) and dbias (bias dtype, NULL with bias NULL).  dbias is the conv-bias
+ * gradient sum_{n,hw} dx in CLOSED FORM, per sample k1*S1 - HW*k2 - k3*X (S1 = sum dyr, X = sum xhat
+ * per channel, k1 = gamma*invstd, k2 / k3 the group terms of dx), summed over samples in fp64 from
+ * fp32 partial sums before any bf16 rounding — not the column sum of the stored bf16 dx that autograd
+ * would form; the two differ by the bf16 rounding noise of the N*HW summands (with one or two channels
+ * per group the exact sum is ~0 and both are noise; tests/test_netops.py pins it for cpg 1 / 2 / 4 / 8+).
+ * The activation's derivative is taken at its input, recomputed from x (+ res + bias), save_mean /
+ * save_invstd and gamma / beta — the forward output is not read back.  Resident layers (as the
+ * forward, register budget HW <= 4096 row vectors, 2048 with res): one data launch (dy, x read once)
+ * + a parameter finish over per-sample rows; others: statistics rows, then apply + parameter
+ * gradients (two launches). */
 int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,
                     const float* gamma, const float* beta, const float* save_mean, const float* save_invstd,
                     int N, int HW, int C, int G, int act, void* dx, void* dres, void* dbias, float* dgamma,
                     float* dbeta, float* ws, void* stream);
+
+/* BasicBlock tail after the BatchNorm (torchvision BasicBlock via resnet_encoder.py:61-98:
+ * out = relu(bn2(conv2(.)) + identity)): y = relu(bf16(a + b)) over n bf16 elements (n % 8 == 0,
+ * 16-byte aligned; any layout, a / b / y alike) — the add and the ReLU of autocast's op chain in one
+ * pass; and its backward dz = (y <= 0) ? 0 : dy, ATen's threshold_backward (both inputs get dz). */
+int psfm_add_relu_fwd(const void* a, const void* b, long long n, void* y, void* stream);
+int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, void* stream);
 
 const char* psfm_netops_last_error(void);
 

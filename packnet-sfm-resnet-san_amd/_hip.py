@@ -13,6 +13,7 @@ import torch
 
 LIB_NAME = "libpsfm_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+DEFAULT_LIB_PATH = LIB_PATH
 
 MAX_CTX = 4
 MAX_SCALES = 4
@@ -95,7 +96,9 @@ def lib():
                            f"__graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
     G = _graft_entry()
     have, want = G.library_hash(LIB_PATH), G.source_hash()
-    if have != want:
+    # the product library must be the one the tree's sources build (A/B tools may point LIB_PATH at
+    # a variant build under build/variants; only the default path is checked)
+    if LIB_PATH == DEFAULT_LIB_PATH and have != want:
         raise RuntimeError(f"{LIB_PATH} was built from sources {have}, the tree holds {want}: rebuild "
                            f"(__graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
@@ -139,6 +142,8 @@ def lib():
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,
                              V], c_int),
         "psfm_netops_last_error": ([], ctypes.c_char_p),
+        "psfm_add_relu_fwd": ([V, V, ctypes.c_longlong, V, V], c_int),
+        "psfm_relu_mask_bwd": ([V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_upcat_bwd": ([V, c_int, c_int, c_int, c_int, c_int, V, V, V], c_int),
         "psfm_upcat_bias_relu_fwd": ([V, V, c_int, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
@@ -156,6 +161,7 @@ def lib():
         "psfm_augment_plan": ([ctypes.POINTER(AugmentParams), V], ctypes.c_longlong),
         "psfm_augment_ws_bytes": ([ctypes.POINTER(AugmentParams)], c_size_t),
         "psfm_train_augment": ([ctypes.POINTER(AugmentParams), V, V, V, V, V, V, V], c_int),
+        "psfm_gather_frames": ([c_int, V, V, V, V, c_int, c_int, c_int, V, V, V], c_int),
         "psfm_augment_last_error": ([], ctypes.c_char_p),
         # include/psfm_pose.h
         "psfm_pose_from_vec_fwd": ([V, c_int, c_int, V, V], c_int),
@@ -178,11 +184,13 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
+            "psfm_add_relu_fwd", "psfm_relu_mask_bwd",
             "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",
             "psfm_upcat_ws_floats",
             "psfm_depth_metrics", "psfm_metrics_last_error",
             "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
-            "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_augment_last_error",
+            "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_gather_frames",
+            "psfm_augment_last_error",
             "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error")
 
 
@@ -190,11 +198,12 @@ def check(rc, what):
     if rc != 0:
         if what.startswith(("psfm_optim", "psfm_grad", "psfm_adam")):
             err = lib().psfm_optim_last_error
-        elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops", "psfm_upcat")):
+        elif what.startswith(("psfm_bias_act", "psfm_bn_act", "psfm_gn_act", "psfm_netops", "psfm_upcat",
+                              "psfm_add_relu", "psfm_relu_mask")):
             err = lib().psfm_netops_last_error
         elif what.startswith("psfm_depth_metrics"):
             err = lib().psfm_metrics_last_error
-        elif what.startswith(("psfm_augment", "psfm_train_augment")):
+        elif what.startswith(("psfm_augment", "psfm_train_augment", "psfm_gather_frames")):
             err = lib().psfm_augment_last_error
         elif what.startswith(("psfm_pose_from_vec", "psfm_pinhole_cam_records")):
             err = lib().psfm_pose_last_error

@@ -566,6 +566,48 @@ __global__ void __launch_bounds__(NT) k_jitter(Geo g, const int32_t* __restrict_
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// ResidentLoader batch gather (datasets/synthetic.py; the training-sample batch of one step from
+// the HBM-resident dataset): every image store of a batch in ONE launch, written in both layouts the
+// step consumes (NCHW for the loss kernels, channels_last for the nets), plus the intrinsics rows —
+// instead of an index_select (+ layout copy) per tensor.  Thread = 4 pixels of one (store, image):
+// 3 float4 plane loads, 3 float4 NCHW stores, 3 float4 NHWC stores (4 pixels x 3 channels).
+// ------------------------------------------------------------------------------------------
+struct GatherArgs {
+    const float* src[PSFM_GATHER_MAX];
+    float* nchw[PSFM_GATHER_MAX];
+    float* nhwc[PSFM_GATHER_MAX];
+    const int64_t* idx;
+    const float* intr_src;
+    float* intr_dst;
+    int ntensor, B, cams, HW, q;  // q = HW / 4 pixel quads per image
+};
+
+__global__ __launch_bounds__(256) void k_gather_frames(GatherArgs a) {
+    const int t = blockIdx.y, b = blockIdx.z;
+    const int quad = blockIdx.x * blockDim.x + threadIdx.x;
+    // row of image b: sample idx[b / cams], camera b % cams (flatten_cameras order)
+    const int64_t row = a.idx[b / a.cams] * a.cams + (b % a.cams);
+    if (t == 0 && blockIdx.x == 0 && a.intr_dst && threadIdx.x < 9)
+        a.intr_dst[(size_t)b * 9 + threadIdx.x] = a.intr_src[(size_t)row * 9 + threadIdx.x];
+    if (quad >= a.q) return;
+    const float* s = a.src[t] + (size_t)row * 3 * a.HW + (size_t)quad * 4;
+    float4 v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = *reinterpret_cast<const float4*>(s + (size_t)c * a.HW);
+    if (a.nchw[t]) {
+        float* d = a.nchw[t] + (size_t)b * 3 * a.HW + (size_t)quad * 4;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) *reinterpret_cast<float4*>(d + (size_t)c * a.HW) = v[c];
+    }
+    if (a.nhwc[t]) {
+        float4* d = reinterpret_cast<float4*>(a.nhwc[t] + ((size_t)b * a.HW + (size_t)quad * 4) * 3);
+        d[0] = make_float4(v[0].x, v[1].x, v[2].x, v[0].y);
+        d[1] = make_float4(v[1].y, v[2].y, v[0].z, v[1].z);
+        d[2] = make_float4(v[2].z, v[0].w, v[1].w, v[2].w);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -646,6 +688,28 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail((int)e, std::string("launch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int psfm_gather_frames(int ntensor, const float* const* src, float* const* dst_nchw, float* const* dst_nhwc,
+                       const int64_t* idx, int B, int cams, int HW, const float* intr_src, float* intr_dst,
+                       void* stream) {
+    if (ntensor < 1 || ntensor > PSFM_GATHER_MAX || !src || !dst_nchw || !dst_nhwc || !idx || B < 1 || cams < 1 ||
+        HW < 4 || HW % 4 || (!intr_src) != (!intr_dst))
+        return fail(-1, "gather_frames: bad arguments (1..PSFM_GATHER_MAX stores, HW a multiple of 4)");
+    GatherArgs a{};
+    for (int t = 0; t < ntensor; ++t) {
+        if (!src[t] || (!dst_nchw[t] && !dst_nhwc[t])) return fail(-1, "gather_frames: null store / destination");
+        const uintptr_t al = (uintptr_t)src[t] | (uintptr_t)dst_nchw[t] | (uintptr_t)dst_nhwc[t];
+        if (al & 15) return fail(-2, "gather_frames: 16-byte aligned buffers required");
+        a.src[t] = src[t], a.nchw[t] = dst_nchw[t], a.nhwc[t] = dst_nhwc[t];
+    }
+    a.idx = idx, a.intr_src = intr_src, a.intr_dst = intr_dst;
+    a.ntensor = ntensor, a.B = B, a.cams = cams, a.HW = HW, a.q = HW / 4;
+    const dim3 grid((a.q + 255) / 256, ntensor, B * cams);   // one z per image of the batch
+    hipLaunchKernelGGL(k_gather_frames, grid, dim3(256), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
     return 0;
 }
 

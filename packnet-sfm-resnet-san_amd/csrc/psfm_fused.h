@@ -101,6 +101,12 @@ struct Args {
     psfm_inputs in;
     psfm_workspace ws;
     float* grad_sig[PSFM_MAX_SCALES];
+    // Wave-pair balance (psfm_photometric.hip k12_priority): the workgroups of an XCD are dealt
+    // round-robin to its SIMDs, so in a one-round launch the in-XCD index i = L >> 3 >= young_from
+    // (= the XCD's SIMD count) marks the SECOND wave on its SIMD, which loses every VALU
+    // arbitration tie to the older one by age.  prio_mode 1: the younger wave runs one priority
+    // level higher in every phase; 2: in the p-eval only; 0: off.
+    int young_from, prio_mode;
 };
 
 __device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }   // both halves (op_sel broadcast)
@@ -341,6 +347,19 @@ struct K12 {
     float* gt;   // this lane's dL/dT accumulators: gt[2 m + j] (entry m, context j), 16-B aligned
     const float* camrec;   // record of (s, context 0, b); context j is j*B records further
     const float* campair;  // context-paired record of (s, b) (ws.cam_pairs)
+    bool young;            // the second wave dispatched to its SIMD (Args::young_from), wave-uniform
+    int prio_mode;
+
+    // phase priorities: 2 (issue / q-eval / resolve) and 0 (p-eval), the younger wave of a SIMD
+    // pair one level up per Args::prio_mode
+    __device__ __forceinline__ void prio_hi() const {
+        if (young && prio_mode == 1) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(2);
+    }
+    __device__ __forceinline__ void prio_lo() const {
+        if (young) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
 
     // Camera scalars are re-loaded at each use (s_load through the constant address space:
     // scalar cache, no VGPRs) instead of being held in SGPRs for the whole sweep; the laundered
@@ -372,6 +391,11 @@ struct K12 {
         s = wi.s;
         unit = wi.unit;
         lane = threadIdx.x;
+        prio_mode = a_.prio_mode;
+        {
+            const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+            young = prio_mode != 0 && (L >> 3) >= a_.young_from;
+        }
         y0 = (unit / nst) * RB;
         const int c0 = (unit % nst) * OW;
         col = c0 - 2 + lane;
@@ -472,7 +496,7 @@ struct K12 {
         // LDS read-modify-write chain), the resolve and the next issue (its gathers go out first) —
         // runs at priority 2, the p-eval at 0, so the other wave's p-eval fills the latency
         // (kbench B=4 104.7-105.8 -> 98.4 us, B=6 146-147 -> 138 us; profiles/r03/k12ab)
-        __builtin_amdgcn_s_setprio(2);
+        prio_hi();
         if (LOAD) {
             const float sg = S.sg_next;
             S.sg_next = load_sig(v + 1);
@@ -500,11 +524,11 @@ struct K12 {
                 }
             }
         }
-        __builtin_amdgcn_s_setprio(0);
+        prio_lo();
         PSFM_PHASE();
         if (PEVAL) peval<IA, IB, IC>(S, v - 2);
         PSFM_PHASE();
-        __builtin_amdgcn_s_setprio(2);
+        prio_hi();
         if (QEVAL) qeval<IA>(S, v - 3, k);
         PSFM_PHASE();
         if (PEVAL) {  // rotate the carried per-row terms

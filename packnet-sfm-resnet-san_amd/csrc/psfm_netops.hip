@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/psfm_netops.h"
@@ -1020,6 +1021,419 @@ __global__ __launch_bounds__(NT) void k_gn_bwd_apply(GNArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// One-pass ("resident") GroupNorm for the layers whose (sample, channel block) fits the registers
+// of one workgroup — every PackNet / PoseNet layer below 96x320 (layers01.py:10-72, PoseNet.py:15-19):
+// a workgroup owns sample n and CB consecutive channels = gpw whole groups (CB = cpg, or 8 channels
+// = 8 / cpg groups when cpg < 8, so every pixel run is one or more 16-byte vectors), holds its
+// RPT row vectors per thread in registers, reduces the group statistics in-workgroup (fixed-order
+// wave butterflies, then fp64 over the waves) and applies them from the registers:
+//   forward  ONE launch (read x [+ res] once, write y)        instead of stats + apply (2 reads);
+//   backward ONE data launch (read dy, x [+ res] once, write dx [+ dres]) + a one-workgroup
+//            parameter finish (per-(sample, channel) partial rows -> dgamma, dbeta, dbias),
+//            instead of stats + apply (2 reads of dy and x).
+// Same arithmetic as the two-pass kernels (fp32 per thread, fp64 totals; the conv-bias gradient
+// in the closed form sum_hw dx = k1 S1 - HW k2 - k3 X per sample, fp64); deterministic.
+// ------------------------------------------------------------------------------------------
+constexpr int RNT = 256;  // threads per workgroup
+
+struct GNRArgs {
+    const uint16_t* x;
+    const uint16_t* res;
+    const void* bias;
+    const uint16_t* dy;
+    const float* gamma;
+    const float* beta;
+    float* save_mean;
+    float* save_invstd;
+    uint16_t* out;
+    uint16_t* out2;
+    float* part;      // backward: [N][3][C] per-sample S1 | S2 | conv-bias partials
+    void* dbias;
+    float* dgamma;
+    float* dbeta;
+    float eps;
+    int N, HW, C, NG, act, bias_bf16;
+    int cpg, CB, CV, gpw, nblk;  // channels per group / per workgroup, 16-byte columns, groups per workgroup,
+                                 // workgroups per sample
+};
+
+// sum over the lanes of this wave that share t % CV (CV = 1, 2, 4): xor butterflies CV..32, fixed order
+template <int K>
+__device__ __forceinline__ void wave_colsum(float (&v)[K], int CV) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        if (off < CV) break;
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], off, 64);
+    }
+}
+
+// per-channel totals of K per-thread accumulators [K][8] over the workgroup -> tot[k * CB + c] (fp64)
+// red: LDS [waves][CV][K*8] floats
+template <int K>
+__device__ __forceinline__ void wg_chan_totals(float (&acc)[K * 8], float* red, double* tot, int CV, int CB) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+    wave_colsum<K * 8>(acc, CV);
+    if (lane < CV) {
+#pragma unroll
+        for (int k = 0; k < K * 8; ++k) red[(w * CV + lane) * (K * 8) + k] = acc[k];
+    }
+    __syncthreads();
+    for (int j = t; j < K * CB; j += blockDim.x) {
+        const int k = j / CB, c = j - k * CB, cv = c >> 3, i = c & 7;
+        double s = 0.0;
+        for (int ww = 0; ww < nw; ++ww) s += (double)red[(ww * CV + cv) * (K * 8) + k * 8 + i];
+        tot[j] = s;
+    }
+    __syncthreads();
+}
+
+// the held row vectors become opaque across the reduction: the apply pass re-unpacks them from the
+// packed bf16 registers instead of the compiler keeping every unpacked fp32 value live (2x VGPRs)
+__device__ __forceinline__ void opaque4(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+template <int RPT, bool RES>
+__global__ __launch_bounds__(RNT) void k_gnr_fwd(GNRArgs a) {
+    __shared__ float red[(RNT / 64) * 4 * 16];
+    __shared__ double tot[2 * 32];
+    __shared__ float gsc[32], gsh[32];
+    const int t = threadIdx.x, cv = t % a.CV, r = t / a.CV, RL = blockDim.x / a.CV;
+    const int n = blockIdx.x / a.nblk, blk = blockIdx.x - n * a.nblk;
+    const int c0 = blk * a.CB + cv * 8;  // this thread's 8 channels
+    const size_t so = (size_t)n * a.HW * a.C;
+    uint4 xv[RPT], rv[RES ? RPT : 1];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = r + k * RL;
+        const size_t o = so + (size_t)min(row, a.HW - 1) * a.C + c0;
+        xv[k] = *reinterpret_cast<const uint4*>(a.x + o);
+        if constexpr (RES) rv[k] = *reinterpret_cast<const uint4*>(a.res + o);
+    }
+    const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        if (r + k * RL >= a.HW) break;
+        const uint32_t w4[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w4[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+        if constexpr (RES) {
+            const uint32_t q4[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v[2 * i] += __uint_as_float(q4[i] << 16);
+                v[2 * i + 1] += __uint_as_float(q4[i] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float u = v[i] + b.v[i];
+            acc[i] += u;
+            acc[8 + i] += u * u;
+        }
+    }
+    wg_chan_totals<2>(acc, red, tot, a.CV, a.CB);
+    if (t < a.gpw) {  // group statistics (fp64, channel order)
+        const int g = blk * a.gpw + t;
+        double s1 = 0.0, s2 = 0.0;
+        for (int u = 0; u < a.cpg; ++u) {
+            s1 += tot[t * a.cpg + u];
+            s2 += tot[a.CB + t * a.cpg + u];
+        }
+        const double inv_cnt = 1.0 / ((double)a.HW * a.cpg);
+        const double mean = s1 * inv_cnt;
+        const double var = fmax(s2 * inv_cnt - mean * mean, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        gsc[t] = (float)mean;
+        gsh[t] = invstd;
+        a.save_mean[n * a.NG + g] = (float)mean;
+        a.save_invstd[n * a.NG + g] = invstd;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        opaque4(xv[k]);
+        if constexpr (RES) opaque4(rv[k]);
+    }
+    float sc[8], sh[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int gl = (cv * 8 + i) / a.cpg;  // group within the block
+        sc[i] = a.gamma[c0 + i] * gsh[gl];
+        sh[i] = a.beta[c0 + i] - gsc[gl] * sc[i];
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = r + k * RL;
+        if (row >= a.HW) break;
+        const uint32_t w4[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        Vec<8> v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v.v[2 * i] = __uint_as_float(w4[i] << 16);
+            v.v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+        if constexpr (RES) {
+            const uint32_t q4[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v.v[2 * i] += __uint_as_float(q4[i] << 16);
+                v.v[2 * i + 1] += __uint_as_float(q4[i] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v.v[i] = gn_act_f((v.v[i] + b.v[i]) * sc[i] + sh[i], a.act);
+        st_bf<8>(a.out + so + (size_t)row * a.C + c0, v);
+    }
+}
+
+template <int RPT, bool RES>
+__global__ __launch_bounds__(RNT) void k_gnr_bwd(GNRArgs a) {
+    __shared__ float red[(RNT / 64) * 4 * 24];
+    __shared__ double tot[3 * 32];
+    __shared__ float gk2[32], gk3[32];
+    const int t = threadIdx.x, cv = t % a.CV, r = t / a.CV, RL = blockDim.x / a.CV;
+    const int n = blockIdx.x / a.nblk, blk = blockIdx.x - n * a.nblk;
+    const int c0 = blk * a.CB + cv * 8;
+    const size_t so = (size_t)n * a.HW * a.C;
+    uint4 gv[RPT], xv[RPT], rv[RES ? RPT : 1];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = r + k * RL;
+        const size_t o = so + (size_t)min(row, a.HW - 1) * a.C + c0;
+        gv[k] = *reinterpret_cast<const uint4*>(a.dy + o);
+        xv[k] = *reinterpret_cast<const uint4*>(a.x + o);
+        if constexpr (RES) rv[k] = *reinterpret_cast<const uint4*>(a.res + o);
+    }
+    const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+    float mu[8], is[8], ga[8], be[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int g = (c0 + i) / a.cpg;
+        mu[i] = a.save_mean[n * a.NG + g];
+        is[i] = a.save_invstd[n * a.NG + g];
+        ga[i] = a.gamma[c0 + i];
+        be[i] = a.beta[c0 + i];
+    }
+    // xhat and the activation-masked gradient of one row vector
+    auto row_vals = [&](int k, float (&xh)[8], float (&gg)[8]) {
+        const uint32_t w4[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+        const uint32_t d4[4] = {gv[k].x, gv[k].y, gv[k].z, gv[k].w};
+        float v[8], d[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w4[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+            d[2 * i] = __uint_as_float(d4[i] << 16);
+            d[2 * i + 1] = __uint_as_float(d4[i] & 0xffff0000u);
+        }
+        if constexpr (RES) {
+            const uint32_t q4[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v[2 * i] += __uint_as_float(q4[i] << 16);
+                v[2 * i + 1] += __uint_as_float(q4[i] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            xh[i] = (v[i] + b.v[i] - mu[i]) * is[i];
+            gg[i] = gn_act_g(d[i], xh[i] * ga[i] + be[i], a.act);
+        }
+    };
+    float acc[24];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        if (r + k * RL >= a.HW) break;
+        float xh[8], gg[8];
+        row_vals(k, xh, gg);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            acc[i] += gg[i];
+            acc[8 + i] += gg[i] * xh[i];
+            acc[16 + i] += xh[i];
+        }
+    }
+    wg_chan_totals<3>(acc, red, tot, a.CV, a.CB);   // tot = [S1 | S2 | X][CB]
+    const double cnt = (double)a.HW * a.cpg;
+    if (t < a.gpw) {
+        const int g = blk * a.gpw + t;
+        double A = 0.0, Bq = 0.0;
+        for (int u = 0; u < a.cpg; ++u) {
+            const int c = t * a.cpg + u;
+            const double gc = a.gamma[blk * a.CB + c];
+            A += gc * tot[c];
+            Bq += gc * tot[a.CB + c];
+        }
+        const double isg = a.save_invstd[n * a.NG + g];
+        gk2[t] = (float)(A / cnt * isg);
+        gk3[t] = (float)(Bq / cnt * isg);
+    }
+    __syncthreads();
+    // per-(sample, channel) partial rows of the parameter gradients (the closed-form conv-bias term
+    // with the same fp32 k2 / k3 the dx below uses)
+    for (int c = t; c < a.CB; c += blockDim.x) {
+        const int cg = blk * a.CB + c, gl = c / a.cpg;
+        const double isg = a.save_invstd[n * a.NG + cg / a.cpg], gc = a.gamma[cg];
+        float* pr = a.part + (size_t)n * 3 * a.C;
+        pr[cg] = (float)tot[c];
+        pr[a.C + cg] = (float)tot[a.CB + c];
+        pr[2 * a.C + cg] = (float)(gc * isg * tot[c] - (double)a.HW * (double)gk2[gl] -
+                                   (double)gk3[gl] * tot[2 * a.CB + c]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        opaque4(xv[k]);
+        opaque4(gv[k]);
+        if constexpr (RES) opaque4(rv[k]);
+    }
+    float k1[8], k2[8], k3[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int gl = (cv * 8 + i) / a.cpg;
+        k1[i] = ga[i] * is[i];
+        k2[i] = gk2[gl];
+        k3[i] = gk3[gl];
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = r + k * RL;
+        if (row >= a.HW) break;
+        float xh[8], gg[8];
+        row_vals(k, xh, gg);
+        Vec<8> d;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d.v[i] = k1[i] * gg[i] - k2[i] - xh[i] * k3[i];
+        st_bf<8>(a.out + so + (size_t)row * a.C + c0, d);
+        if (a.out2) st_bf<8>(a.out2 + so + (size_t)row * a.C + c0, d);
+    }
+}
+
+// parameter gradients from the per-sample rows: thread = channel, samples in order (fp64)
+__global__ __launch_bounds__(256) void k_gnr_params(GNRArgs a) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.C) return;
+    double s1 = 0.0, s2 = 0.0, sb = 0.0;
+    for (int n = 0; n < a.N; ++n) {
+        const float* pr = a.part + (size_t)n * 3 * a.C;
+        s1 += (double)pr[c];
+        s2 += (double)pr[a.C + c];
+        sb += (double)pr[2 * a.C + c];
+    }
+    a.dbeta[c] = (float)s1;
+    a.dgamma[c] = (float)s2;
+    if (a.dbias) {
+        if (a.bias_bf16)
+            static_cast<uint16_t*>(a.dbias)[c] = f2bf((float)sb);
+        else
+            static_cast<float*>(a.dbias)[c] = (float)sb;
+    }
+}
+
+// resident-path geometry: CB channels per workgroup (whole groups, a multiple of 8 with CV = CB / 8
+// in {1, 2, 4}), nthr threads, RPT row vectors per thread (a template value) — false when the layer
+// does not fit (cap = row vectors per thread the register budget allows)
+struct GNRGeo {
+    int CB, CV, gpw, nthr, rpt;
+};
+inline bool gnr_geometry(int HW, int C, int G, int cap, GNRGeo& g) {
+    if (C % G) return false;
+    const int cpg = C / G;
+    if (cpg >= 8) {
+        if (cpg % 8 || cpg > 32) return false;
+        g.CB = cpg, g.gpw = 1;
+    } else {
+        if (8 % cpg || G % (8 / cpg)) return false;
+        g.CB = 8, g.gpw = 8 / cpg;
+    }
+    if (C % g.CB || g.gpw > 32) return false;
+    g.CV = g.CB / 8;
+    // 256-thread workgroups only: in the PackNet step the 512 / 1024-thread forms were slower than
+    // the two-pass kernels (a whole-CU workgroup waits for a CU to drain beside the concurrent pose
+    // branch, and RPT row vectors per thread are one long latency chain; profiles/r04/gn)
+    static const int tmpl[] = {1, 2, 4};
+    const int nthr = 256, RL = nthr / g.CV;
+    const int need = (HW + RL - 1) / RL;
+    for (int r : tmpl) {
+        if (r > cap) break;
+        if (r >= need) {
+            g.nthr = nthr, g.rpt = r;
+            return true;
+        }
+    }
+    return false;
+}
+// row vectors per thread: <= 4 (the resident path only pays for small layers, see gnr_geometry);
+// backward with res 2 (RPT 4 + res spills: compiler resource report, -Rpass-analysis=kernel-resource-usage)
+inline int gnr_cap_fwd(bool res) { (void)res; return 4; }
+inline int gnr_cap_bwd(bool res) { return res ? 2 : 4; }
+
+// RPT instantiations: forward 1, 2, 4, backward 1, 2, 4 (res <= 2), see gnr_cap_*
+#define GNR_CASE(KERNEL, R, RES_, grid, nthr, st, a)                                   \
+    case R:                                                                          \
+        if (RES_) hipLaunchKernelGGL((KERNEL<R, true>), grid, dim3(nthr), 0, st, a);   \
+        else hipLaunchKernelGGL((KERNEL<R, false>), grid, dim3(nthr), 0, st, a);       \
+        break
+#define GNR_LAUNCH_FWD(RPT_, RES_, grid, nthr, st, a)                                  \
+    do {                                                                             \
+        switch (RPT_) {                                                              \
+            GNR_CASE(k_gnr_fwd, 1, RES_, grid, nthr, st, a);                         \
+            GNR_CASE(k_gnr_fwd, 2, RES_, grid, nthr, st, a);                         \
+            GNR_CASE(k_gnr_fwd, 4, RES_, grid, nthr, st, a);                         \
+        }                                                                            \
+    } while (0)
+#define GNR_LAUNCH_BWD(RPT_, RES_, grid, nthr, st, a)                                  \
+    do {                                                                             \
+        switch (RPT_) {                                                              \
+            GNR_CASE(k_gnr_bwd, 1, RES_, grid, nthr, st, a);                         \
+            GNR_CASE(k_gnr_bwd, 2, RES_, grid, nthr, st, a);                         \
+            default: hipLaunchKernelGGL((k_gnr_bwd<4, false>), grid, dim3(nthr), 0, st, a); break; \
+        }                                                                            \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// BasicBlock tail (resnet_encoder.py:61-98 -> torchvision BasicBlock: out = relu(bn2(conv2(.)) +
+// identity)) after MIOpen's BatchNorm: y = relu(a + b) in ONE pass (bf16 in, fp32 add, one rounding —
+// what autocast's bf16 add followed by relu produces: the add rounds to bf16 and relu keeps it), and
+// its backward dz = dy * (y > 0), written once and handed to both inputs.  16-byte vectors, one per
+// thread, a grid over the tensor (no row loops: these run at the launch floor).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_add_relu_fwd(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                       uint4* __restrict__ y, long long n8) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const Vec<8> va = ld_bf<8>(reinterpret_cast<const uint16_t*>(a + i));
+    const Vec<8> vb = ld_bf<8>(reinterpret_cast<const uint16_t*>(b + i));
+    Vec<8> o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = fmaxf(bfround(va.v[k] + vb.v[k]), 0.0f);
+    st_bf<8>(reinterpret_cast<uint16_t*>(y + i), o);
+}
+__global__ __launch_bounds__(256) void k_relu_mask_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ y,
+                                                        uint4* __restrict__ dz, long long n8) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const uint4 g = dy[i], v = y[i];
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, vw[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // ATen threshold_backward: dz = (y <= 0) ? 0 : dy (NaN passes)
+        const uint32_t lo = (__uint_as_float(vw[k] << 16) <= 0.0f) ? 0u : 0x0000ffffu;
+        const uint32_t hi = (__uint_as_float(vw[k] & 0xffff0000u) <= 0.0f) ? 0u : 0xffff0000u;
+        o[k] = gw[k] & (lo | hi);
+    }
+    dz[i] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <typename A>
 void set_geo(A& a, const Geo& g) {
     a.G = g.G;
@@ -1039,7 +1453,13 @@ inline int check_vec(int C, const char* what) {
 
 // GN geometry: the grid stays <= TARGET_BLOCKS workgroups over the N samples
 inline Geo gn_geometry(int N, int HW, int C) {
-    return geometry(HW, C, pick_vec(C), std::max(1, TARGET_BLOCKS / N));
+    // PSFM_GN_BLOCKS (A/B): the two-pass grid target, TARGET_BLOCKS by default
+    static const int tb = [] {
+        const char* e = getenv("PSFM_GN_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : TARGET_BLOCKS;
+    }();
+    return geometry(HW, C, pick_vec(C), std::max(1, tb / N));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1263,7 +1683,28 @@ size_t psfm_netops_ws_floats(int M, int C) {   // partial rows [nblk][2C] + coef
 }
 
 size_t psfm_gn_ws_floats(int N, int HW, int C, int G) {
-    return gn_ws(N, gn_geometry(N, HW, C).nblk, C, G);
+    // two-pass statistics rows, or the resident backward's per-sample parameter rows [N][3][C]
+    return std::max(gn_ws(N, gn_geometry(N, HW, C).nblk, C, G), align4((size_t)3 * N * C));
+}
+
+int psfm_add_relu_fwd(const void* a, const void* b, long long n, void* y, void* stream) {
+    if (!a || !b || !y || n < 0 || n % 8 || (((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) & 15))
+        return fail(-1, "add_relu_fwd: n a multiple of 8, 16-byte aligned bf16 buffers");
+    const long long n8 = n / 8;
+    if (n8) hipLaunchKernelGGL(k_add_relu_fwd, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                               static_cast<const uint4*>(a), static_cast<const uint4*>(b), static_cast<uint4*>(y), n8);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, void* stream) {
+    if (!dy || !y || !dz || n < 0 || n % 8 || (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)dz) & 15))
+        return fail(-1, "relu_mask_bwd: n a multiple of 8, 16-byte aligned bf16 buffers");
+    const long long n8 = n / 8;
+    if (n8) hipLaunchKernelGGL(k_relu_mask_bwd, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                               static_cast<const uint4*>(dy), static_cast<const uint4*>(y), static_cast<uint4*>(dz), n8);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
 }
 
 int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y, void* stream) {
@@ -1376,6 +1817,18 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
     return 0;
 }
 
+// the resident path is the default; PSFM_GN_PATH=twopass forces the two-pass kernels (A/B, tests)
+static bool gnr_enabled() {
+    const char* e = getenv("PSFM_GN_PATH");
+    return !(e && std::string(e) == "twopass");
+}
+static void gnr_common(GNRArgs& r, const GNRGeo& rg, const GNArgs& a) {
+    r.x = a.x, r.res = a.res, r.bias = a.bias, r.bias_bf16 = a.bias_bf16, r.gamma = a.gamma, r.beta = a.beta;
+    r.save_mean = a.save_mean, r.save_invstd = a.save_invstd, r.out = a.out, r.eps = a.eps;
+    r.N = a.N, r.HW = a.HW, r.C = a.C, r.NG = a.NG, r.act = a.act;
+    r.cpg = a.C / a.NG, r.CB = rg.CB, r.CV = rg.CV, r.gpw = rg.gpw, r.nblk = a.C / rg.CB;
+}
+
 static int gn_setup(GNArgs& a, int N, int HW, int C, int G, Geo& g, int& vec) {
     if (N < 1 || HW < 1 || C < 1 || G < 1 || C % G != 0) return fail(-1, "groupnorm: bad shape");
     if (int e = check_vec(C, "groupnorm")) return e;
@@ -1404,6 +1857,15 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
     a.out = static_cast<uint16_t*>(y);
     a.ws = ws, a.act = act, a.RW = 2 * G;
     hipStream_t st = (hipStream_t)stream;
+    GNRGeo rg;
+    if (vec == 8 && gnr_enabled() && gnr_geometry(HW, C, G, gnr_cap_fwd(res != nullptr), rg)) {
+        GNRArgs r{};
+        gnr_common(r, rg, a);
+        const dim3 rgrid(N * r.nblk);
+        GNR_LAUNCH_FWD(rg.rpt, res != nullptr, rgrid, rg.nthr, st, r);
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
     const dim3 grid(N * g.nblk);
     if (vec == 8) {
         hipLaunchKernelGGL(k_gn_fwd_stats<8>, grid, dim3(NT), 0, st, a);
@@ -1437,6 +1899,17 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
     a.ws = ws, a.act = act, a.RW = gn_rw_bwd(C, G);
     a.dbias = dbias, a.dgamma = dgamma, a.dbeta = dbeta;
     hipStream_t st = (hipStream_t)stream;
+    GNRGeo rg;
+    if (vec == 8 && gnr_enabled() && gnr_geometry(HW, C, G, gnr_cap_bwd(res != nullptr), rg)) {
+        GNRArgs r{};
+        gnr_common(r, rg, a);
+        r.dy = a.dy, r.out2 = a.out2, r.part = ws, r.dbias = dbias, r.dgamma = dgamma, r.dbeta = dbeta;
+        const dim3 rgrid(N * r.nblk);
+        GNR_LAUNCH_BWD(rg.rpt, res != nullptr, rgrid, rg.nthr, st, r);
+        hipLaunchKernelGGL(k_gnr_params, dim3((C + 255) / 256), dim3(256), 0, st, r);
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
     const dim3 grid(N * g.nblk), grid_apply(N * g.nblk + (C + 3) / 4);
     if (vec == 8) {
         hipLaunchKernelGGL(k_gn_bwd_stats<8>, grid, dim3(NT), 0, st, a);

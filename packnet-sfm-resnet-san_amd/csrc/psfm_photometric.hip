@@ -19,11 +19,20 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "psfm_common.h"
 #include "psfm_sweep.h"
 #include "psfm_fused.h"
+
+#ifndef PSFM_K12_PRIO_DEFAULT
+// fused::Args::prio_mode when PSFM_K12_PRIO is unset: 2 = the younger wave of a SIMD pair one
+// level up in its p-eval (A/B on one box, profiles/r04/prio: kbench B=4 101.0 -> 98.0 us, B=6
+// 141.3 -> 135.4 us; in the step 95.6-97.3 -> 93.8-94.1 us); 1 (younger up everywhere) only swaps
+// which wave of the pair finishes last
+#define PSFM_K12_PRIO_DEFAULT 2
+#endif
 
 using namespace psfm;
 
@@ -1031,7 +1040,20 @@ bool fused_ok(const psfm_params* p) { return use_sweep(p) && p->N <= 2; }
 // wave running ~0.6 of a shared one.  Pick the candidate with the smallest steps x rounds on this
 // device's CU count (B = 4 at 192 x 640: RB 18 -> 1936 waves, one round; B = 6: RB 28 -> 1848
 // waves beat RB 18's 2904 = three waves on some SIMDs).
+int simd_count();
 int rb_for(const psfm_params* p) {
+    const int simds = simd_count();
+    auto cost = [&](int rb) {
+        const double waves = (double)fused::units(p->H, p->W, rb) * p->B * p->S;
+        const int n = (int)std::ceil(waves / simds);
+        return (double)(rb + 5) * ((n / 2) + ((n & 1) ? 0.6 : 0.0));
+    };
+    return cost(fused::RB_HI) < cost(fused::RB_LO) ? fused::RB_HI : fused::RB_LO;
+}
+// K12 wave-pair balance (fused::Args young_from / prio_mode): the XCD's SIMD count, and the mode
+// from PSFM_K12_PRIO (0 off, 1 younger +1 everywhere, 2 younger +1 in the p-eval; read per launch so
+// an A/B can switch it in one process); only meaningful when the launch fits one wave round
+int simd_count() {
     static int simds[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -1040,13 +1062,16 @@ int rb_for(const psfm_params* p) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
         simds[dev] = 4 * cus;
     }
-    auto cost = [&](int rb) {
-        const double waves = (double)fused::units(p->H, p->W, rb) * p->B * p->S;
-        const int n = (int)std::ceil(waves / simds[dev]);
-        return (double)(rb + 5) * ((n / 2) + ((n & 1) ? 0.6 : 0.0));
-    };
-    return cost(fused::RB_HI) < cost(fused::RB_LO) ? fused::RB_HI : fused::RB_LO;
+    return simds[dev];
 }
+void k12_priority(fused::Args& fa, long waves) {
+    const int simds = simd_count();
+    const char* e = getenv("PSFM_K12_PRIO");
+    fa.prio_mode = e ? atoi(e) : PSFM_K12_PRIO_DEFAULT;
+    fa.young_from = simds / 8;  // SIMDs per XCD (8 XCDs)
+    if (waves > 2L * simds || fa.prio_mode < 0 || fa.prio_mode > 2) fa.prio_mode = 0;
+}
+
 int fwd_units(const psfm_params* p) {
     if (p->grad_fused && fused_ok(p)) return fused::units(p->H, p->W, rb_for(p));
     return stats_units(p);
@@ -1411,6 +1436,7 @@ int psfm_photometric_fwd_grad(const psfm_params* p, const psfm_inputs* in, const
     const dim3 grid(fused::units(p->H, p->W, rb), p->B, p->S);
     const size_t lds = fused::lds_bytes(p->N);
     const bool fast = fast_cfg(p, in);
+    k12_priority(fa, (long)grid.x * grid.y * grid.z);
     if (rb == fused::RB_HI) launch_k12<fused::RB_HI>(p, fast, grid, lds, st, fa);
     else launch_k12<fused::RB_LO>(p, fast, grid, lds, st, fa);
     PSFM_LAUNCH_CHECK();

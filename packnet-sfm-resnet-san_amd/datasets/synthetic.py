@@ -18,6 +18,8 @@ same shapes and keys as `train_transforms` output (datasets/transforms.py:21-50)
     batch of this rank's sampler partition into caller-owned (e.g. HIP-graph static) tensors
     with `index_select` on device indices — no host sync, no PCIe in the timed loop.
 """
+import ctypes
+
 import torch
 import torch.nn.functional as F
 from torch.utils.data import DataLoader, Dataset
@@ -137,6 +139,51 @@ class ResidentLoader:
             return t.index_select(0, idx)
         return torch.index_select(t, 0, idx, out=out) if out.is_contiguous() else out.copy_(t.index_select(0, idx))
 
+    def _gather_hip(self, idx, dst):
+        """The whole batch in ONE HIP launch (include/psfm_augment.h psfm_gather_frames): every image
+        store into its NCHW (loss) and channels_last (nets) destinations, plus the intrinsics — the
+        index_select + layout-copy chain of `_sel` is ~10 launches per step.  False (the chain runs)
+        off the GPU or for layouts the kernel does not write."""
+        st = self.store
+        if self.device.type != "cuda" or "rgb_original" not in dst:
+            return False
+        keys = [("rgb", "rgb_original", st["rgb"])] + [
+            (("rgb_context", j), ("rgb_context_original", j), c) for j, c in enumerate(st["rgb_context"])]
+
+        def get(k):
+            return dst[k] if isinstance(k, str) else dst[k[0]][k[1]]
+
+        srcs, nchw, nhwc = [], [], []
+        for kn, ko, src in keys:
+            a, b = get(kn), get(ko)
+            pair = {"nchw": None, "nhwc": None}
+            for t in (a, b) if a is not b else (a,):
+                if t.dtype != torch.float32 or tuple(t.shape) != (self.B * self.cameras,) + tuple(src.shape[-3:]):
+                    return False
+                if t.is_contiguous():
+                    slot = "nchw"
+                elif t.is_contiguous(memory_format=torch.channels_last):
+                    slot = "nhwc"
+                else:
+                    return False
+                if pair[slot] is not None:
+                    return False
+                pair[slot] = t
+            srcs.append(src)
+            nchw.append(pair["nchw"])
+            nhwc.append(pair["nhwc"])
+        H, W = srcs[0].shape[-2:]
+        if (len(srcs) > 4 or (H * W) % 4 or srcs[0].shape[-3] != 3 or not all(s_.is_contiguous() for s_ in srcs)
+                or not dst["intrinsics"].is_contiguous() or not st["intrinsics"].is_contiguous()):
+            return False
+        from .. import _hip
+        P = ctypes.c_void_p * len(srcs)
+        _hip.check(_hip.lib().psfm_gather_frames(
+            len(srcs), P(*[s_.data_ptr() for s_ in srcs]), P(*[t.data_ptr() if t is not None else None for t in nchw]),
+            P(*[t.data_ptr() if t is not None else None for t in nhwc]), _hip.ptr(idx), self.B, self.cameras, H * W,
+            _hip.ptr(st["intrinsics"]), _hip.ptr(dst["intrinsics"]), _hip.stream(idx.device)), "psfm_gather_frames")
+        return True
+
     def next_into(self, dst=None):
         if self.step_in_epoch >= self.steps_per_epoch:
             self.epoch += 1
@@ -150,6 +197,8 @@ class ResidentLoader:
             ctx = [self._sel(c, idx, None) for c in st["rgb_context"]]
             return {"rgb": rgb, "rgb_context": ctx, "rgb_original": rgb, "rgb_context_original": ctx,
                     "intrinsics": self._sel(st["intrinsics"], idx, None)}
+        if self._gather_hip(idx, dst):
+            return dst
         self._sel(st["rgb"], idx, dst["rgb"])
         for j, c in enumerate(st["rgb_context"]):
             self._sel(c, idx, dst["rgb_context"][j])

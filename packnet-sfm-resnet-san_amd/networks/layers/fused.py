@@ -130,6 +130,47 @@ class _BNAct(torch.autograd.Function):
         return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None
 
 
+class _AddReLU(torch.autograd.Function):
+    """relu(a + b) on bf16 (include/psfm_netops.h psfm_add_relu_fwd / psfm_relu_mask_bwd): the
+    BasicBlock tail after MIOpen's BatchNorm, one pass each way instead of add + relu / the ReLU
+    backward (the add's backward is the identity to both inputs)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        y = torch.empty_like(a)
+        _hip.check(_hip.lib().psfm_add_relu_fwd(_hip.ptr(a), _hip.ptr(b), a.numel(), _hip.ptr(y),
+                                                _hip.stream(a.device)), "psfm_add_relu_fwd")
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=_fmt(y))
+        dz = torch.empty_like(y)
+        _hip.check(_hip.lib().psfm_relu_mask_bwd(_hip.ptr(dy), _hip.ptr(y), y.numel(), _hip.ptr(dz),
+                                                 _hip.stream(y.device)), "psfm_relu_mask_bwd")
+        return dz, dz
+
+
+def _fmt(t):
+    return torch.channels_last if (t.dim() == 4 and not t.is_contiguous()
+                                   and t.is_contiguous(memory_format=torch.channels_last)) else torch.contiguous_format
+
+
+ADD_RELU = True   # the BasicBlock tail on HIP (bench.py --no-add-relu: the op chain)
+
+
+def add_relu(a, b):
+    """relu(a + b): ONE HIP pass each way for bf16 tensors of the same shape and layout on a ROCm
+    device (the ResNet BasicBlock's `out += identity; relu(out)`); otherwise the op chain."""
+    if (ADD_RELU and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.shape == b.shape
+            and a.numel() % 8 == 0 and a.device == b.device and _fmt(a) == _fmt(b)
+            and a.is_contiguous(memory_format=_fmt(a)) and b.is_contiguous(memory_format=_fmt(b))):
+        return _AddReLU.apply(a, b)
+    return torch.relu(a + b)
+
+
 def bn_act(x, bn, relu=True, residual=None):
     """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn`."""
     if (_fusable(x, "bn") and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
@@ -140,6 +181,8 @@ def bn_act(x, bn, relu=True, residual=None):
                             float(bn.eps), bool(relu))
     y = bn(x)
     if residual is not None:
+        if relu and residual.dtype == y.dtype:
+            return add_relu(y, residual)
         y = y + residual
     return torch.relu(y) if relu else y
 
@@ -189,6 +232,16 @@ class _GNAct(torch.autograd.Function):
 
 
 ACT_ELU = 3  # PSFM_ACT_ELU (GroupNorm only)
+# limits of psfm_gn_act_* (psfm_netops.hip gn_setup): the parameter-gradient pass gives each sample
+# 64 / N lanes (N <= 64), the group totals of a sample fit one workgroup (G <= 128), C <= 512
+GN_MAX_N, GN_MAX_G, GN_MAX_C = 64, 128, 512
+
+
+def gn_shape_ok(shape, num_groups):
+    """The GroupNorm shapes the HIP kernels take; anything else runs the torch chain."""
+    N, C = shape[0], shape[1]
+    return (len(shape) == 4 and C % num_groups == 0 and N <= GN_MAX_N and num_groups <= GN_MAX_G
+            and C <= GN_MAX_C and (C % 8 == 0 or C <= 256))
 
 
 def gn_act(x, bias, gn, relu=True, act=None, residual=None):
@@ -196,7 +249,7 @@ def gn_act(x, bias, gn, relu=True, act=None, residual=None):
     ReLU (relu=True, PoseNet) / none, or `act=ACT_ELU` (PackNet Conv2D / ResidualConv).  `bias`
     may be None."""
     act = (ACT_RELU if relu else ACT_NONE) if act is None else act
-    if (_fusable(x, "gn") and gn.affine and x.shape[1] % gn.num_groups == 0
+    if (_fusable(x, "gn") and gn.affine and gn_shape_ok(tuple(x.shape), gn.num_groups)
             and (residual is None or (residual.shape == x.shape and residual.device == x.device))):
         return _GNAct.apply(x, residual, bias, gn.weight, gn.bias, int(gn.num_groups), float(gn.eps), act)
     if residual is not None:

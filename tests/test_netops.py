@@ -134,9 +134,28 @@ def test_bn_act_matches_torch(dev, shape, relu, residual):
         _close(r.grad, rr.grad, 2e-2, far)
 
 
+@pytest.fixture(params=["resident", "twopass"])
+def gn_path(request, monkeypatch):
+    """Both GroupNorm implementations: the one-pass resident kernels (default wherever the layer
+    fits a workgroup's registers) and the two-pass statistics-rows kernels (PSFM_GN_PATH=twopass;
+    always used for the large layers)."""
+    if request.param == "twopass":
+        monkeypatch.setenv("PSFM_GN_PATH", "twopass")
+    else:
+        monkeypatch.delenv("PSFM_GN_PATH", raising=False)
+    return request.param
+
+
+# GN shapes: two-pass (large HW), resident both ways at every row-vector count (RPT 1 / 2 / 4 of a
+# 256-thread workgroup) and channel block (cpg 1 / 2 / 4 -> 8-channel blocks of 8 / 4 / 2 groups,
+# cpg 16 / 32 -> 2 / 4 vector columns), resident forward + two-pass backward (res, RPT 4)
+GN_SHAPES = [(4, 16, 96, 320), (4, 64, 24, 80), (4, 256, 3, 10), (2, 32, 5, 7), (6, 16, 24, 80),
+             (6, 32, 12, 40), (6, 128, 48, 160), (6, 512, 12, 40), (6, 512, 6, 20), (3, 64, 60, 160)]
+
+
 @gpu
-@pytest.mark.parametrize("shape", [(4, 16, 96, 320), (4, 64, 24, 80), (4, 256, 3, 10), (2, 32, 5, 7)])
-def test_gn_act_matches_torch(dev, shape):
+@pytest.mark.parametrize("shape", GN_SHAPES)
+def test_gn_act_matches_torch(dev, shape, gn_path):
     g = torch.Generator(device="cpu").manual_seed(3)
     C = shape[1]
     conv_b = torch.randn(C, generator=g).to(dev, torch.bfloat16).requires_grad_(True)
@@ -223,6 +242,20 @@ def test_resnet_encoder_fused_matches_unfused(dev):
         assert ef <= 2.0 * ep + 2e-2, (k, ef, ep)
 
 
+def test_gn_shapes_outside_the_kernels_take_the_torch_chain():
+    """psfm_gn_act_* reject N > 64, G > 128, C > 512 (psfm_netops.hip gn_setup); gn_act must send those
+    shapes to the reference op chain instead of raising."""
+    assert FU.gn_shape_ok((64, 64, 8, 8), 16)
+    assert not FU.gn_shape_ok((65, 64, 8, 8), 16)
+    assert not FU.gn_shape_ok((2, 1024, 8, 8), 16)
+    assert not FU.gn_shape_ok((2, 256, 8, 8), 256)
+    assert not FU.gn_shape_ok((2, 60, 8, 8), 16)
+    torch.manual_seed(0)
+    gn = nn.GroupNorm(16, 32)
+    x, b = torch.randn(65, 32, 3, 4), torch.randn(32)
+    assert torch.equal(FU.gn_act(x, b, gn, True), torch.relu(gn(x + b.view(1, -1, 1, 1))))
+
+
 def test_cpu_path_is_the_reference_op_chain():
     """On CPU the helpers are exactly the reference's modules (BN -> +res -> ReLU etc.)."""
     torch.manual_seed(0)
@@ -268,8 +301,10 @@ def test_upcat_matches_torch(dev, N, C1, C2, h, w):
 
 @gpu
 @pytest.mark.parametrize("shape,residual,bias", [((6, 64, 96, 320), True, True), ((6, 32, 48, 160), False, True),
-                                                 ((2, 256, 12, 40), True, False), ((2, 32, 5, 7), False, True)])
-def test_gn_elu_matches_torch(dev, shape, residual, bias):
+                                                 ((2, 256, 12, 40), True, False), ((2, 32, 5, 7), False, True),
+                                                 ((6, 128, 48, 160), True, True), ((6, 256, 24, 80), True, True),
+                                                 ((6, 64, 24, 80), True, True), ((6, 512, 6, 20), False, True)])
+def test_gn_elu_matches_torch(dev, shape, residual, bias, gn_path):
     """PackNet Conv2D / ResidualConv epilogue: ELU(GroupNorm(16)(x [+ res] + bias)) and its backward
     (dx, dres, dbias, dgamma, dbeta) against the fp32 torch chain (layers01.py:10-61)."""
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -391,3 +426,33 @@ def test_conv_block_up_cat_equals_the_unfused_chain(dev, N, C1, C2, h, w, bias_b
     assert (dsf is None and dsu is None) or torch.equal(dsf, dsu)
     assert dbf.dtype == b.dtype
     assert (dbf.float() - dbu.float()).abs().max() <= 1e-6 * dbu.float().abs().max() + (2 ** -8 if bias_bf16 else 0) * dbu.float().abs().max()
+
+
+@gpu
+@pytest.mark.parametrize("shape,cl", [((4, 64, 48, 160), True), ((4, 512, 6, 20), True), ((2, 8, 3, 5), False)])
+def test_add_relu_equals_the_op_chain_bitwise(dev, shape, cl):
+    """The BasicBlock tail relu(bn_out + identity) (psfm_add_relu_fwd / psfm_relu_mask_bwd) equals
+    autocast's bf16 add + relu and their backward bit for bit (incl. zeros, -0, inf and NaN outputs)."""
+    g = torch.Generator(device="cpu").manual_seed(8)
+    mk = lambda: torch.randn(shape, generator=g).to(dev, torch.bfloat16)  # noqa: E731
+    a, b = mk(), mk()
+    a.view(-1)[:4] = torch.tensor([0.0, -0.0, float("inf"), float("nan")], dtype=torch.bfloat16)
+    b.view(-1)[:4] = torch.tensor([0.0, 0.0, 1.0, 1.0], dtype=torch.bfloat16)
+    if cl:
+        a, b = _cl(a), _cl(b)
+    a1, b1 = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    a2, b2 = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    calls = []
+    orig = FU._AddReLU.apply
+    FU._AddReLU.apply = lambda *x: calls.append(1) or orig(*x)
+    try:
+        y1 = FU.add_relu(a1, b1)
+    finally:
+        FU._AddReLU.apply = orig
+    y2 = torch.relu(a2 + b2)
+    assert calls and torch.equal(y1.nan_to_num(), y2.nan_to_num()) and y1.stride() == y2.stride()
+    dy = mk()
+    dy = _cl(dy) if cl else dy
+    y1.backward(dy)
+    y2.backward(dy)
+    assert torch.equal(a1.grad, a2.grad) and torch.equal(b1.grad, b2.grad)

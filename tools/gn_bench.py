@@ -27,6 +27,11 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--lib", default=None)
 ap.add_argument("--net", default="depth", choices=["depth", "pose"], help="record the depth or the pose net's GN calls")
 ap.add_argument("--eager", action="store_true", help="time eager calls (default: HIP-graph replays of --iters calls)")
+# capture-crash bisection (tools/diag_gn_capture.py): drop one step of the sequence
+ap.add_argument("--max-shapes", type=int, default=0, help="stop after this many shapes (0: all)")
+ap.add_argument("--no-live-grad", action="store_true", help="no grad-enabled call kept alive before the timing")
+ap.add_argument("--no-events", action="store_true", help="create the timing events after the capture")
+ap.add_argument("--fwd-only", action="store_true", help="time the forward only")
 args = ap.parse_args()
 import __graft_entry__  # noqa: E402
 
@@ -84,7 +89,8 @@ def timed(fn):
             fn()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if not args.no_events:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if args.eager:
         e0.record()
         for _ in range(args.iters):
@@ -96,6 +102,8 @@ def timed(fn):
             for _ in range(args.iters):
                 fn()
         g.replay()
+        if args.no_events:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         g.replay()
         e1.record()
@@ -104,19 +112,23 @@ def timed(fn):
 
 
 tot = collections.Counter()
-for (shape, has_res, has_bias, ng, act), n in calls.items():
+for ishape, ((shape, has_res, has_bias, ng, act), n) in enumerate(calls.items()):
+    if args.max_shapes and ishape >= args.max_shapes:
+        break
     shape = (args.batch,) + shape[1:]
     N, C, H, W = shape
     gn = torch.nn.GroupNorm(ng, C).to(dev)
     x = torch.randn(shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     r = torch.randn_like(x) if has_res else None
     bias = torch.randn(C, device=dev) if has_bias else None
-    xg = x.detach().requires_grad_(True)
-    y = orig(xg, bias, gn, act=act, residual=r)
-    dy = torch.randn_like(y)
+    if not args.no_live_grad:
+        xg = x.detach().requires_grad_(True)
+        y = orig(xg, bias, gn, act=act, residual=r)
+        dy = torch.randn_like(y)
     with torch.no_grad():   # the forward-only call (eval), as a training step's forward costs the same
         fwd_us = timed(lambda: orig(x, bias, gn, act=act, residual=r))
-    bwd_us = timed(lambda: torch.autograd.grad(y, xg, dy, retain_graph=True))
+    bwd_us = 0.0 if (args.fwd_only or args.no_live_grad) else \
+        timed(lambda: torch.autograd.grad(y, xg, dy, retain_graph=True))
     el = x.numel()
     rr = 1 if has_res else 0
     fb, bb = (3 + 2 * rr) * 2 * el, (5 + 3 * rr) * 2 * el

@@ -21,6 +21,8 @@ ap.add_argument("--B", type=int, default=4)
 ap.add_argument("--H", type=int, default=192)
 ap.add_argument("--W", type=int, default=640)
 ap.add_argument("--paths", default="k12,k1k2")
+ap.add_argument("--prio", default="", help="comma list of PSFM_K12_PRIO modes to run (K12 wave-pair balance)")
+ap.add_argument("--reps", type=int, default=1, help="repeat the whole lib x prio sweep (interleaved A/B)")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -41,10 +43,14 @@ fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_w
                               photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
                               min_depth=0.5, max_depth=80.0)
 results = {}
-for lib in (args.lib or [None]):
+runs = [(lib, pm) for _ in range(args.reps) for lib in (args.lib or [None])
+        for pm in (args.prio.split(",") if args.prio else [None])]
+for lib, pm in runs:
     if lib:
         _hip.LIB_PATH = lib
         _hip._lib = None
+    if pm is not None:
+        os.environ["PSFM_K12_PRIO"] = pm
     for fused in [p == "k12" for p in args.paths.split(",")]:
         HP.FUSED_GRAD = fused
         for _ in range(2):
@@ -57,6 +63,6 @@ for lib in (args.lib or [None]):
         res = {k: round(v, 2) for k, v in HP.graph_replay_times_us(rec, dev, reps=10, iters=args.iters).items()}
         res["total_us"] = round(sum(res.values()), 2)
         res["loss"] = float(out["loss"].detach())
-        tag = (lib or "default") + (" k12" if fused else " k1k2")
+        tag = (lib or "default") + (" k12" if fused else " k1k2") + (f" prio{pm}" if pm is not None else "")
         results[tag] = res
         print(tag, json.dumps(res), flush=True)
