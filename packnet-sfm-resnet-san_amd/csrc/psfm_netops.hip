@@ -1415,7 +1415,10 @@ __global__ __launch_bounds__(256) void k_add_relu_fwd(const uint4* __restrict__ 
     const Vec<8> vb = ld_bf<8>(reinterpret_cast<const uint16_t*>(b + i));
     Vec<8> o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o.v[k] = fmaxf(bfround(va.v[k] + vb.v[k]), 0.0f);
+    for (int k = 0; k < 8; ++k) {   // ATen relu: NaN propagates (fmaxf would drop it)
+        const float sum = bfround(va.v[k] + vb.v[k]);
+        o.v[k] = sum <= 0.0f ? 0.0f : sum;
+    }
     st_bf<8>(reinterpret_cast<uint16_t*>(y + i), o);
 }
 __global__ __launch_bounds__(256) void k_relu_mask_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ y,

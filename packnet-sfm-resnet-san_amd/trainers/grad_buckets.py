@@ -58,7 +58,7 @@ class GradBuckets:
             self.launch_order = sorted(range(len(self.buckets)), key=lambda b: first.get(b, len(order)))
         else:
             self.launch_order = list(range(len(self.buckets)))[::-1]
-        self.launch_order = self._agree(self.launch_order, device)
+        self.launch_order = self._agree(self.launch_order, device, self.ranges)
         self.stream = torch.cuda.Stream(device=device) if device.type == "cuda" else None
         self.armed = False
         self.capturing = False
@@ -66,18 +66,29 @@ class GradBuckets:
             self._plan_tables()
 
     @staticmethod
-    def _agree(order, device):
-        """Every rank must issue its bucket collectives in ONE order, or the all-reduces pair up
-        different buckets (a hang for different sizes, silently mixed slices for equal ones).
-        Rank 0's learned order is broadcast and adopted by all ranks (as torch DDP broadcasts its
-        rebuilt bucket order)."""
+    def _agree(order, device, ranges):
+        """Every rank must issue its bucket collectives in ONE order over the SAME bucket cuts, or the
+        all-reduces pair up different buckets (a hang for different sizes, silently mixed slices for
+        equal ones).  Rank 0's learned order is broadcast and adopted by all ranks (as torch DDP
+        broadcasts its rebuilt bucket order); rank 0's cuts (flat element ranges) are broadcast too
+        and every rank checks its own against them."""
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return order
         dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor(order, dtype=torch.int64, device=dev)
+        cuts = [v for r in ranges for v in r]
+        t = torch.tensor([len(order)] + list(order) + cuts, dtype=torch.int64, device=dev)
+        # plan sizes first (every rank learns a mismatch: all raise together, none waits in a collective)
+        n = torch.tensor([t.numel(), -t.numel()], dtype=torch.int64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        if int(n[0]) != -int(n[1]):
+            raise RuntimeError(f"ranks cut different buckets: plan sizes {-int(n[1])}..{int(n[0])} differ")
         dist.broadcast(t, src=0)
-        agreed = [int(v) for v in t.cpu()]
-        assert sorted(agreed) == sorted(order), "ranks cut different buckets"
+        got = [int(v) for v in t.cpu()]
+        agreed, cuts0 = got[1:1 + len(order)], got[1 + len(order):]
+        bad = torch.tensor([int(cuts0 != cuts or sorted(agreed) != sorted(order))], dtype=torch.int64, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if int(bad):
+            raise RuntimeError("ranks cut different buckets: a rank's flat ranges differ from rank 0's")
         return agreed
 
     # -------------------------------------------------------------------------------------------
@@ -184,7 +195,21 @@ class GradBuckets:
             self._pending = []
 
     def unpack(self, scale):
-        """Plain-optimizer path: averaged slices back into the parameters' .grad."""
-        for p, off in zip(self.params, self.offsets):
-            if p.grad is not None:
-                p.grad.copy_(self.flat[off:off + p.numel()].view_as(p.grad) * scale)
+        """Plain-optimizer path: averaged slices back into the parameters' .grad.  Whether a
+        parameter has a gradient is agreed across ranks first (one small all-reduce of a flag per
+        parameter): one that has a gradient on ANY rank gets the average on every rank (its slice
+        summed zeros where it had none), one with no gradient anywhere stays None everywhere (the
+        optimizer skips it, as for a single process).  Otherwise a rank whose gradient was None would
+        skip an update the other ranks apply, and the replicas would drift apart."""
+        has = torch.tensor([p.grad is not None for p in self.params], dtype=torch.int32)
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            has = has.to(self.device if dist.get_backend() == "nccl" else torch.device("cpu"))
+            dist.all_reduce(has, op=dist.ReduceOp.SUM)
+        for p, off, h in zip(self.params, self.offsets, has.tolist()):
+            if not h:
+                continue
+            avg = self.flat[off:off + p.numel()].view(p.shape) * scale
+            if p.grad is None:
+                p.grad = avg.to(p.dtype)
+            else:
+                p.grad.copy_(avg.view_as(p.grad))

@@ -350,3 +350,61 @@ def test_checkpoint_round_trips_through_load_network(tmp_path):
     load_network(fresh.pose_net, str(path), ["pose_net"])
     for k, v in model.state_dict().items():
         assert torch.equal(fresh.state_dict()[k], v), k
+
+
+def _half_none_worker(rank, world, init_file, out_dir):
+    """Rank 1 has NO gradient for parameter 1 this step, rank 0 has one: after the bucketed
+    all-reduce both ranks must hold the same averaged gradient for it (rank 1 used to keep
+    None and skip the update the other rank applied); parameter 3 has no gradient anywhere and stays
+    None on both ranks."""
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.grad_buckets import GradBuckets
+    ps = [torch.nn.Parameter(torch.zeros(10)) for _ in range(4)]
+    flat = torch.zeros(40)
+    gb = GradBuckets(ps, [0, 10, 20, 30], flat, 80, torch.device("cpu"))
+    gb.arm()
+    for i, p in enumerate(ps):
+        if i == 3 or (i == 1 and rank == 1):
+            continue
+        p.grad = torch.full((10,), float(rank + 1 + 10 * i))
+        gb.on_grad(p)
+    gb.finish()
+    gb.unpack(1.0 / world)
+    torch.save([None if p.grad is None else p.grad.clone() for p in ps], os.path.join(out_dir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_unpack_agrees_on_missing_gradients():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_half_none_worker, args=(world, os.path.join(d, "init"), d), nprocs=world, join=True)
+        g = [torch.load(os.path.join(d, f"g{r}.pt"), weights_only=True) for r in range(world)]
+    for i in range(3):
+        assert torch.equal(g[0][i], g[1][i]), i
+    assert torch.equal(g[0][1], torch.full((10,), (11.0 + 0.0) / 2))   # rank 0's 11, rank 1's zeros
+    assert g[0][3] is None and g[1][3] is None
+
+
+def _cut_worker(rank, world, init_file, out_dir):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import packnet_sfm_amd  # noqa: F401
+    from packnet_sfm_amd.trainers.grad_buckets import GradBuckets
+    ps = [torch.nn.Parameter(torch.zeros(10)) for _ in range(4)]
+    try:   # the ranks cut different buckets (different caps): both must refuse
+        GradBuckets(ps, [0, 10, 20, 30], torch.zeros(40), 80 if rank == 0 else 160, torch.device("cpu"))
+        msg = "no error"
+    except RuntimeError as e:
+        msg = str(e)
+    with open(os.path.join(out_dir, f"c{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.destroy_process_group()
+
+
+def test_mismatched_bucket_cuts_are_refused():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_cut_worker, args=(world, os.path.join(d, "init"), d), nprocs=world, join=True)
+        msgs = [open(os.path.join(d, f"c{r}.txt")).read() for r in range(world)]
+    assert all("ranks cut different buckets" in m for m in msgs), msgs

@@ -12,7 +12,11 @@ is the bench's path.
     bitwise identical fp32 master weights and bf16 model weights;
   * fp32 nets with deterministic MIOpen solvers: both ranks' weights equal, bit for bit, one
     process stepping torch Adam on the average of the two ranks' gradients of the same samples
-    (within 16 ulps of the optimizer replay's weights, step by step).
+    (within 16 ulps of the optimizer replay's weights, step by step);
+  * config 5's per-rank workload (configs/train_packnet_san_ddad.yaml): PackNetSAN01 + PoseNet, ONE
+    sample x 4 cameras per rank (flatten_cameras: the loss sees 4 images), bf16 + fused Adam — the
+    same identical-masters check (at 192 x 320 instead of 384 x 640 to keep the test short; the
+    full-size 4-camera step is pinned by test_networks.py against the oracle).
 """
 import os
 import tempfile
@@ -30,6 +34,17 @@ B, H, W, STEPS = 2, 64, 192, 3
 class _A:
     depth_net, pose_net, batch, height, width = "ResNetSAN01", "PoseNet", B, H, W
     min_depth, max_depth = 0.5, 80.0
+    cameras = 1
+
+
+class _DDAD:   # config 5 per rank: 1 sample x 4 cameras, PackNetSAN01 (max depth 200, DDAD yaml)
+    depth_net, pose_net, batch, height, width = "PackNetSAN01", "PoseNet", 1, 192, 320
+    min_depth, max_depth = 0.5, 200.0
+    cameras = 4
+
+
+def _cfg(mode):
+    return _DDAD if mode.startswith("ddad") else _A
 
 
 def _setup(mode):
@@ -38,7 +53,7 @@ def _setup(mode):
     torch.backends.cudnn.deterministic = mode == "fp32det"
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = bench.to_channels_last(bench.build_model(_A, dev))
+    model = bench.to_channels_last(bench.build_model(_cfg(mode), dev))
     return bench, dev, model
 
 
@@ -50,15 +65,18 @@ def _worker(rank, world, init_file, out_dir, mode):
     bench, dev, model = _setup(mode)
     from packnet_sfm_amd.datasets.synthetic import ResidentLoader, SyntheticSfmDataset, get_datasampler
     from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
-    bf16 = mode == "bf16"
+    bf16 = mode in ("bf16", "ddad_bf16")
+    A = _cfg(mode)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=bf16)
     tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16 if bf16 else None, graph=True,
                     bf16_weights=bf16, comm="split")
     assert tr.dp and tr.world == world and not tr.overlap
-    ds = SyntheticSfmDataset(4 * B * world, H, W, 2, 1, seed=0)
-    loader = ResidentLoader(ds, B, get_datasampler(ds, "train"), dev)
+    Bs = A.batch
+    ds = SyntheticSfmDataset(4 * Bs * world, A.height, A.width, 2, A.cameras, seed=0)
+    loader = ResidentLoader(ds, Bs, get_datasampler(ds, "train"), dev)
     batch = bench.net_layout(loader.next_into(None))
-    seen = [loader.partition[0:B]]
+    assert batch["rgb"].shape[0] == Bs * A.cameras
+    seen = [loader.partition[0:Bs]]
     # this rank's own packed gradient as it enters the all-reduce (host-enqueued between the two
     # graph replays) and the averaged buffer the optimizer graph read
     own, avg, real = [], [], dist.all_reduce
@@ -75,7 +93,7 @@ def _worker(rank, world, init_file, out_dir, mode):
             if i:
                 k = loader.step_in_epoch
                 loader.next_into(tr.static_batch)
-                seen.append(loader.partition[k * B:(k + 1) * B])
+                seen.append(loader.partition[k * Bs:(k + 1) * Bs])
             losses.append(float(tr.train_step(batch)["loss"]))
             torch.cuda.synchronize()
             avg.append(tr.flat_grad.detach().cpu().clone())
@@ -103,8 +121,9 @@ def _run(mode, world=2):
     return [torch.load(os.path.join(d, f"{mode}_r{r}.pt"), weights_only=True) for r in range(world)]
 
 
-def test_two_ranks_bf16_fused_split_path_keep_identical_masters():
-    r0, r1 = _run("bf16")
+@pytest.mark.parametrize("mode", ["bf16", "ddad_bf16"])
+def test_two_ranks_bf16_fused_split_path_keep_identical_masters(mode):
+    r0, r1 = _run(mode)
     # the sampler gave the ranks disjoint samples, so they computed different gradients ...
     assert not set(r0["seen"].flatten().tolist()) & set(r1["seen"].flatten().tolist())
     assert not torch.equal(r0["losses"], r1["losses"])

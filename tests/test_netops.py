@@ -456,3 +456,33 @@ def test_add_relu_equals_the_op_chain_bitwise(dev, shape, cl):
     y1.backward(dy)
     y2.backward(dy)
     assert torch.equal(a1.grad, a2.grad) and torch.equal(b1.grad, b2.grad)
+
+
+@gpu
+def test_gn_backward_captures_when_its_forward_ran_on_the_capture_stream(dev):
+    """tools/gn_bench.py's round-3 capture segfault, resolved (profiles/r04/cap): 20 captured
+    torch.autograd.grad calls through psfm_gn_act_bwd at [6, 64, 192, 640] replay bit-exactly when
+    the forward ran on the stream the graph captures on.  (With the forward on the default stream
+    the autograd engine launches the backward there, outside the capture, and HIP crashes in
+    capture_end: tools/diag_gn_capture.py --capture-bwd, a usage error the step graph never makes —
+    it captures forward and backward together.)"""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    shape, C = (6, 64, 192, 640), 64
+    gn = nn.GroupNorm(16, C).to(dev)
+    b = torch.randn(C, generator=g).to(dev)
+    x = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16).requires_grad_(True)
+    dy = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cs):
+        y = FU.gn_act(x, b, gn, act=FU.ACT_ELU)
+        ref = torch.autograd.grad(y, x, dy, retain_graph=True)[0].clone()
+    torch.cuda.current_stream().wait_stream(cs)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cs):
+        for _ in range(19):
+            torch.autograd.grad(y, x, dy, retain_graph=True)
+        out = torch.autograd.grad(y, x, dy, retain_graph=True)[0]
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

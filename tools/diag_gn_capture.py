@@ -16,6 +16,11 @@ tools/diag_capture_fwd.py passed.  Each flag adds one thing gn_bench does before
   --events       create two timing events before the capture (gn_bench.py:87) and record them
                  around a second replay
 
+  --capture-bwd  capture `torch.autograd.grad(y, xg, dy, retain_graph=True)` x iters instead of the
+                 forward (what gn_bench.py:119 — the crashing line — actually times); y from a forward
+                 run BEFORE the capture on the default stream, as gn_bench does
+  --bwd-on-capture-stream  with --capture-bwd: run that forward on the stream the graph then captures on
+
 One configuration per process (a segfault ends it); prints OK on a clean capture + replay."""
 import argparse
 import faulthandler
@@ -34,6 +39,9 @@ ap.add_argument("--no-bench", action="store_true")
 ap.add_argument("--side-warmup", action="store_true")
 ap.add_argument("--keep", action="store_true")
 ap.add_argument("--drop-all", action="store_true")
+ap.add_argument("--capture-bwd", action="store_true")
+ap.add_argument("--bwd-on-capture-stream", action="store_true")
+ap.add_argument("--torch-chain", action="store_true", help="with --capture-bwd: torch's own GroupNorm + ELU ops")
 ap.add_argument("--events", action="store_true")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--shape", default="6,64,192,640")
@@ -74,6 +82,33 @@ gn = torch.nn.GroupNorm(16, C).to(dev)
 x = torch.randn(shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 bias = torch.randn(C, device=dev)
 keep = None
+if args.capture_bwd:
+    if args.torch_chain:   # the reference op chain (autocast-style fp32 GN on the bf16 input)
+        orig = lambda x_, b_, gn_, act=None: torch.nn.functional.elu(gn_(x_.float() + b_.view(1, -1, 1, 1)))  # noqa: E731
+    cs = torch.cuda.Stream()
+    xg = x.detach().requires_grad_(True)
+    dy = torch.randn(shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if args.torch_chain:
+        dy = dy.float()
+    if args.bwd_on_capture_stream:
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            y = orig(xg, bias, gn, act=FU.ACT_ELU)
+        torch.cuda.current_stream().wait_stream(cs)
+    else:
+        y = orig(xg, bias, gn, act=FU.ACT_ELU)
+    ref = torch.autograd.grad(y, xg, dy, retain_graph=True)[0].clone()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cs):
+        for _ in range(args.iters - 1):
+            torch.autograd.grad(y, xg, dy, retain_graph=True)
+        out = torch.autograd.grad(y, xg, dy, retain_graph=True)[0]
+    g.replay()
+    torch.cuda.synchronize()
+    ok = torch.equal(out, ref)
+    print(f"OK backward capture + replay ({vars(args)}), dx equals eager: {ok}", flush=True)
+    sys.exit(0 if ok else 1)
 if args.live_grad:
     xg = x.detach().requires_grad_(True)
     y = orig(xg, bias, gn, act=FU.ACT_ELU)

@@ -77,12 +77,19 @@ with torch.no_grad():
 print(f"{sum(calls.values())} gn_act calls, {len(calls)} shapes", flush=True)
 
 
+# ONE stream for the recorded forwards, the warm-ups and the captures.  The round-3 segfault in
+# capture_end (profiles/r03/cap/gn_bench_graph_crash.log, line 119 = the BACKWARD timing) was the
+# backward of a forward that ran on the default stream, captured on torch.cuda.graph's own stream:
+# the autograd engine runs each backward op on its forward's stream, so those launches went to a
+# stream outside the capture (HIP then crashes at capture end instead of refusing the launch;
+# tools/diag_gn_capture.py --capture-bwd reproduces it, --bwd-on-capture-stream passes bit-exactly).
+cs = torch.cuda.Stream()
+
+
 def timed(fn):
     """Per-call GPU time: a HIP graph of args.iters calls replayed between two HIP events (no host
     launch gaps; --eager: back-to-back eager calls, an upper bound for small shapes)."""
-    # warm-up on a side stream, then capture (torch.cuda.graph's documented pattern: the warm-up
-    # calls on the default stream followed by a capture crashed in capture_end, r3 session 2)
-    s = torch.cuda.Stream()
+    s = cs
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         for _ in range(3):
@@ -98,7 +105,7 @@ def timed(fn):
         e1.record()
     else:
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=cs):
             for _ in range(args.iters):
                 fn()
         g.replay()
@@ -123,8 +130,11 @@ for ishape, ((shape, has_res, has_bias, ng, act), n) in enumerate(calls.items())
     bias = torch.randn(C, device=dev) if has_bias else None
     if not args.no_live_grad:
         xg = x.detach().requires_grad_(True)
-        y = orig(xg, bias, gn, act=act, residual=r)
-        dy = torch.randn_like(y)
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):   # the backward then runs (and is captured) on cs
+            y = orig(xg, bias, gn, act=act, residual=r)
+            dy = torch.randn_like(y)
+        torch.cuda.current_stream().wait_stream(cs)
     with torch.no_grad():   # the forward-only call (eval), as a training step's forward costs the same
         fwd_us = timed(lambda: orig(x, bias, gn, act=act, residual=r))
     bwd_us = 0.0 if (args.fwd_only or args.no_live_grad) else \
@@ -134,10 +144,9 @@ for ishape, ((shape, has_res, has_bias, ng, act), n) in enumerate(calls.items())
     fb, bb = (3 + 2 * rr) * 2 * el, (5 + 3 * rr) * 2 * el
     line = {"shape": shape, "res": has_res, "bias": has_bias, "calls_per_fwd": n,
             "fwd_us": round(fwd_us, 2), "fwd_frac": round(fb / (fwd_us * 1e-6) / 8e12, 3),
-            "bwd_us": round(bwd_us, 2), "bwd_frac": round(bb / (bwd_us * 1e-6) / 8e12, 3)}
+            "bwd_us": round(bwd_us, 2), "bwd_frac": round(bb / (bwd_us * 1e-6) / 8e12, 3) if bwd_us else None}
     tot["fwd_us"] += n * fwd_us
     tot["bwd_us"] += n * bwd_us
     tot["bytes"] += n * (fb + bb)
     print(json.dumps(line), flush=True)
-print(json.dumps({"total_fwd_us": round(tot["fwd_us"], 1), "total_bwd_us": round(tot["bwd_us"], 1),
-                  "total_frac": round(tot["bytes"] / ((tot["fwd_us"] + tot["bwd_us"]) * 1e-6) / 8e12, 3)}))
+print(json.dumps({"total_fwd_us": round(tot["fwd_us"], 1), "total_bwd_us": round(tot["bwd_us"], 1)}))
