@@ -1437,6 +1437,300 @@ __global__ __launch_bounds__(256) void k_relu_mask_bwd(const uint4* __restrict__
     dz[i] = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// ------------------------------------------------------------------------------------------
+// Two-pass GroupNorm, software-pipelined (VEC = 8): the large layers (PackNet 192x640 / 96x320) run
+// from HBM in the step, where one row step's loads then its arithmetic left each thread waiting a
+// full memory latency per step (2.1-2.8 TB/s in the step, profiles/r04/gn).  Here every thread keeps
+// the NEXT row step's loads in flight while it works on the current one (two register buffers,
+// raw 16-byte words: no conversion may sit between a load and the next step's compute).  The loads
+// are unconditional (rows clamped into the range, masked at use) and the trip count is uniform, so
+// no branch around a load makes the wait counts conservative.  Same arithmetic and order as
+// k_gn_*<8> (bitwise equal results).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ Vec<8> unpack8(const uint4 q) {
+    Vec<8> r;
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r.v[2 * i] = __uint_as_float(w[i] << 16);
+        r.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+    return r;
+}
+__device__ __forceinline__ uint4 ldq(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// x (+ res) of row step `it` of this thread: rows row0 + r + it*U*TR + u*TR, clamped to row1 - 1
+template <bool RES>
+struct RowsX {
+    uint4 x[U], q[RES ? U : 1];
+    __device__ __forceinline__ void load(const GNArgs& a, size_t so, int c0, int first, int TR, int row1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t o = so + (size_t)min(first + u * TR, row1 - 1) * a.C + c0;
+            x[u] = ldq(a.x + o);
+            if constexpr (RES) q[u] = ldq(a.res + o);
+        }
+    }
+    __device__ __forceinline__ Vec<8> val(int u) const {
+        Vec<8> v = unpack8(x[u]);
+        if constexpr (RES) {
+            const Vec<8> w = unpack8(q[u]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] += w.v[i];
+        }
+        return v;
+    }
+};
+template <bool RES>
+struct RowsGX : RowsX<RES> {
+    uint4 g[U];
+    __device__ __forceinline__ void load(const GNArgs& a, size_t so, int c0, int first, int TR, int row1) {
+        RowsX<RES>::load(a, so, c0, first, TR, row1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) g[u] = ldq(a.dy + so + (size_t)min(first + u * TR, row1 - 1) * a.C + c0);
+    }
+};
+
+// drive body(rows, first_row) over the row steps with the next step's loads in flight
+#define GNP_PIPELINE(ROWS_T, ROW0, ROW1, R, TR, SO, C0, BODY)                      \
+    do {                                                                       \
+        const int step_ = U * (TR);                                            \
+        const int niter_ = ((ROW1) - (ROW0) + step_ - 1) / step_;              \
+        ROWS_T A_, B_;                                                         \
+        if (niter_ > 0) A_.load(a, SO, C0, (ROW0) + (R), TR, ROW1);            \
+        for (int it_ = 0; it_ < niter_; it_ += 2) {                            \
+            B_.load(a, SO, C0, (ROW0) + (R) + (it_ + 1) * step_, TR, ROW1);    \
+            BODY(A_, (ROW0) + (R) + it_ * step_);                              \
+            if (it_ + 1 >= niter_) break;                                      \
+            A_.load(a, SO, C0, (ROW0) + (R) + (it_ + 2) * step_, TR, ROW1);    \
+            BODY(B_, (ROW0) + (R) + (it_ + 1) * step_);                        \
+        }                                                                      \
+    } while (0)
+
+template <bool RES>
+__global__ __launch_bounds__(NT) void k_gnp_fwd_stats(GNArgs a) {
+    __shared__ float red[2 * NT * 8];
+    __shared__ float chan[2 * MAX_C];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
+    float acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
+    if (r < a.TR) {
+        const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+        const size_t so = (size_t)n * a.HW * a.C;
+        const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
+#define GNP_FWD_STATS_BODY(RW, FIRST)                                          \
+        _Pragma("unroll") for (int u = 0; u < U; ++u) {                        \
+            const bool in = (FIRST) + u * a.TR < row1;                         \
+            const Vec<8> v = RW.val(u);                                        \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) {                    \
+                const float w = in ? v.v[i] + b.v[i] : 0.0f;                   \
+                acc[0][i] += w;                                                \
+                acc[1][i] += w * w;                                            \
+            }                                                                  \
+        }
+        GNP_PIPELINE(RowsX<RES>, row0, row1, r, a.TR, so, c0, GNP_FWD_STATS_BODY);
+#undef GNP_FWD_STATS_BODY
+    }
+    block_colsum<8, 2>(acc, red, a.G, a.TR);
+    chan_to_lds<8, 2>(acc, chan, a.C, c0, r);
+    const int cpg = a.C / a.NG;
+    float* row = a.ws + (size_t)blockIdx.x * a.RW;
+    for (int j = t; j < 2 * a.NG; j += NT) {
+        const int k = j / a.NG, g = j - k * a.NG;
+        float s = 0.0f;
+        for (int u = 0; u < cpg; ++u) s += chan[k * a.C + g * cpg + u];
+        row[j] = s;
+    }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(NT) void k_gnp_fwd_apply(GNArgs a) {
+    __shared__ double tot[2 * MAX_NG];
+    __shared__ double scr[NT];
+    __shared__ float gmean[MAX_NG], ginv[MAX_NG];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
+    const size_t so = (size_t)n * a.HW * a.C;
+    const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
+    const bool live = r < a.TR;
+    const int step = U * a.TR, niter = (row1 - row0 + step - 1) / step;
+    RowsX<RES> A, B;
+    // the first two row steps go out before the prologue (their latency overlaps the reduction)
+    if (live && niter > 0) A.load(a, so, c0, row0 + r, a.TR, row1);
+    if (live && niter > 0) B.load(a, so, c0, row0 + r + step, a.TR, row1);
+    group_totals(a.ws + (size_t)n * a.bpn * a.RW, a.bpn, a.RW, 2 * a.NG, tot, scr);
+    const int cpg = a.C / a.NG;
+    if (t < a.NG) {
+        const double inv_cnt = 1.0 / ((double)a.HW * cpg);
+        const double mean = tot[t] * inv_cnt;
+        const double var = fmax(tot[a.NG + t] * inv_cnt - mean * mean, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        gmean[t] = (float)mean;
+        ginv[t] = invstd;
+        if (bl == 0) {
+            a.save_mean[n * a.NG + t] = (float)mean;
+            a.save_invstd[n * a.NG + t] = invstd;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    Vec<8> sc, sh;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int g = (c0 + i) / cpg;
+        sc.v[i] = a.gamma[c0 + i] * ginv[g];
+        sh.v[i] = a.beta[c0 + i] - gmean[g] * sc.v[i];
+    }
+    const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+    auto body = [&](const RowsX<RES>& RW, int first) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = first + u * a.TR;
+            Vec<8> v = RW.val(u);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v.v[i] = gn_act_f((v.v[i] + b.v[i]) * sc.v[i] + sh.v[i], a.act);
+            if (row < row1) st_bf<8>(a.out + so + (size_t)row * a.C + c0, v);
+        }
+    };
+    for (int it = 0; it < niter; it += 2) {
+        body(A, row0 + r + it * step);
+        if (it + 1 >= niter) break;
+        A.load(a, so, c0, row0 + r + (it + 2) * step, a.TR, row1);
+        body(B, row0 + r + (it + 1) * step);
+        B.load(a, so, c0, row0 + r + (it + 3) * step, a.TR, row1);
+    }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(NT) void k_gnp_bwd_stats(GNArgs a) {
+    __shared__ float red[3 * NT * 8];
+    __shared__ float chan[3 * MAX_C];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
+    const int cpg = a.C / a.NG;
+    float acc[3][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = acc[2][i] = 0.0f;
+    if (r < a.TR) {
+        const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+        float mu[8], is[8], ga[8], be[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            mu[i] = a.save_mean[n * a.NG + (c0 + i) / cpg];
+            is[i] = a.save_invstd[n * a.NG + (c0 + i) / cpg];
+            ga[i] = a.gamma[c0 + i];
+            be[i] = a.beta[c0 + i];
+        }
+        const size_t so = (size_t)n * a.HW * a.C;
+        const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
+#define GNP_BWD_STATS_BODY(RW, FIRST)                                          \
+        _Pragma("unroll") for (int u = 0; u < U; ++u) {                        \
+            const bool in_u = (FIRST) + u * a.TR < row1;                       \
+            const Vec<8> x = RW.val(u), g = unpack8(RW.g[u]);                  \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) {                    \
+                const float gv = in_u ? g.v[i] : 0.0f, xv = in_u ? x.v[i] : 0.0f; \
+                const float xh = (xv + b.v[i] - mu[i]) * is[i];                \
+                const float gg = gn_act_g(gv, xh * ga[i] + be[i], a.act);      \
+                acc[0][i] += gg;                                               \
+                acc[1][i] += gg * xh;                                          \
+                acc[2][i] += in_u ? xh : 0.0f;                                 \
+            }                                                                  \
+        }
+        GNP_PIPELINE(RowsGX<RES>, row0, row1, r, a.TR, so, c0, GNP_BWD_STATS_BODY);
+#undef GNP_BWD_STATS_BODY
+    }
+    block_colsum<8, 3>(acc, red, a.G, a.TR);
+    chan_to_lds<8, 3>(acc, chan, a.C, c0, r);
+    float* row = a.ws + (size_t)blockIdx.x * a.RW;
+    for (int j = t; j < 2 * a.NG; j += NT) {
+        const int k = j / a.NG, g = j - k * a.NG;
+        float s = 0.0f;
+        for (int u = 0; u < cpg; ++u) s += a.gamma[g * cpg + u] * chan[k * a.C + g * cpg + u];
+        row[j] = s;
+    }
+    for (int j = t; j < 3 * a.C; j += NT) row[2 * a.NG + j] = chan[j];
+}
+
+template <bool RES>
+__global__ __launch_bounds__(NT) void k_gnp_bwd_apply(GNArgs a) {
+    if ((int)blockIdx.x >= a.N * a.bpn) {
+        gn_bwd_params(a, blockIdx.x - a.N * a.bpn);
+        return;
+    }
+    __shared__ double tot[2 * MAX_NG];
+    __shared__ double scr[NT];
+    __shared__ float gk2[MAX_NG], gk3[MAX_NG];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    const int n = blockIdx.x / a.bpn, bl = blockIdx.x % a.bpn;
+    const int cpg = a.C / a.NG;
+    const size_t so = (size_t)n * a.HW * a.C;
+    const int row0 = bl * a.rpb, row1 = min(a.HW, row0 + a.rpb);
+    const bool live = r < a.TR;
+    const int step = U * a.TR, niter = (row1 - row0 + step - 1) / step;
+    RowsGX<RES> A, B;
+    if (live && niter > 0) A.load(a, so, c0, row0 + r, a.TR, row1);
+    if (live && niter > 0) B.load(a, so, c0, row0 + r + step, a.TR, row1);
+    group_totals(a.ws + (size_t)n * a.bpn * a.RW, a.bpn, a.RW, 2 * a.NG, tot, scr);
+    if (t < a.NG) {
+        const double cnt = (double)a.HW * cpg;
+        const double is = a.save_invstd[n * a.NG + t];
+        gk2[t] = (float)(tot[t] / cnt * is);
+        gk3[t] = (float)(tot[a.NG + t] / cnt * is);
+    }
+    __syncthreads();
+    if (!live) return;
+    const Vec<8> b = a.bias ? ld_param<8>(a.bias, a.bias_bf16, c0) : zero<8>();
+    float mu[8], is[8], ga[8], be[8], k1[8], k2[8], k3[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int gi = (c0 + i) / cpg;
+        mu[i] = a.save_mean[n * a.NG + gi];
+        is[i] = a.save_invstd[n * a.NG + gi];
+        ga[i] = a.gamma[c0 + i];
+        be[i] = a.beta[c0 + i];
+        k1[i] = ga[i] * is[i];
+        k2[i] = gk2[gi];
+        k3[i] = gk3[gi];
+    }
+    auto body = [&](const RowsGX<RES>& RW, int first) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = first + u * a.TR;
+            const Vec<8> x = RW.val(u), g = unpack8(RW.g[u]);
+            Vec<8> d;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float xh = (x.v[i] + b.v[i] - mu[i]) * is[i];
+                const float gg = gn_act_g(g.v[i], xh * ga[i] + be[i], a.act);
+                d.v[i] = k1[i] * gg - k2[i] - xh * k3[i];
+            }
+            if (row < row1) {
+                st_bf<8>(a.out + so + (size_t)row * a.C + c0, d);
+                if (a.out2) st_bf<8>(a.out2 + so + (size_t)row * a.C + c0, d);
+            }
+        }
+    };
+    for (int it = 0; it < niter; it += 2) {
+        body(A, row0 + r + it * step);
+        if (it + 1 >= niter) break;
+        A.load(a, so, c0, row0 + r + (it + 2) * step, a.TR, row1);
+        body(B, row0 + r + (it + 1) * step);
+        B.load(a, so, c0, row0 + r + (it + 3) * step, a.TR, row1);
+    }
+}
+
+// PSFM_GN_PIPE=0 (A/B): the unpipelined two-pass kernels
+static bool gnp_enabled() {
+    const char* e = getenv("PSFM_GN_PIPE");
+    return !(e && e[0] == '0');
+}
+
 template <typename A>
 void set_geo(A& a, const Geo& g) {
     a.G = g.G;
@@ -1870,7 +2164,15 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
         return 0;
     }
     const dim3 grid(N * g.nblk);
-    if (vec == 8) {
+    if (vec == 8 && gnp_enabled()) {
+        if (res) {
+            hipLaunchKernelGGL(k_gnp_fwd_stats<true>, grid, dim3(NT), 0, st, a);
+            hipLaunchKernelGGL(k_gnp_fwd_apply<true>, grid, dim3(NT), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(k_gnp_fwd_stats<false>, grid, dim3(NT), 0, st, a);
+            hipLaunchKernelGGL(k_gnp_fwd_apply<false>, grid, dim3(NT), 0, st, a);
+        }
+    } else if (vec == 8) {
         hipLaunchKernelGGL(k_gn_fwd_stats<8>, grid, dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_gn_fwd_apply<8>, grid, dim3(NT), 0, st, a);
     } else {
@@ -1914,7 +2216,15 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
         return 0;
     }
     const dim3 grid(N * g.nblk), grid_apply(N * g.nblk + (C + 3) / 4);
-    if (vec == 8) {
+    if (vec == 8 && gnp_enabled()) {
+        if (res) {
+            hipLaunchKernelGGL(k_gnp_bwd_stats<true>, grid, dim3(NT), 0, st, a);
+            hipLaunchKernelGGL(k_gnp_bwd_apply<true>, grid_apply, dim3(NT), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(k_gnp_bwd_stats<false>, grid, dim3(NT), 0, st, a);
+            hipLaunchKernelGGL(k_gnp_bwd_apply<false>, grid_apply, dim3(NT), 0, st, a);
+        }
+    } else if (vec == 8) {
         hipLaunchKernelGGL(k_gn_bwd_stats<8>, grid, dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_gn_bwd_apply<8>, grid_apply, dim3(NT), 0, st, a);
     } else {

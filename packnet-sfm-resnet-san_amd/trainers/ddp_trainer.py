@@ -369,7 +369,9 @@ class DDPTrainer:
         {'config', 'epoch', 'state_dict', 'optimizer', 'scheduler'} with 'state_dict' keyed as
         ModelWrapper.state_dict() is — the SfmModel under 'model.' — so utils/load.py
         load_network(net, ckpt['state_dict'], 'depth_net') strips the prefix as for a reference
-        checkpoint.  Written with torch.save(), it loads with weights_only=True."""
+        checkpoint.  Written with torch.save(), it loads with weights_only=True when `config` is None
+        or a plain dict / list / scalar tree (a yacs CfgNode or another object would need the
+        unpickling loader; pass config as a dict)."""
         sd = {"model." + k: v.detach().cpu() for k, v in self.state_dict().items()}
         return {"config": config, "epoch": int(epoch), "state_dict": sd,
                 "optimizer": self.optimizer.state_dict(),

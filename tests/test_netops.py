@@ -486,3 +486,34 @@ def test_gn_backward_captures_when_its_forward_ran_on_the_capture_stream(dev):
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@gpu
+@pytest.mark.parametrize("residual", [False, True])
+def test_pipelined_two_pass_gn_is_bitwise_the_unpipelined_one(dev, monkeypatch, residual):
+    """The software-pipelined two-pass GroupNorm kernels (k_gnp_*, the default for 8-wide channel
+    vectors) keep the unpipelined kernels' arithmetic and order: every output and gradient bitwise
+    equal (PSFM_GN_PIPE=0 selects the unpipelined ones), at a large PackNet shape."""
+    g = torch.Generator(device="cpu").manual_seed(10)
+    shape, C = (6, 64, 96, 320), 64
+    gn = nn.GroupNorm(16, C).to(dev)
+    with torch.no_grad():
+        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        gn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    b = torch.randn(C, generator=g).to(dev, torch.bfloat16)
+    x = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    r = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) if residual else None
+    dy = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    outs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("PSFM_GN_PIPE", pipe)
+        xi, bi = x.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        ri = r.clone().requires_grad_(True) if residual else None
+        gn.zero_grad(set_to_none=True)
+        y = FU.gn_act(xi, bi, gn, act=FU.ACT_ELU, residual=ri)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        outs.append([t.detach().clone() for t in (y, xi.grad, bi.grad, gn.weight.grad, gn.bias.grad)
+                     + ((ri.grad,) if residual else ())])
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)

@@ -23,6 +23,9 @@ ap.add_argument("--W", type=int, default=640)
 ap.add_argument("--paths", default="k12,k1k2")
 ap.add_argument("--prio", default="", help="comma list of PSFM_K12_PRIO modes to run (K12 wave-pair balance)")
 ap.add_argument("--reps", type=int, default=1, help="repeat the whole lib x prio sweep (interleaved A/B)")
+ap.add_argument("--noisy", action="store_true",
+                help="i.i.d. U[0, 2] per-pixel sigmoid maps (what a random-init PackNetSAN01's InvDepth heads "
+                     "produce: sigmoid / min_depth, no spatial smoothness) instead of smooth maps in [0.01, 0.2]")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -37,7 +40,10 @@ image = gu.smooth_texture(g, B, 3, H, W).to(dev)
 ctx = [gu.smooth_texture(g, B, 3, H, W).to(dev) for _ in range(2)]
 K = gu.kitti_K(B, H, W).to(dev)
 vec = gu.pose_vecs(g, B, 2).to(dev)
-sigs = [gu.sigmoid_maps(g, B, H, W).to(dev).requires_grad_(True) for _ in range(4)]
+if args.noisy:
+    sigs = [(2.0 * torch.rand(B, 1, H, W, generator=g)).to(dev).requires_grad_(True) for _ in range(4)]
+else:
+    sigs = [gu.sigmoid_maps(g, B, H, W).to(dev).requires_grad_(True) for _ in range(4)]
 poses = [Pose.from_vec(vec[:, j], "euler") for j in range(2)]
 fn = MultiViewPhotometricLoss(num_scales=4, ssim_loss_weight=0.85, smooth_loss_weight=0.001,
                               photometric_reduce_op="min", automask_loss=True, clip_loss=0.0,
