@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/psfm_pack3d.h"
@@ -38,6 +39,9 @@ int fail(int code, const std::string& msg) {
 constexpr int NTH = 256;
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
+#ifndef P3D_DX_MFMA_DEFAULT
+#define P3D_DX_MFMA_DEFAULT 0   // dx of bf16 channels_last pack layers on the matrix cores by default
+#endif
 #ifndef MFMA_DW
 #define MFMA_DW 1   // weight gradient of bf16 channels_last pack layers on the matrix cores
 #endif
@@ -611,6 +615,173 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
 }
 
 // --------------------------------------------------------------------------------------------
+// dV of a bf16 channels_last pack layer (r = 2) on the matrix cores.  The transposed stencil splits
+// into a channel mix and a spatial shift-sum:
+//   G_s[k, p'] = sum_{o, dz} w[o, dz, s] dy[o, k - dz + 1, p']          (s = (ty, tx), 9 shifts)
+//   dV[k, y, x] = sum_s G_s[k, y - ty + 1, x - tx + 1]
+// The mix is one v_mfma_f32_16x16x32_bf16 product per (halo pixel pair x 8 k): rows = the 9 shifts
+// (A = weights), columns = (8 k, 2 pixels), contraction = (dz, o) with every weight split into
+// bf16 hi + lo parts (w = hi + lo to 16 mantissa bits; dy is bf16, so each product is exact in
+// fp32): d = 4 is 3 dz x 4 o x 2 parts = 24 of one MFMA's 32, d = 8 48 of two MFMAs' 64.  G goes
+// to LDS in fp32 and each thread sums its 9 shifted values for two channels of one input
+// sub-pixel (one 4-byte bf16 pair store: k and k + 4 are channels c, c + 1 at the same (i, j)).
+// Workgroup = 4 x 16 pixels x 8 k, 256 threads; the dy halo tile is staged as sd[pixel][k''][o]
+// (o fastest: a B fragment's 8 contraction values are one 16- (d = 8) or 8-byte (d = 4) read),
+// transposed from the (pixel, o) 16-byte runs of channels_last dy.  XCD-aware 1-D grid with the
+// chunk fastest, as k_p3d_bwd_x_cl: the 8 chunks of a 128-byte dy line run on one XCD.
+template <int ND>
+__global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) {
+    constexpr int TY = 4, TX = 16, DC = 8, LY = TY + 2, LX = TX + 2, NPIX = LY * LX, LKK = DC + 2;
+    constexpr int GS = NPIX * DC + 4;   // per-shift stride of the G tile (floats): 4 GS = 16 mod 64 banks
+    constexpr int NPAIR = ND / 2, UNITS = NPIX * NPAIR, ITER = (UNITS + 255) / 256;
+    constexpr int NMF = ND == 8 ? 2 : 1, HW = ND / 2;   // MFMAs per pixel pair; 32-bit words per (pixel, k'')
+    typedef short bf8 __attribute__((ext_vector_type(8)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint32_t sd[NPIX * LKK * HW];
+    __shared__ __attribute__((aligned(16))) float sG[9 * GS];
+    const int nch = a.K / DC;
+    int L;
+    {
+        const int n = gridDim.x, w = blockIdx.x, q = n / 8, rm = n % 8, xcd = w % 8, idx = w / 8;
+        L = xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
+    }
+    const int k0 = (L % nch) * DC;
+    const int rest = L / nch, tile = rest % (gxn * gyn), b = rest / (gxn * gyn);
+    const int x0 = (tile % gxn) * TX, y0 = (tile / gxn) * TY;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, m = lane & 15, j = lane >> 4;
+    const uint16_t* dyb = static_cast<const uint16_t*>(a.dy) + b * a.ys[0];
+    const int ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
+    // staging: unit = (halo pixel, o pair): two 16-byte runs (k0 .. k0+7 of o and o+1) + the k0-1 /
+    // k0+8 halo elements; out-of-image pixels and out-of-range k stage zeros
+    uint4 v0[ITER], v1[ITER];
+    uint32_t hlo[ITER], hhi[ITER];
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+        const int u = t + i * 256, pix = u / NPAIR, o = 2 * (u % NPAIR);
+        const int gy = y0 - 1 + pix / LX, gx = x0 - 1 + pix % LX;
+        const bool in = u < UNITS && (unsigned)gy < (unsigned)a.Hv && (unsigned)gx < (unsigned)a.Wv;
+        const uint16_t* s0 = dyb + (in ? gy * ys2 + gx * ys3 + o * a.K + k0 : 0);
+        const uint16_t* s1 = s0 + a.K;
+        v0[i] = in ? *reinterpret_cast<const uint4*>(s0) : make_uint4(0u, 0u, 0u, 0u);
+        v1[i] = in ? *reinterpret_cast<const uint4*>(s1) : make_uint4(0u, 0u, 0u, 0u);
+        const bool lo = in && k0 > 0, hi = in && k0 + DC < a.K;
+        hlo[i] = lo ? (uint32_t)s0[-1] | ((uint32_t)s1[-1] << 16) : 0u;
+        hhi[i] = hi ? (uint32_t)s0[DC] | ((uint32_t)s1[DC] << 16) : 0u;
+    }
+    // A fragments (lane row m = shift s, contraction block j): bf16 hi / lo parts of the weights
+    bf8 A[NMF];
+#pragma unroll
+    for (int c = 0; c < NMF; ++c) {
+        uint32_t wd[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t hv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int el = 2 * e + h;
+                int dz, o, part;
+                bool live;
+                if (ND == 8) {   // blocks 4c + j: (dz 0..2, hi), (dz 0..2, lo), zero, zero; element = o
+                    const int gb = 4 * c + j;
+                    live = gb < 6;
+                    dz = gb % 3, part = gb / 3, o = el;
+                } else {         // block j: dz = j (j < 3); elements 0..3 hi of o 0..3, 4..7 lo
+                    live = j < 3;
+                    dz = j, part = el >> 2, o = el & 3;
+                }
+                live = live && m < 9;
+                const float wf = live ? a.w[o * 27 + dz * 9 + m] : 0.0f;
+                uint32_t u = __float_as_uint(wf);
+                const uint32_t hib = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;   // RNE
+                const float lof = wf - __uint_as_float(hib << 16);               // exact
+                const uint32_t ul = __float_as_uint(lof);
+                const uint32_t lob = (ul + 0x7fffu + ((ul >> 16) & 1u)) >> 16;
+                hv[h] = part ? lob : hib;
+            }
+            wd[e] = hv[0] | (hv[1] << 16);
+        }
+        A[c] = __builtin_bit_cast(bf8, make_uint4(wd[0], wd[1], wd[2], wd[3]));
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+        const int u = t + i * 256;
+        if (u >= UNITS) break;
+        const int pix = u / NPAIR, op = u % NPAIR;
+        uint32_t* d = sd + pix * LKK * HW + op;   // word (o, o + 1) of k'' = 0
+        const uint32_t a4[4] = {v0[i].x, v0[i].y, v0[i].z, v0[i].w}, b4[4] = {v1[i].x, v1[i].y, v1[i].z, v1[i].w};
+        d[0] = hlo[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            d[(2 * q + 1) * HW] = (a4[q] & 0xffffu) | (b4[q] << 16);
+            d[(2 * q + 2) * HW] = (a4[q] >> 16) | (b4[q] & 0xffff0000u);
+        }
+        d[(LKK - 1) * HW] = hhi[i];
+    }
+    __syncthreads();
+    // the channel mix: N tile = halo pixel pair np (column m = kk + 8 pp)
+    {
+        const int kk = m & 7, pp = m >> 3;
+        int dzb[NMF];
+        bool zb[NMF];
+#pragma unroll
+        for (int c = 0; c < NMF; ++c) {
+            const int gb = ND == 8 ? 4 * c + j : j;
+            zb[c] = ND == 8 ? gb >= 6 : j >= 3;
+            dzb[c] = zb[c] ? 0 : (ND == 8 ? gb % 3 : j);
+        }
+        // C/D map: column = lane & 15, row = 4 j + register -> shift s
+        const int prow = (kk & 3) * 2 + (kk >> 2);   // G position of k: (k, k + 4) adjacent
+#pragma unroll 2
+        for (int np = wv; np < NPIX / 2; np += 4) {
+            const int pix = 2 * np + pp;
+            f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < NMF; ++c) {
+                const uint32_t* src = sd + (pix * LKK + kk - dzb[c] + 2) * HW;
+                uint4 bw;
+                if (ND == 8) {
+                    bw = *reinterpret_cast<const uint4*>(src);
+                } else {
+                    const uint2 h2 = *reinterpret_cast<const uint2*>(src);
+                    bw = make_uint4(h2.x, h2.y, h2.x, h2.y);   // the hi and lo blocks share dy
+                }
+                if (zb[c]) bw = make_uint4(0u, 0u, 0u, 0u);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[c], __builtin_bit_cast(bf8, bw), acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int s = 4 * j + r;
+                if (s < 9) sG[s * GS + pix * DC + prow] = acc[r];
+            }
+        }
+    }
+    __syncthreads();
+    // the shift-sum: thread = (tile pixel, sub-pixel (i, j)): k = k0 + 2 i + j and k + 4
+    const int p = t >> 2, sub = t & 3, py = p / TX, px = p % TX;
+    float2 sum = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+        const int ty = s / 3, tx = s % 3;
+        const float2 g = *reinterpret_cast<const float2*>(sG + s * GS + ((py - ty + 2) * LX + (px - tx + 2)) * DC + 2 * sub);
+        sum.x += g.x;
+        sum.y += g.y;
+    }
+    const int gy = y0 + py, gx = x0 + px;
+    if (gy < a.Hv && gx < a.Wv) {
+        const int64_t off = vaddr<PSFM_P3D_PACK>(a, b, k0 + sub, gy, gx);
+        uint32_t ux = __float_as_uint(sum.x), uy = __float_as_uint(sum.y);
+        ux = (ux + 0x7fffu + ((ux >> 16) & 1u)) >> 16;
+        uy = (uy + 0x7fffu + ((uy >> 16) & 1u)) >> 16;
+        if (a.xs[1] == 1) {   // channels c, c + 1 adjacent (even offset: host-checked)
+            *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(a.dx) + off) = ux | (uy << 16);
+        } else {
+            static_cast<uint16_t*>(a.dx)[off] = (uint16_t)ux;
+            static_cast<uint16_t*>(a.dx)[off + a.xs[1]] = (uint16_t)uy;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
 // dW[o][tap] = sum_{b,p,k} dy[o, k, p] V[k + dz - 1, p + (dy, dx) - 1], dbias[o] = sum dy[o, ., .]:
 // per-workgroup partials over a 4 x 16 pixel tile and its share of the channel chunks.
 // Thread t < 252: spatial shift s = t % 9 ((dy, dx) of the tap) and pixel group pg = t / 9
@@ -1088,7 +1259,19 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         const bool cl = t->mode == PSFM_P3D_PACK && a.dy32 && a.ys[1] == 1 && a.K % 16 == 0 &&
                         a.ys[0] % vec == 0 && a.ys[2] % vec == 0 && a.ys[3] % vec == 0 &&
                         (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
-        if (cl) {
+        // the matrix-core form: bf16, r = 2; 4-byte stores of (c, c + 1) pairs when x is channels_last
+        // with even strides (else two 2-byte stores)
+        const bool xpair = a.xs[1] != 1 || (a.xs[0] % 2 == 0 && a.xs[2] % 2 == 0 && a.xs[3] % 2 == 0 &&
+                                            (reinterpret_cast<uintptr_t>(dx) & 3) == 0);
+        const char* env = getenv("PSFM_P3D_DX");   // A/B knob: "mfma" / "cl" (the VALU k-pair kernel)
+        const bool want = env ? std::string(env) == "mfma" : P3D_DX_MFMA_DEFAULT;
+        const bool mfma = cl && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 8 == 0 && xpair && want;
+        if (mfma) {
+            const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
+            const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / 8)));   // one 8-k chunk per workgroup
+            if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_x_mfma<4>, g1, dim3(256), 0, st, a, gxn, gyn);
+            else hipLaunchKernelGGL(k_p3d_bwd_x_mfma<8>, g1, dim3(256), 0, st, a, gxn, gyn);
+        } else if (cl) {
             const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / 16)));   // one 16-k chunk per workgroup
             if (t->dtype == PSFM_P3D_BF16) {

@@ -165,3 +165,32 @@ def test_real_layer_shapes_match_torch_chain(dev, mode, d, shape):
     print(f"mode {mode} d={d} {shape}: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     assert errs["y"] <= 1e-2 and errs["dx"] <= 1e-2, errs
     assert errs["dW"] <= 2e-3 and errs["db"] <= 2e-3, errs
+
+
+@pytest.mark.parametrize("d", [8, 4])
+@pytest.mark.parametrize("shape", [(1, 40, 10, 36), (2, 16, 22, 70), (1, 8, 8, 20), (3, 24, 30, 34)])
+def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, d, shape):
+    """dV of bf16 channels_last pack layers: the matrix-core form (k_p3d_bwd_x_mfma: 8-k chunks,
+    weights split into bf16 hi + lo, fp32 shift-sum) and the VALU k-pair form (PSFM_P3D_DX=cl) both
+    within one bf16 rounding of the float64 reference chain (layers01.py:213-223), and within two
+    bf16 ulps of each other (partial edge tiles, K = 32 .. 160, first / last chunk halos)."""
+    from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
+    g = torch.Generator().manual_seed(sum(shape) + d)
+    x = torch.randn(shape, generator=g).to(torch.bfloat16)
+    w = torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2
+    b = torch.randn(d, generator=g) * 0.1
+    xd, conv, yref = _ref(0, x.float(), w, b, 2)
+    gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
+    (yref * gy.double()).sum().backward()
+    grads = {}
+    for form in ("mfma", "cl"):
+        monkeypatch.setenv("PSFM_P3D_DX", form)
+        xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        y = Pack3dFn.apply(xg, w.to(dev), b.to(dev), 0, 2)
+        y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
+        grads[form] = xg.grad.double().cpu()
+        ref = xd.grad
+        err = (grads[form] - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item(), (form, err, ref.abs().max().item())
+    diff = (grads["mfma"] - grads["cl"]).abs()
+    assert (diff <= 2 * 2.0 ** -8 * grads["cl"].abs() + 3e-5 * grads["cl"].abs().max()).all(), diff.max().item()
