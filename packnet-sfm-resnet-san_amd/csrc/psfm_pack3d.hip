@@ -625,60 +625,125 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
 // fp32): d = 4 is 3 dz x 4 o x 2 parts = 24 of one MFMA's 32, d = 8 48 of two MFMAs' 64.  G goes
 // to LDS in fp32 and each thread sums its 9 shifted values for two channels of one input
 // sub-pixel (one 4-byte bf16 pair store: k and k + 4 are channels c, c + 1 at the same (i, j)).
-// Workgroup = 4 x 16 pixels x 8 k, 256 threads; the dy halo tile is staged as sd[pixel][k''][o]
-// (o fastest: a B fragment's 8 contraction values are one 16- (d = 8) or 8-byte (d = 4) read),
-// transposed from the (pixel, o) 16-byte runs of channels_last dy.  XCD-aware 1-D grid with the
-// chunk fastest, as k_p3d_bwd_x_cl: the 8 chunks of a 128-byte dy line run on one XCD.
-template <int ND>
+// Workgroup = 4 x 16 pixels, CPW consecutive 8-k chunks, 256 threads; the dy halo tile is staged
+// as sd[pixel][k''][o] (o fastest: a B fragment's 8 contraction values are one 16- (d = 8) or
+// 8-byte (d = 4) read), transposed from the (pixel, o) 16-byte runs of channels_last dy.  The next
+// chunk's runs are loaded into registers while this chunk's mix and shift-sum run (offsets
+// computed once, loads unconditional — out-of-image units read offset 0 — and the validity
+// select at the LDS store, so no select makes the prefetch complete early).  XCD-aware 1-D grid
+// with the chunk group fastest, as k_p3d_bwd_x_cl: the workgroups sharing a 128-byte dy line run
+// back to back on one XCD.
+template <int ND, int CPW, int MODE>
 __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) {
     constexpr int TY = 4, TX = 16, DC = 8, LY = TY + 2, LX = TX + 2, NPIX = LY * LX, LKK = DC + 2;
     constexpr int GS = NPIX * DC + 4;   // per-shift stride of the G tile (floats): 4 GS = 16 mod 64 banks
     constexpr int NPAIR = ND / 2, UNITS = NPIX * NPAIR, ITER = (UNITS + 255) / 256;
     constexpr int NMF = ND == 8 ? 2 : 1, HW = ND / 2;   // MFMAs per pixel pair; 32-bit words per (pixel, k'')
+    constexpr bool PK = MODE == PSFM_P3D_PACK;
     typedef short bf8 __attribute__((ext_vector_type(8)));
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) uint32_t sd[NPIX * LKK * HW];
     __shared__ __attribute__((aligned(16))) float sG[9 * GS];
-    const int nch = a.K / DC;
+    const int ngr = a.K / (DC * CPW);   // chunk groups (host: K % (8 CPW) == 0)
     int L;
     {
         const int n = gridDim.x, w = blockIdx.x, q = n / 8, rm = n % 8, xcd = w % 8, idx = w / 8;
         L = xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
     }
-    const int k0 = (L % nch) * DC;
-    const int rest = L / nch, tile = rest % (gxn * gyn), b = rest / (gxn * gyn);
+    const int kbase = (L % ngr) * (DC * CPW);
+    const int rest = L / ngr, tile = rest % (gxn * gyn), b = rest / (gxn * gyn);
     const int x0 = (tile % gxn) * TX, y0 = (tile / gxn) * TY;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, m = lane & 15, j = lane >> 4;
     const uint16_t* dyb = static_cast<const uint16_t*>(a.dy) + b * a.ys[0];
     const int ys2 = (int)a.ys[2], ys3 = (int)a.ys[3];
-    // staging: unit = (halo pixel, o pair): two 16-byte runs (k0 .. k0+7 of o and o+1) + the k0-1 /
-    // k0+8 halo elements; out-of-image pixels and out-of-range k stage zeros
-    uint4 v0[ITER], v1[ITER];
-    uint32_t hlo[ITER], hhi[ITER];
+    // staging unit = (halo pixel, o pair): k0 .. k0+7 of o and o+1 + the k0-1 / k0+8 halo elements;
+    // chunk-independent int32 offsets (host-checked) and validity bits.  Pack: channel o K + k of
+    // the pixel, one 16-byte run per o.  Unpack (dy pixel-shuffled): channel c' = (o K + k) / 4 of
+    // sub-pixel (2y + i, 2x + j), (i, j) = k & 3 — per o the 8 k are 4 sub-pixels x 2 channels
+    // (c', c' + 1), four 4-byte loads.
+    int off[ITER], cb[ITER];
+    uint32_t ok = 0u;
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
         const int u = t + i * 256, pix = u / NPAIR, o = 2 * (u % NPAIR);
         const int gy = y0 - 1 + pix / LX, gx = x0 - 1 + pix % LX;
         const bool in = u < UNITS && (unsigned)gy < (unsigned)a.Hv && (unsigned)gx < (unsigned)a.Wv;
-        const uint16_t* s0 = dyb + (in ? gy * ys2 + gx * ys3 + o * a.K + k0 : 0);
-        const uint16_t* s1 = s0 + a.K;
-        v0[i] = in ? *reinterpret_cast<const uint4*>(s0) : make_uint4(0u, 0u, 0u, 0u);
-        v1[i] = in ? *reinterpret_cast<const uint4*>(s1) : make_uint4(0u, 0u, 0u, 0u);
-        const bool lo = in && k0 > 0, hi = in && k0 + DC < a.K;
-        hlo[i] = lo ? (uint32_t)s0[-1] | ((uint32_t)s1[-1] << 16) : 0u;
-        hhi[i] = hi ? (uint32_t)s0[DC] | ((uint32_t)s1[DC] << 16) : 0u;
+        off[i] = in ? (PK ? gy * ys2 + gx * ys3 + o * a.K : 2 * gy * ys2 + 2 * gx * ys3) : 0;
+        cb[i] = (o * a.K) >> 2;
+        ok |= in ? 1u << i : 0u;
     }
+    uint4 v0[ITER], v1[ITER];   // pack: the two runs; unpack: the 4 sub-pixel words of o, o + 1
+    uint16_t e[ITER][4];
+    auto load = [&](int k0) {
+        const bool lo = k0 > 0, hi = k0 + DC < a.K;   // clamped halo reads (zeroed at the store)
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+            if constexpr (PK) {
+                const uint16_t* s0 = dyb + off[i] + k0;
+                const uint16_t* s1 = s0 + a.K;
+                v0[i] = *reinterpret_cast<const uint4*>(s0);
+                v1[i] = *reinterpret_cast<const uint4*>(s1);
+                e[i][0] = s0[lo ? -1 : 0];
+                e[i][1] = s1[lo ? -1 : 0];
+                e[i][2] = s0[hi ? DC : 0];
+                e[i][3] = s1[hi ? DC : 0];
+            } else {
+                const uint16_t* p = dyb + off[i] + cb[i] + (k0 >> 2);   // (2y, 2x), channel c' of o
+                const int ko = a.K >> 2;                                  // o + 1: K / 4 channels on
+                uint32_t w[2][4];
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int ij = 0; ij < 4; ++ij)
+                        w[r][ij] = *reinterpret_cast<const uint32_t*>(p + r * ko + (ij >> 1) * ys2 + (ij & 1) * ys3);
+                v0[i] = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);
+                v1[i] = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
+                // k0 - 1 = channel c' - 1 at (1, 1); k0 + 8 = channel c' + 2 at (0, 0)
+                e[i][0] = p[lo ? ys2 + ys3 - 1 : 0];
+                e[i][1] = p[lo ? ko + ys2 + ys3 - 1 : 0];
+                e[i][2] = p[hi ? 2 : 0];
+                e[i][3] = p[hi ? ko + 2 : 0];
+            }
+        }
+    };
+    // unpack words -> the pack run order (k0 + kk: kk = 2 i + j of channel c', then of c' + 1)
+    auto runs = [](uint4 w) {
+        return make_uint4((w.x & 0xffffu) | (w.y << 16), (w.z & 0xffffu) | (w.w << 16),
+                          (w.x >> 16) | (w.y & 0xffff0000u), (w.z >> 16) | (w.w & 0xffff0000u));
+    };
+    auto store = [&](int k0) {
+        const bool lo = k0 > 0, hi = k0 + DC < a.K;
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+            const int u = t + i * 256;
+            if (u >= UNITS) break;
+            const bool in = (ok >> i) & 1u;
+            const int pix = u / NPAIR, op = u % NPAIR;
+            uint32_t* d = sd + pix * LKK * HW + op;   // word (o, o + 1) of k'' = 0
+            const uint4 r0 = PK ? v0[i] : runs(v0[i]), r1 = PK ? v1[i] : runs(v1[i]);
+            const uint4 p0 = in ? r0 : make_uint4(0u, 0u, 0u, 0u), p1 = in ? r1 : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t a4[4] = {p0.x, p0.y, p0.z, p0.w}, b4[4] = {p1.x, p1.y, p1.z, p1.w};
+            d[0] = in && lo ? (uint32_t)e[i][0] | ((uint32_t)e[i][1] << 16) : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                d[(2 * q + 1) * HW] = (a4[q] & 0xffffu) | (b4[q] << 16);
+                d[(2 * q + 2) * HW] = (a4[q] >> 16) | (b4[q] & 0xffff0000u);
+            }
+            d[(LKK - 1) * HW] = in && hi ? (uint32_t)e[i][2] | ((uint32_t)e[i][3] << 16) : 0u;
+        }
+    };
+    load(kbase);
     // A fragments (lane row m = shift s, contraction block j): bf16 hi / lo parts of the weights
     bf8 A[NMF];
 #pragma unroll
     for (int c = 0; c < NMF; ++c) {
         uint32_t wd[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int q = 0; q < 4; ++q) {
             uint32_t hv[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int el = 2 * e + h;
+                const int el = 2 * q + h;
                 int dz, o, part;
                 bool live;
                 if (ND == 8) {   // blocks 4c + j: (dz 0..2, hi), (dz 0..2, lo), zero, zero; element = o
@@ -691,46 +756,40 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
                 }
                 live = live && m < 9;
                 const float wf = live ? a.w[o * 27 + dz * 9 + m] : 0.0f;
-                uint32_t u = __float_as_uint(wf);
+                const uint32_t u = __float_as_uint(wf);
                 const uint32_t hib = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;   // RNE
                 const float lof = wf - __uint_as_float(hib << 16);               // exact
                 const uint32_t ul = __float_as_uint(lof);
                 const uint32_t lob = (ul + 0x7fffu + ((ul >> 16) & 1u)) >> 16;
                 hv[h] = part ? lob : hib;
             }
-            wd[e] = hv[0] | (hv[1] << 16);
+            wd[q] = hv[0] | (hv[1] << 16);
         }
         A[c] = __builtin_bit_cast(bf8, make_uint4(wd[0], wd[1], wd[2], wd[3]));
     }
+    // B fragment geometry: column m = kk + 8 pp (pixel pp of the pair), contraction block j -> dz
+    const int kk = m & 7, pp = m >> 3;
+    int dzb[NMF];
+    bool zb[NMF];
 #pragma unroll
-    for (int i = 0; i < ITER; ++i) {
-        const int u = t + i * 256;
-        if (u >= UNITS) break;
-        const int pix = u / NPAIR, op = u % NPAIR;
-        uint32_t* d = sd + pix * LKK * HW + op;   // word (o, o + 1) of k'' = 0
-        const uint32_t a4[4] = {v0[i].x, v0[i].y, v0[i].z, v0[i].w}, b4[4] = {v1[i].x, v1[i].y, v1[i].z, v1[i].w};
-        d[0] = hlo[i];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            d[(2 * q + 1) * HW] = (a4[q] & 0xffffu) | (b4[q] << 16);
-            d[(2 * q + 2) * HW] = (a4[q] >> 16) | (b4[q] & 0xffff0000u);
-        }
-        d[(LKK - 1) * HW] = hhi[i];
+    for (int c = 0; c < NMF; ++c) {
+        const int gb = ND == 8 ? 4 * c + j : j;
+        zb[c] = ND == 8 ? gb >= 6 : j >= 3;
+        dzb[c] = zb[c] ? 0 : (ND == 8 ? gb % 3 : j);
     }
-    __syncthreads();
-    // the channel mix: N tile = halo pixel pair np (column m = kk + 8 pp)
-    {
-        const int kk = m & 7, pp = m >> 3;
-        int dzb[NMF];
-        bool zb[NMF];
-#pragma unroll
-        for (int c = 0; c < NMF; ++c) {
-            const int gb = ND == 8 ? 4 * c + j : j;
-            zb[c] = ND == 8 ? gb >= 6 : j >= 3;
-            dzb[c] = zb[c] ? 0 : (ND == 8 ? gb % 3 : j);
-        }
-        // C/D map: column = lane & 15, row = 4 j + register -> shift s
-        const int prow = (kk & 3) * 2 + (kk >> 2);   // G position of k: (k, k + 4) adjacent
+    // G position of k: the two k a shift-sum thread stores adjacent — pack: k, k + 4 (channels c,
+    // c + 1 of one input sub-pixel), unpack: k, k + 1 (adjacent channels of x)
+    const int prow = PK ? (kk & 3) * 2 + (kk >> 2) : kk;
+    // shift-sum thread = (tile pixel, pair): pack k = k0 + 2 i + j and k + 4; unpack k0 + 2 sub, + 1
+    const int p = t >> 2, sub = t & 3, py = p / TX, px = p % TX;
+    const int oy = y0 + py, ox = x0 + px;
+    for (int ci = 0; ci < CPW; ++ci) {
+        const int k0 = kbase + ci * DC;
+        if (ci) __syncthreads();   // the previous chunk's mix (sd) and shift-sum (sG) are done
+        store(k0);
+        __syncthreads();
+        if (ci + 1 < CPW) load(k0 + DC);
+        // the channel mix: N tile = halo pixel pair np; C/D map: column = lane & 15, row = 4 j + reg
 #pragma unroll 2
         for (int np = wv; np < NPIX / 2; np += 4) {
             const int pix = 2 * np + pp;
@@ -754,29 +813,26 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
                 if (s < 9) sG[s * GS + pix * DC + prow] = acc[r];
             }
         }
-    }
-    __syncthreads();
-    // the shift-sum: thread = (tile pixel, sub-pixel (i, j)): k = k0 + 2 i + j and k + 4
-    const int p = t >> 2, sub = t & 3, py = p / TX, px = p % TX;
-    float2 sum = make_float2(0.0f, 0.0f);
+        __syncthreads();
+        float2 sum = make_float2(0.0f, 0.0f);
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-        const int ty = s / 3, tx = s % 3;
-        const float2 g = *reinterpret_cast<const float2*>(sG + s * GS + ((py - ty + 2) * LX + (px - tx + 2)) * DC + 2 * sub);
-        sum.x += g.x;
-        sum.y += g.y;
-    }
-    const int gy = y0 + py, gx = x0 + px;
-    if (gy < a.Hv && gx < a.Wv) {
-        const int64_t off = vaddr<PSFM_P3D_PACK>(a, b, k0 + sub, gy, gx);
-        uint32_t ux = __float_as_uint(sum.x), uy = __float_as_uint(sum.y);
-        ux = (ux + 0x7fffu + ((ux >> 16) & 1u)) >> 16;
-        uy = (uy + 0x7fffu + ((uy >> 16) & 1u)) >> 16;
-        if (a.xs[1] == 1) {   // channels c, c + 1 adjacent (even offset: host-checked)
-            *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(a.dx) + off) = ux | (uy << 16);
-        } else {
-            static_cast<uint16_t*>(a.dx)[off] = (uint16_t)ux;
-            static_cast<uint16_t*>(a.dx)[off + a.xs[1]] = (uint16_t)uy;
+        for (int s = 0; s < 9; ++s) {
+            const int ty = s / 3, tx = s % 3;
+            const float2 g = *reinterpret_cast<const float2*>(sG + s * GS + ((py - ty + 2) * LX + (px - tx + 2)) * DC + 2 * sub);
+            sum.x += g.x;
+            sum.y += g.y;
+        }
+        if (oy < a.Hv && ox < a.Wv) {
+            const int64_t o = vaddr<MODE>(a, b, PK ? k0 + sub : k0 + 2 * sub, oy, ox);
+            uint32_t ux = __float_as_uint(sum.x), uy = __float_as_uint(sum.y);
+            ux = (ux + 0x7fffu + ((ux >> 16) & 1u)) >> 16;
+            uy = (uy + 0x7fffu + ((uy >> 16) & 1u)) >> 16;
+            if (a.xs[1] == 1) {   // the pair's channels adjacent (even offset: host-checked)
+                *reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(a.dx) + o) = ux | (uy << 16);
+            } else {
+                static_cast<uint16_t*>(a.dx)[o] = (uint16_t)ux;
+                static_cast<uint16_t*>(a.dx)[o + a.xs[1]] = (uint16_t)uy;
+            }
         }
     }
 }
@@ -1256,21 +1312,48 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
     if (dx) {
         // channel-contiguous dy of a pack layer (channels_last), every 16-k run 16-byte aligned
         const int vec = t->dtype == PSFM_P3D_BF16 ? 8 : 4;
-        const bool cl = t->mode == PSFM_P3D_PACK && a.dy32 && a.ys[1] == 1 && a.K % 16 == 0 &&
-                        a.ys[0] % vec == 0 && a.ys[2] % vec == 0 && a.ys[3] % vec == 0 &&
-                        (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+        const bool cl8 = t->mode == PSFM_P3D_PACK && a.dy32 && a.ys[1] == 1 && a.K % 8 == 0 &&
+                         a.ys[0] % vec == 0 && a.ys[2] % vec == 0 && a.ys[3] % vec == 0 &&
+                         (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+        const bool cl = cl8 && a.K % 16 == 0;
         // the matrix-core form: bf16, r = 2; 4-byte stores of (c, c + 1) pairs when x is channels_last
         // with even strides (else two 2-byte stores)
         const bool xpair = a.xs[1] != 1 || (a.xs[0] % 2 == 0 && a.xs[2] % 2 == 0 && a.xs[3] % 2 == 0 &&
                                             (reinterpret_cast<uintptr_t>(dx) & 3) == 0);
-        const char* env = getenv("PSFM_P3D_DX");   // A/B knob: "mfma" / "cl" (the VALU k-pair kernel)
-        const bool want = env ? std::string(env) == "mfma" : P3D_DX_MFMA_DEFAULT;
-        const bool mfma = cl && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 8 == 0 && xpair && want;
+        // A/B knob: "mfma" (or "mfma1" / "mfma2" / "mfma4": chunks per workgroup) / "cl" (the VALU k-pair kernel)
+        const char* env = getenv("PSFM_P3D_DX");
+        const std::string form = env ? env : "";
+        const bool want = env ? form.compare(0, 4, "mfma") == 0 : P3D_DX_MFMA_DEFAULT;
+        // unpack layers: channels_last dy (2 Hv x 2 Wv, d K / 4 channels), 4-byte sub-pixel words
+        const int64_t umax = (int64_t)(t->d * a.K / 4 - 1) * a.ys[1] + (int64_t)(2 * a.Hv - 1) * a.ys[2] +
+                             (int64_t)(2 * a.Wv - 1) * a.ys[3];
+        const bool ucl = t->mode == PSFM_P3D_UNPACK && a.ys[1] == 1 && a.K % 8 == 0 && a.ys[0] % 2 == 0 &&
+                         a.ys[2] % 2 == 0 && a.ys[3] % 2 == 0 && a.ys[2] >= 0 && a.ys[3] >= 0 &&
+                         umax < (int64_t)INT32_MAX && (reinterpret_cast<uintptr_t>(dy) & 3) == 0;
+        const bool mfma = (cl8 || ucl) && t->dtype == PSFM_P3D_BF16 && t->r == 2 && xpair && want;
         if (mfma) {
             const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
-            const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / 8)));   // one 8-k chunk per workgroup
-            if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_x_mfma<4>, g1, dim3(256), 0, st, a, gxn, gyn);
-            else hipLaunchKernelGGL(k_p3d_bwd_x_mfma<8>, g1, dim3(256), 0, st, a, gxn, gyn);
+            int cpw = a.K % 32 == 0 ? 4 : a.K % 16 == 0 ? 2 : 1;   // 8-k chunks per workgroup
+            if (form.size() == 5 && (form[4] == '1' || form[4] == '2' || form[4] == '4') && a.K % (8 * (form[4] - '0')) == 0)
+                cpw = form[4] - '0';
+            const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / (8 * cpw))));
+#define P3D_DXM(ND, CPW)                                                                                              \
+    do {                                                                                                              \
+        if (t->mode == PSFM_P3D_PACK)                                                                                 \
+            hipLaunchKernelGGL((k_p3d_bwd_x_mfma<ND, CPW, PSFM_P3D_PACK>), g1, dim3(256), 0, st, a, gxn, gyn);        \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_p3d_bwd_x_mfma<ND, CPW, PSFM_P3D_UNPACK>), g1, dim3(256), 0, st, a, gxn, gyn);      \
+    } while (0)
+            if (t->d == 4) {
+                if (cpw == 4) P3D_DXM(4, 4);
+                else if (cpw == 2) P3D_DXM(4, 2);
+                else P3D_DXM(4, 1);
+            } else {
+                if (cpw == 4) P3D_DXM(8, 4);
+                else if (cpw == 2) P3D_DXM(8, 2);
+                else P3D_DXM(8, 1);
+            }
+#undef P3D_DXM
         } else if (cl) {
             const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / 16)));   // one 16-k chunk per workgroup

@@ -168,25 +168,28 @@ def test_real_layer_shapes_match_torch_chain(dev, mode, d, shape):
 
 
 @pytest.mark.parametrize("d", [8, 4])
-@pytest.mark.parametrize("shape", [(1, 40, 10, 36), (2, 16, 22, 70), (1, 8, 8, 20), (3, 24, 30, 34)])
-def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, d, shape):
-    """dV of bf16 channels_last pack layers: the matrix-core form (k_p3d_bwd_x_mfma: 8-k chunks,
-    weights split into bf16 hi + lo, fp32 shift-sum) and the VALU k-pair form (PSFM_P3D_DX=cl) both
-    within one bf16 rounding of the float64 reference chain (layers01.py:213-223), and within two
-    bf16 ulps of each other (partial edge tiles, K = 32 .. 160, first / last chunk halos)."""
+@pytest.mark.parametrize("mode,shape", [(0, (1, 40, 10, 36)), (0, (2, 16, 22, 70)), (0, (1, 10, 8, 20)), (0, (3, 12, 30, 34)),
+                                        (1, (1, 40, 10, 36)), (1, (2, 16, 11, 35)), (1, (1, 8, 8, 20)), (1, (3, 48, 6, 34))])
+def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mode, d, shape):
+    """dV of bf16 channels_last pack (mode 0) and unpack (mode 1) layers: the matrix-core form
+    (k_p3d_bwd_x_mfma: 8-k chunks, weights split into bf16 hi + lo, fp32 shift-sum) and the VALU
+    form (PSFM_P3D_DX=cl: the k-pair kernel for pack layers with K % 16 == 0, the generic kernel
+    otherwise) both within one bf16 rounding of the float64 reference chain (layers01.py:213-282),
+    and within two bf16 ulps of each other.  Pack K = 160 / 64 / 40 / 48 and unpack K = 40 / 16 /
+    8 / 48: 4, 4 (2), 1 and 2 chunks per workgroup, partial edge tiles, first / last chunk halos."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
-    g = torch.Generator().manual_seed(sum(shape) + d)
+    g = torch.Generator().manual_seed(sum(shape) + d + 10 * mode)
     x = torch.randn(shape, generator=g).to(torch.bfloat16)
     w = torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2
     b = torch.randn(d, generator=g) * 0.1
-    xd, conv, yref = _ref(0, x.float(), w, b, 2)
+    xd, conv, yref = _ref(mode, x.float(), w, b, 2)
     gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
     (yref * gy.double()).sum().backward()
     grads = {}
     for form in ("mfma", "cl"):
         monkeypatch.setenv("PSFM_P3D_DX", form)
         xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
-        y = Pack3dFn.apply(xg, w.to(dev), b.to(dev), 0, 2)
+        y = Pack3dFn.apply(xg, w.to(dev), b.to(dev), mode, 2)
         y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
         grads[form] = xg.grad.double().cpu()
         ref = xd.grad

@@ -10,8 +10,12 @@ timeout -k 10 300 python -u -m pytest tests/test_pack3d.py -m gpu -q -x --timeou
   > "$OUT/p3d_tests.log" 2>&1; rc=$?
 echo "[p3d tests] rc=$rc"; tail -3 "$OUT/p3d_tests.log"
 [ $rc -ne 0 ] && exit $rc
+PSFM_P3D_DX=mfma timeout -k 10 300 python -u -m pytest tests/test_pack3d.py -m gpu -q -x --timeout 200 --timeout-method thread -rfE \
+  -k "real_layer or matches_reference_chain or fused_op" -s > "$OUT/p3d_tests_mfma.log" 2>&1; rc=$?
+echo "[p3d tests mfma default] rc=$rc"; tail -3 "$OUT/p3d_tests_mfma.log"; grep "^mode" "$OUT/p3d_tests_mfma.log"
+[ $rc -ne 0 ] && exit $rc
 for net in packnet packnet-san; do
-  timeout -k 10 200 python -u tools/p3d_bench.py --net $net --dx mfma,cl,mfma,cl > "$OUT/p3d_bench_$net.log" 2>&1; rc=$?
+  timeout -k 10 200 python -u tools/p3d_bench.py --net $net --dx mfma4,mfma2,mfma1,cl,mfma4,mfma2,mfma1,cl > "$OUT/p3d_bench_$net.log" 2>&1; rc=$?
   echo "[p3d bench $net] rc=$rc"; cut -c1-400 "$OUT/p3d_bench_$net.log" | tail -4
   [ $rc -ne 0 ] && exit $rc
 done
