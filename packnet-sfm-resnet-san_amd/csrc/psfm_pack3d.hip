@@ -12,6 +12,9 @@
 //   k_p3d_bwd_x_cl dV = conv3d^T(dy)         pack layers, channels_last dy: one 4 x 16 pixel x 16 k
 //                                            chunk per workgroup (XCD-aware order), o in passes
 //                                            of 4, thread = 4 pixels x a k pair (packed f32)
+//   k_p3d_bwd_x_mfma dV = conv3d^T(dy)       bf16 channels_last, r = 2 (default for unpack layers):
+//                                            channel mix on the matrix cores (9 shifts x (8 k, 2
+//                                            pixels) x (dz, o, hi/lo weight)), fp32 shift-sum in LDS
 //   k_p3d_bwd_x    dV = conv3d^T(dy)         any other layout: 4 x 8 pixels x 16 k
 //   k_p3d_bwd_w    per-workgroup dw / db partials (thread = (spatial shift, pixel group), ND x 3
 //                  register partials; 16-byte dy staging for channels_last pack layers), fixed-order
@@ -40,7 +43,7 @@ constexpr int NTH = 256;
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
 #ifndef P3D_DX_MFMA_DEFAULT
-#define P3D_DX_MFMA_DEFAULT 0   // dx of bf16 channels_last pack layers on the matrix cores by default
+#define P3D_DX_MFMA_DEFAULT 0   // 1: dx of bf16 channels_last PACK layers on the matrix cores by default too
 #endif
 #ifndef MFMA_DW
 #define MFMA_DW 1   // weight gradient of bf16 channels_last pack layers on the matrix cores
@@ -1323,7 +1326,11 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         // A/B knob: "mfma" (or "mfma1" / "mfma2" / "mfma4": chunks per workgroup) / "cl" (the VALU k-pair kernel)
         const char* env = getenv("PSFM_P3D_DX");
         const std::string form = env ? env : "";
-        const bool want = env ? form.compare(0, 4, "mfma") == 0 : P3D_DX_MFMA_DEFAULT;
+        // default: the matrix-core form for unpack layers (2x the generic kernel at every PackNet
+        // shape), the VALU k-pair kernel for pack layers (the matrix-core form's staging issues 1.5x
+        // its per-lane line accesses: 0.85-1.0 vs 0.54 ms on the first PackNet01 layer,
+        // profiles/r04/p3d/)
+        const bool want = env ? form.compare(0, 4, "mfma") == 0 : t->mode == PSFM_P3D_UNPACK || P3D_DX_MFMA_DEFAULT;
         // unpack layers: channels_last dy (2 Hv x 2 Wv, d K / 4 channels), 4-byte sub-pixel words
         const int64_t umax = (int64_t)(t->d * a.K / 4 - 1) * a.ys[1] + (int64_t)(2 * a.Hv - 1) * a.ys[2] +
                              (int64_t)(2 * a.Wv - 1) * a.ys[3];
@@ -1333,7 +1340,9 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         const bool mfma = (cl8 || ucl) && t->dtype == PSFM_P3D_BF16 && t->r == 2 && xpair && want;
         if (mfma) {
             const int gxn = (a.Wv + 15) / 16, gyn = (a.Hv + 3) / 4;
-            int cpw = a.K % 32 == 0 ? 4 : a.K % 16 == 0 ? 2 : 1;   // 8-k chunks per workgroup
+            // 8-k chunks per workgroup: 2 when that still leaves >= 1024 workgroups (unpack 96x320 / 48x160
+            // layers: 128 vs 138 us), else 1 (the small layers want the workgroups)
+            int cpw = a.K % 16 == 0 && (int64_t)gxn * gyn * a.B * (a.K / 16) >= 1024 ? 2 : 1;
             if (form.size() == 5 && (form[4] == '1' || form[4] == '2' || form[4] == '4') && a.K % (8 * (form[4] - '0')) == 0)
                 cpw = form[4] - '0';
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / (8 * cpw))));

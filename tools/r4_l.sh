@@ -32,5 +32,4 @@ for v in pipe nopipe; do
   python3 tools/summarize_trace.py "$TR" "$OUT/step_summary_$v.txt" && head -3 "$OUT/step_summary_$v.txt" | cut -c1-150
   rm -rf "$OUT/prof_$v"
 done
-bash tools/r4_k.sh ${TAG}_ddad
 exit 0
