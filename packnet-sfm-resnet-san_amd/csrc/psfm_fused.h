@@ -107,6 +107,7 @@ struct Args {
     // arbitration tie to the older one by age.  prio_mode 1: the younger wave runs one priority
     // level higher in every phase; 2: in the p-eval only; 0: off.
     int young_from, prio_mode;
+    int xcd_parts;   // sweep::work_item_parts: parts per image in an XCD's run (k12_dealing)
 };
 
 __device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }   // both halves (op_sel broadcast)
@@ -386,7 +387,7 @@ struct K12 {
         plane = (uint32_t)(H * W);
         pb = plane * 4u;
         const int nst = stripes(W);
-        const sweep::WorkItem wi = work_item();
+        const sweep::WorkItem wi = sweep::work_item_parts(a_.xcd_parts);
         b = wi.b;
         s = wi.s;
         unit = wi.unit;

@@ -1070,6 +1070,11 @@ void k12_priority(fused::Args& fa, long waves) {
     fa.prio_mode = e ? atoi(e) : PSFM_K12_PRIO_DEFAULT;
     fa.young_from = simds / 8;  // SIMDs per XCD (8 XCDs)
     if (waves > 2L * simds || fa.prio_mode < 0 || fa.prio_mode > 2) fa.prio_mode = 0;
+    // XCD dealing: with fewer than 8 images each image's bands are split over 8 / B XCDs, every
+    // XCD sweeping its part for all scales (sweep::work_item_parts); PSFM_K12_PARTS overrides (A/B)
+    const char* pe = getenv("PSFM_K12_PARTS");
+    const int B = fa.p.B;
+    fa.xcd_parts = pe ? std::max(1, atoi(pe)) : (B < 8 ? 8 / B : 1);
 }
 
 int fwd_units(const psfm_params* p) {

@@ -53,6 +53,24 @@ __device__ __forceinline__ WorkItem work_item() {
     const int bs = w / units;
     return WorkItem{w - bs * units, bs / S, bs % S};
 }
+// The same dealing with each image's units cut into P contiguous parts (bands: unit = band x
+// stripes + stripe) and the run ordered (b, part, s, unit): an XCD's run then holds one part of an
+// image for ALL scales instead of all units for some scales — the scales share the image's
+// target and context frames, and a part's rows are what that XCD's L2 must hold (K12 at 384 x 640:
+// one image's three frames are 8.8 MB against a 4 MB L2).  P = 1 is work_item().
+__device__ __forceinline__ WorkItem work_item_parts(int P) {
+    const int units = gridDim.x, B = gridDim.y, S = gridDim.z;
+    const int T = units * B * S;
+    const int L = blockIdx.x + units * (blockIdx.y + B * blockIdx.z);
+    const int xcd = L & 7, i = L >> 3, q = T >> 3, r = T & 7;
+    const int w = xcd < r ? xcd * (q + 1) + i : r * (q + 1) + (xcd - r) * q + i;
+    const int per_b = S * units, b = w / per_b, wb = w - b * per_b;
+    const int PL = (units + P - 1) / P;            // units per part (the last part may be shorter)
+    const int part = wb / (S * PL), rr = wb - part * S * PL;
+    const int len = min(PL, units - part * PL);
+    const int s = rr / len;
+    return WorkItem{part * PL + (rr - s * len), b, s};
+}
 
 template <int I>
 using Slot = std::integral_constant<int, I>;
