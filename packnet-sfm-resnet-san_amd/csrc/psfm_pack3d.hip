@@ -636,11 +636,18 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
 // select at the LDS store, so no select makes the prefetch complete early).  XCD-aware 1-D grid
 // with the chunk group fastest, as k_p3d_bwd_x_cl: the workgroups sharing a 128-byte dy line run
 // back to back on one XCD.
-template <int ND, int CPW, int MODE>
+// GRP (pack layers, CPW = 4): the group's four chunks are loaded at once, lane = (pixel, o pair,
+// chunk) with the chunk fastest — four lanes read one contiguous 64-byte piece of each (pixel, o)
+// dy line instead of four lanes touching four lines (the per-lane line accesses of the chunk-wise
+// staging bound it: 0.85-1.0 ms vs the VALU kernel's 0.54 on the first PackNet01 layer); a chunk's
+// k0-1 / k0+8 halo elements come from the neighbouring chunks' registers, only the group's two
+// ends are extra 2-byte loads.
+template <int ND, int CPW, int MODE, bool GRP = false>
 __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) {
     constexpr int TY = 4, TX = 16, DC = 8, LY = TY + 2, LX = TX + 2, NPIX = LY * LX, LKK = DC + 2;
     constexpr int GS = NPIX * DC + 4;   // per-shift stride of the G tile (floats): 4 GS = 16 mod 64 banks
-    constexpr int NPAIR = ND / 2, UNITS = NPIX * NPAIR, ITER = (UNITS + 255) / 256;
+    constexpr int NPAIR = ND / 2, UNITS = NPIX * NPAIR * (GRP ? CPW : 1), ITER = (UNITS + 255) / 256;
+    static_assert(!GRP || (CPW == 4 && MODE == PSFM_P3D_PACK), "grouped staging: pack layers, 4 chunks");
     constexpr int NMF = ND == 8 ? 2 : 1, HW = ND / 2;   // MFMAs per pixel pair; 32-bit words per (pixel, k'')
     constexpr bool PK = MODE == PSFM_P3D_PACK;
     typedef short bf8 __attribute__((ext_vector_type(8)));
@@ -668,10 +675,10 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
     uint32_t ok = 0u;
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
-        const int u = t + i * 256, pix = u / NPAIR, o = 2 * (u % NPAIR);
+        const int u = t + i * 256, pu = GRP ? u >> 2 : u, pix = pu / NPAIR, o = 2 * (pu % NPAIR);
         const int gy = y0 - 1 + pix / LX, gx = x0 - 1 + pix % LX;
         const bool in = u < UNITS && (unsigned)gy < (unsigned)a.Hv && (unsigned)gx < (unsigned)a.Wv;
-        off[i] = in ? (PK ? gy * ys2 + gx * ys3 + o * a.K : 2 * gy * ys2 + 2 * gx * ys3) : 0;
+        off[i] = in ? (PK ? gy * ys2 + gx * ys3 + o * a.K + (GRP ? 8 * (t & 3) : 0) : 2 * gy * ys2 + 2 * gx * ys3) : 0;
         cb[i] = (o * a.K) >> 2;
         ok |= in ? 1u << i : 0u;
     }
@@ -681,7 +688,16 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
         const bool lo = k0 > 0, hi = k0 + DC < a.K;   // clamped halo reads (zeroed at the store)
 #pragma unroll
         for (int i = 0; i < ITER; ++i) {
-            if constexpr (PK) {
+            if constexpr (GRP) {   // k0 = the group's first k; this lane's chunk t & 3 is in off[]
+                const uint16_t* s0 = dyb + off[i] + k0;
+                const uint16_t* s1 = s0 + a.K;
+                v0[i] = *reinterpret_cast<const uint4*>(s0);
+                v1[i] = *reinterpret_cast<const uint4*>(s1);
+                const int c = t & 3;
+                const bool glo = c == 0 && k0 > 0, ghi = c == 3 && k0 + 4 * DC < a.K;
+                e[i][0] = s0[glo ? -1 : (ghi ? DC : 0)];
+                e[i][1] = s1[glo ? -1 : (ghi ? DC : 0)];
+            } else if constexpr (PK) {
                 const uint16_t* s0 = dyb + off[i] + k0;
                 const uint16_t* s1 = s0 + a.K;
                 v0[i] = *reinterpret_cast<const uint4*>(s0);
@@ -713,6 +729,34 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
     auto runs = [](uint4 w) {
         return make_uint4((w.x & 0xffffu) | (w.y << 16), (w.z & 0xffffu) | (w.w << 16),
                           (w.x >> 16) | (w.y & 0xffff0000u), (w.z >> 16) | (w.w & 0xffff0000u));
+    };
+    // grouped: chunk ci of the group starting at kg; lanes of chunk ci write k'' = 1..8, the lanes of
+    // chunk ci - 1 / ci + 1 their last / first element pair as k'' = 0 / 9 (the group ends: the
+    // 2-byte halo loads of the chunk 0 / 3 lanes, zero outside 0 .. K-1)
+    auto store_g = [&](int kg, int ci) {
+        const int c = t & 3;
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+            const int u = t + i * 256;
+            if (u >= UNITS) break;
+            const bool in = (ok >> i) & 1u;
+            const int pu = u >> 2, pix = pu / NPAIR, op = pu % NPAIR;
+            uint32_t* d = sd + pix * LKK * HW + op;
+            const uint4 p0 = in ? v0[i] : make_uint4(0u, 0u, 0u, 0u), p1 = in ? v1[i] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t a4[4] = {p0.x, p0.y, p0.z, p0.w}, b4[4] = {p1.x, p1.y, p1.z, p1.w};
+            const uint32_t ew = (uint32_t)e[i][0] | ((uint32_t)e[i][1] << 16);
+            if (c == ci) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    d[(2 * q + 1) * HW] = (a4[q] & 0xffffu) | (b4[q] << 16);
+                    d[(2 * q + 2) * HW] = (a4[q] >> 16) | (b4[q] & 0xffff0000u);
+                }
+                if (ci == 0) d[0] = in && kg > 0 ? ew : 0u;
+                if (ci == 3) d[(LKK - 1) * HW] = in && kg + 4 * DC < a.K ? ew : 0u;
+            }
+            if (c == ci - 1) d[0] = (a4[3] >> 16) | (b4[3] & 0xffff0000u);            // element 7
+            if (c == ci + 1) d[(LKK - 1) * HW] = (a4[0] & 0xffffu) | (b4[0] << 16);  // element 0
+        }
     };
     auto store = [&](int k0) {
         const bool lo = k0 > 0, hi = k0 + DC < a.K;
@@ -789,9 +833,10 @@ __global__ __launch_bounds__(256) void k_p3d_bwd_x_mfma(P3 a, int gxn, int gyn) 
     for (int ci = 0; ci < CPW; ++ci) {
         const int k0 = kbase + ci * DC;
         if (ci) __syncthreads();   // the previous chunk's mix (sd) and shift-sum (sG) are done
-        store(k0);
+        if constexpr (GRP) store_g(kbase, ci);
+        else store(k0);
         __syncthreads();
-        if (ci + 1 < CPW) load(k0 + DC);
+        if (!GRP && ci + 1 < CPW) load(k0 + DC);
         // the channel mix: N tile = halo pixel pair np; C/D map: column = lane & 15, row = 4 j + reg
 #pragma unroll 2
         for (int np = wv; np < NPIX / 2; np += 4) {
@@ -1345,6 +1390,8 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
             int cpw = a.K % 16 == 0 && (int64_t)gxn * gyn * a.B * (a.K / 16) >= 1024 ? 2 : 1;
             if (form.size() == 5 && (form[4] == '1' || form[4] == '2' || form[4] == '4') && a.K % (8 * (form[4] - '0')) == 0)
                 cpw = form[4] - '0';
+            const bool grp = t->mode == PSFM_P3D_PACK && a.K % 32 == 0 && form == "mfmag";
+            if (grp) cpw = 4;
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / (8 * cpw))));
 #define P3D_DXM(ND, CPW)                                                                                              \
     do {                                                                                                              \
@@ -1353,7 +1400,10 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         else                                                                                                          \
             hipLaunchKernelGGL((k_p3d_bwd_x_mfma<ND, CPW, PSFM_P3D_UNPACK>), g1, dim3(256), 0, st, a, gxn, gyn);      \
     } while (0)
-            if (t->d == 4) {
+            if (grp) {
+                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_mfma<4, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
+                else hipLaunchKernelGGL((k_p3d_bwd_x_mfma<8, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
+            } else if (t->d == 4) {
                 if (cpw == 4) P3D_DXM(4, 4);
                 else if (cpw == 2) P3D_DXM(4, 2);
                 else P3D_DXM(4, 1);

@@ -169,6 +169,7 @@ def test_real_layer_shapes_match_torch_chain(dev, mode, d, shape):
 
 @pytest.mark.parametrize("d", [8, 4])
 @pytest.mark.parametrize("mode,shape", [(0, (1, 40, 10, 36)), (0, (2, 16, 22, 70)), (0, (1, 10, 8, 20)), (0, (3, 12, 30, 34)),
+                                        (0, (2, 32, 14, 38)),
                                         (1, (1, 40, 10, 36)), (1, (2, 16, 11, 35)), (1, (1, 8, 8, 20)), (1, (3, 48, 6, 34))])
 def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mode, d, shape):
     """dV of bf16 channels_last pack (mode 0) and unpack (mode 1) layers: the matrix-core form
@@ -176,7 +177,8 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
     form (PSFM_P3D_DX=cl: the k-pair kernel for pack layers with K % 16 == 0, the generic kernel
     otherwise) both within one bf16 rounding of the float64 reference chain (layers01.py:213-282),
     and within two bf16 ulps of each other.  Pack K = 160 / 64 / 40 / 48 and unpack K = 40 / 16 /
-    8 / 48: 4, 4 (2), 1 and 2 chunks per workgroup, partial edge tiles, first / last chunk halos."""
+    8 / 48: 4, 4 (2), 1 and 2 chunks per workgroup, partial edge tiles, first / last chunk halos;
+    PSFM_P3D_DX=mfmag: the grouped staging (pack layers with K % 32 == 0: K = 160 / 64 / 128)."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
     g = torch.Generator().manual_seed(sum(shape) + d + 10 * mode)
     x = torch.randn(shape, generator=g).to(torch.bfloat16)
@@ -186,7 +188,7 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
     gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
     (yref * gy.double()).sum().backward()
     grads = {}
-    for form in ("mfma", "cl"):
+    for form in ("mfma", "mfmag", "cl"):
         monkeypatch.setenv("PSFM_P3D_DX", form)
         xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
         y = Pack3dFn.apply(xg, w.to(dev), b.to(dev), mode, 2)
@@ -195,5 +197,6 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
         ref = xd.grad
         err = (grads[form] - ref).abs().max().item()
         assert err <= 1e-2 * ref.abs().max().item(), (form, err, ref.abs().max().item())
-    diff = (grads["mfma"] - grads["cl"]).abs()
-    assert (diff <= 2 * 2.0 ** -8 * grads["cl"].abs() + 3e-5 * grads["cl"].abs().max()).all(), diff.max().item()
+    for form in ("mfma", "mfmag"):
+        diff = (grads[form] - grads["cl"]).abs()
+        assert (diff <= 2 * 2.0 ** -8 * grads["cl"].abs() + 3e-5 * grads["cl"].abs().max()).all(), (form, diff.max().item())
