@@ -30,10 +30,13 @@ def main():
     __graft_entry__.build()
     from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
     dev = torch.device("cuda", 0)
+    from packnet_sfm_amd.networks.layers import fused   # the bench's default net epilogues
+    fused.FUSE.update(bias=True, bn=False, gn=True)
+    fused.UPCAT = True
+    fused.ADD_RELU = True
     torch.manual_seed(0)
     torch.backends.cudnn.benchmark = True
     model = bench.to_channels_last(bench.build_model(ns, dev))
-    opt = make_optimizer(model, 1e-4, 1e-4, fused=True)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=True, fused=True)
     tr = DDPTrainer(model, opt, dev, amp_dtype=torch.bfloat16, graph=False, flat=True, bf16_weights=True)
     batch = bench.synthetic_batch(a.batch, 192, 640, dev, seed=0, channels_last=True)
@@ -60,6 +63,21 @@ def main():
         f.write("\n=== by stack (5 frames) ===\n")
         ks = prof.key_averages(group_by_stack_n=6)
         f.write(ks.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=40))
+        # launch attribution of the glue kernels: each device kernel is listed under the innermost
+        # op that launched it (FunctionEvent.kernels), with the op's input shapes
+        from collections import defaultdict
+        att = defaultdict(lambda: [0, 0.0])
+        glue = ("SubTensorOp", "fillBuffer", "CastTensor", "copyBuffer", "elementwise", "indexSelect", "clamp",
+                "BinaryFunctor", "reduce_kernel", "Cast")
+        for e in prof.events():
+            for k in getattr(e, "kernels", []) or []:
+                if any(g in k.name for g in glue):
+                    key = (k.name[:48], e.name, str(e.input_shapes)[:110])
+                    att[key][0] += 1
+                    att[key][1] += k.duration
+        f.write("\n=== glue kernels by launching op (per step) ===\n")
+        for (kn, op, shp), (n, us) in sorted(att.items(), key=lambda kv: -kv[1][1]):
+            f.write(f"{us / a.steps:9.1f} us {n / a.steps:6.1f}x  {kn:48s}  <- {op}  {shp}\n")
     print("wrote", a.out)
 
 
