@@ -1029,8 +1029,13 @@ __device__ __forceinline__ void bwd_w_body(const P3& a) {
 // the chunk as one 16-byte load (k = k0 + 4e + 2i + j); the chunk halo k0 - 1 / k0 + 32 is one
 // element each.  Fixed instruction order, no atomics: deterministic; products of bf16 values are
 // exact in fp32 (the VALU kernel's arithmetic up to the accumulation order).
-template <int ND>
+// UNPACK layers (round 4): V = x itself, channels_last, so a (pixel, quarter) staging unit is 8
+// consecutive k (one 16-byte load, stored as a contiguous run); dy is pixel-shuffled: channel c' =
+// (o K + k) / 4 of sub-pixel (2y + i, 2x + j), (i, j) = k & 3, so a (pixel, o, sub-pixel) unit is 8
+// channels c' (16 bytes) = every 4th k of the 32-k run, stored interleaved.
+template <int ND, int MODE = PSFM_P3D_PACK>
 __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
+    constexpr bool PK = MODE == PSFM_P3D_PACK;
     constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LKP = 40, NP = TY * TX;
     // LDS strides in 16-byte units: a pixel's V run 5, a tile row 97 (= 18 x 5 + 7), a (pixel, o)
     // dy run 5.  The 9 spatial shifts a 16-lane MFMA fragment read touches sit at 5 sx + 97 sy
@@ -1078,21 +1083,21 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         const int e = t + u * NTH, ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
         const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
         const bool ok = e < LY * LX * 4 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
-        vo[u] = ok ? (int)vaddr<PSFM_P3D_PACK>(a, b, ij, gyy, gxx) : 0;
+        vo[u] = ok ? (int)vaddr<MODE>(a, b, PK ? ij : 8 * ij, gyy, gxx) : 0;
         vok |= ok ? 1u << u : 0u;
     }
     const int hi = t & 1;
     {   // chunk halo: kk = 0 <-> V[k0 - 1] = (c0 - 1, i = 1, j = 1); kk = 33 <-> V[k0 + 32] = (c0 + 8, 0, 0)
         const int pix = t >> 1, xx = pix % LX, yy = pix / LX, gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
         hok = t < LY * LX * 2 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
-        ho = hok ? (int)vaddr<PSFM_P3D_PACK>(a, b, hi ? 32 : -1, gyy, gxx) : 0;   // + 4 c0 - ... below
+        ho = hok ? (int)vaddr<MODE>(a, b, hi ? 32 : -1, gyy, gxx) : 0;   // + the chunk's channel below
     }
 #pragma unroll
     for (int u = 0; u < ND; ++u) {   // dy runs: (pixel, o) -> 32 channels o K + k0 .., 4 x 16 B
         const int e = t + u * NTH, qd = e & 3, po = e >> 2, o = po % ND, p = po / ND;
         const int gyy = y0 + p / TX, gxx = x0 + p % TX;
         const bool ok = gyy < a.Hv && gxx < a.Wv;
-        go[u] = ok ? (int)yaddr<PSFM_P3D_PACK>(a, b, o, 0, gyy, gxx) + 8 * qd : 0;
+        go[u] = ok ? (int)yaddr<MODE>(a, b, o, 0, gyy, gxx) + (PK ? 8 * qd : (qd >> 1) * (int)a.ys[2] + (qd & 1) * (int)a.ys[3]) : 0;
         gok |= ok ? 1u << u : 0u;
     }
     uint4 vq[NV], gq[ND];   // NP * ND * 4 / NTH = ND dy slots per thread
@@ -1101,7 +1106,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
     // loads of the NEXT chunk complete before this chunk's MFMA loop starts)
     bool hin = false;
     auto load = [&](int ch) {
-        const int k0 = ch * DC, c0 = k0 >> 2;
+        const int k0 = ch * DC, c0 = PK ? k0 >> 2 : k0, g0 = PK ? k0 : k0 >> 2;   // x / dy channel of the chunk
 #pragma unroll
         for (int u = 0; u < NV; ++u) vq[u] = *reinterpret_cast<const uint4*>(xv + ((vok >> u) & 1u ? vo[u] + c0 : 0));
         // k = k0 - 1 -> channel c0 - 1 (i = j = 1); k = k0 + 32 -> channel c0 + 8 (i = j = 0): the
@@ -1109,7 +1114,7 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
         hin = hok && (hi ? k0 + 32 < a.K : k0 > 0);
         hq = xv[hin ? ho + c0 : 0];
 #pragma unroll
-        for (int u = 0; u < ND; ++u) gq[u] = *reinterpret_cast<const uint4*>(gy + ((gok >> u) & 1u ? go[u] + k0 : 0));
+        for (int u = 0; u < ND; ++u) gq[u] = *reinterpret_cast<const uint4*>(gy + ((gok >> u) & 1u ? go[u] + g0 : 0));
     };
     auto store = [&]() {
 #pragma unroll
@@ -1118,18 +1123,29 @@ __global__ __launch_bounds__(NTH) void k_p3d_bwd_w_mfma(P3 a) {
             if (e >= LY * LX * 4) continue;
             const uint4 vv = (vok >> u) & 1u ? vq[u] : make_uint4(0u, 0u, 0u, 0u);
             const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-            uint16_t* row = sv + (pix / LX) * ROWS + (pix % LX) * LKP + 1 + 2 * (ij >> 1) + (ij & 1);
+            uint16_t* row = sv + (pix / LX) * ROWS + (pix % LX) * LKP + 1 + (PK ? 2 * (ij >> 1) + (ij & 1) : 8 * ij);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                row[8 * q] = (uint16_t)(w[q] & 0xffffu);
-                row[8 * q + 4] = (uint16_t)(w[q] >> 16);
+                row[PK ? 8 * q : 2 * q] = (uint16_t)(w[q] & 0xffffu);
+                row[PK ? 8 * q + 4 : 2 * q + 1] = (uint16_t)(w[q] >> 16);
             }
         }
         if (t < LY * LX * 2) sv[((t >> 1) / LX) * ROWS + ((t >> 1) % LX) * LKP + ((t & 1) ? 33 : 0)] = hin ? hq : (uint16_t)0;
 #pragma unroll
         for (int u = 0; u < ND; ++u) {
             const int e = t + u * NTH, qd = e & 3, po = e >> 2;
-            reinterpret_cast<uint4*>(sg + po * DCP)[qd] = (gok >> u) & 1u ? gq[u] : make_uint4(0u, 0u, 0u, 0u);   // po = p * ND + o
+            const uint4 gv = (gok >> u) & 1u ? gq[u] : make_uint4(0u, 0u, 0u, 0u);   // po = p * ND + o
+            if constexpr (PK) {
+                reinterpret_cast<uint4*>(sg + po * DCP)[qd] = gv;
+            } else {   // sub-pixel qd: channels c' + cc -> k = 4 cc + qd
+                const uint32_t w[4] = {gv.x, gv.y, gv.z, gv.w};
+                uint16_t* dst = sg + po * DCP + qd;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    dst[8 * q] = (uint16_t)(w[q] & 0xffffu);
+                    dst[8 * q + 4] = (uint16_t)(w[q] >> 16);
+                }
+            }
         }
     };
     if (c_lo < c_hi) load(c_lo);
@@ -1448,10 +1464,27 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
                           t->C % 8 == 0 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 &&
                           a.xs[0] >= 0 && a.xs[2] >= 0 && a.xs[3] >= 0 && a.ys[0] >= 0 && xmax < INT32_MAX - 64 &&
                           ymax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && MFMA_DW;
+        // unpack layers (round 4): x channels_last (V = x: 8-k 16-byte runs), dy channels_last
+        // pixel-shuffled (8-channel 16-byte runs per sub-pixel); PSFM_P3D_DW=generic: the VALU kernel (A/B)
+        const int64_t uxmax = (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(a.K - 1) * a.xs[1] +
+                              (int64_t)(a.Hv - 1) * a.xs[2] + (int64_t)(a.Wv - 1) * a.xs[3];
+        const int64_t uymax = (int64_t)(t->B - 1) * a.ys[0] + (int64_t)(t->d * a.K / 4 - 1) * a.ys[1] +
+                              (int64_t)(2 * a.Hv - 1) * a.ys[2] + (int64_t)(2 * a.Wv - 1) * a.ys[3];
+        const char* dwe = getenv("PSFM_P3D_DW");
+        const bool umfma = t->mode == PSFM_P3D_UNPACK && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 32 == 0 &&
+                           a.xs[1] == 1 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 && a.xs[0] >= 0 &&
+                           a.xs[2] >= 0 && a.xs[3] >= 0 && a.ys[1] == 1 && a.ys[0] % 8 == 0 && a.ys[2] % 8 == 0 &&
+                           a.ys[3] % 8 == 0 && a.ys[0] >= 0 && a.ys[2] >= 0 && a.ys[3] >= 0 && uxmax < INT32_MAX - 64 &&
+                           uymax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                           (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && MFMA_DW && !(dwe && std::string(dwe) == "generic");
         if (mfma) {
             grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);
             if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_w_mfma<4>, grid, dim3(NTH), 0, st, aw);
             else hipLaunchKernelGGL(k_p3d_bwd_w_mfma<8>, grid, dim3(NTH), 0, st, aw);
+        } else if (umfma) {
+            grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_w_mfma<4, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, aw);
+            else hipLaunchKernelGGL((k_p3d_bwd_w_mfma<8, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, aw);
         } else if (cl) {
             if (t->dtype == PSFM_P3D_BF16) {
                 if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_w<uint16_t, PSFM_P3D_PACK, 4, true>), grid, dim3(NTH), 0, st, aw);

@@ -200,3 +200,30 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
     for form in ("mfma", "mfmag"):
         diff = (grads[form] - grads["cl"]).abs()
         assert (diff <= 2 * 2.0 ** -8 * grads["cl"].abs() + 3e-5 * grads["cl"].abs().max()).all(), (form, diff.max().item())
+
+
+@pytest.mark.parametrize("d", [8, 4])
+@pytest.mark.parametrize("shape", [(2, 64, 10, 36), (1, 96, 7, 19), (3, 32, 12, 40), (1, 128, 4, 6)])
+def test_unpack_dw_matrix_core_matches_the_reference(dev, monkeypatch, d, shape):
+    """Weight / bias gradient of bf16 channels_last UNPACK layers (layers01.py:226-282) on the
+    matrix cores (k_p3d_bwd_w_mfma<d, UNPACK>: V = x staged as contiguous 8-k runs, pixel-shuffled
+    dy staged per sub-pixel and interleaved) and on the VALU kernel (PSFM_P3D_DW=generic): both
+    within 2e-3 relative of the float64 reference chain; K = 64 / 96 / 32 / 128 (1 .. 4 chunks of
+    32), partial edge tiles."""
+    from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
+    g = torch.Generator().manual_seed(sum(shape) + 3 * d)
+    x = torch.randn(shape, generator=g).to(torch.bfloat16)
+    w = torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2
+    b = torch.randn(d, generator=g) * 0.1
+    xd, conv, yref = _ref(1, x.float(), w, b, 2)
+    gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
+    (yref * gy.double()).sum().backward()
+    for form in ("mfma", "generic"):
+        monkeypatch.setenv("PSFM_P3D_DW", form)
+        xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        wg, bg = w.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+        y = Pack3dFn.apply(xg, wg, bg, 1, 2)
+        y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
+        for got, ref in ((wg.grad, conv.weight.grad), (bg.grad, conv.bias.grad)):
+            err = (got.double().cpu() - ref).abs().max().item()
+            assert err <= 2e-3 * ref.abs().max().item(), (form, err, ref.abs().max().item())

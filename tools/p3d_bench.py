@@ -19,7 +19,8 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--net", default="packnet", choices=["packnet", "packnet-san"],
                 help="packnet: PackNet01 (d=8, n1=64); packnet-san: PackNetSAN01 (d=4, n1=32)")
 ap.add_argument("--only", default="", help="run only the case with this key (e.g. pack64x192x640)")
-ap.add_argument("--dx", default="mfma", help="comma list of PSFM_P3D_DX forms to A/B (mfma, cl)")
+ap.add_argument("--dx", default="", help="comma list of PSFM_P3D_DX forms to A/B (mfma, cl); empty: the default")
+ap.add_argument("--dw", default="", help="comma list of PSFM_P3D_DW forms to A/B (mfma, generic); empty: the default")
 args = ap.parse_args()
 __graft_entry__.build()
 from packnet_sfm_amd import _hip  # noqa: E402
@@ -58,8 +59,12 @@ def timed(fn, iters):
     return 1000.0 * e0.elapsed_time(e1) / iters
 
 
-for lib, form in [(lb, f) for lb in (args.lib or [None]) for f in args.dx.split(",")]:
-    os.environ["PSFM_P3D_DX"] = form
+for lib, form, dwf in [(lb, f, w) for lb in (args.lib or [None]) for f in args.dx.split(",") for w in args.dw.split(",")]:
+    for k, v in (("PSFM_P3D_DX", form), ("PSFM_P3D_DW", dwf)):
+        if v:
+            os.environ[k] = v
+        else:
+            os.environ.pop(k, None)
     if lib:
         _hip.LIB_PATH = lib
         _hip._lib = None
@@ -88,4 +93,4 @@ for lib, form in [(lb, f) for lb in (args.lib or [None]) for f in args.dx.split(
         res[key] = [round(t_f, 1), round(t_x, 1), round(t_w, 1)]
         tot = [tot[0] + t_f, tot[1] + t_x, tot[2] + t_w]
     res["total_fwd_bwdx_bwdw_us"] = [round(t, 1) for t in tot]
-    print(lib or "default", "dx=" + form, json.dumps(res), flush=True)
+    print(lib or "default", "dx=" + (form or "default"), "dw=" + (dwf or "default"), json.dumps(res), flush=True)
