@@ -42,6 +42,9 @@ int fail(int code, const std::string& msg) {
 constexpr int NTH = 256;
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
+#ifndef P3D_FWD_MFMA_DEFAULT
+#define P3D_FWD_MFMA_DEFAULT 0   // forward of bf16 channels_last layers on the matrix cores by default
+#endif
 #ifndef P3D_DX_MFMA_DEFAULT
 #define P3D_DX_MFMA_DEFAULT 0   // 1: dx of bf16 channels_last PACK layers on the matrix cores by default too
 #endif
@@ -613,6 +616,183 @@ __global__ __launch_bounds__(128, 2) void k_p3d_bwd_x_cl(P3 a, int gxn, int gyn)
         if (gy < a.Hv && gx < a.Wv) {
             st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k, gy, gx), acc[q].x);
             st<T>(a.dx, vaddr<PSFM_P3D_PACK>(a, b, k + 1, gy, gx), acc[q].y);
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// forward on the matrix cores (bf16, r = 2, channels_last x, K % 32 == 0; pack outputs channels_last,
+// unpack outputs pixel-shuffled): y[o, k, p] = bias[o] + sum_{s, dz} w[o, dz, s] V[k + dz - 1, p + s].
+// One group = 16 consecutive k of one pixel: A = the im2col rows (row m = k0 + 16 g + m, contraction
+// (s, dz') = 4 s + dz' with dz' = 3 a zero slot: 36 of two v_mfma_f32_16x16x32_bf16's 64), B = the
+// weights, column n = (o, hi / lo bf16 part): the hi and lo columns of o sit 8 lanes apart and are
+// summed after the MFMAs with one DPP row rotate (w = hi + lo to 16 mantissa bits, products of bf16
+// values exact in fp32).  A lane's 4 contraction values of one shift are V[k-1 .. k+2] of one
+// pixel: the V tile is staged twice in LDS, the second copy one element later, so every lane reads
+// its 4 values from a 4-byte aligned pair of dwords (the copy picked by the parity of its row).
+// Workgroup = 4 x 16 pixel tile (wave w: tile row w) x 32-k chunks (the dW kernel's XCD-grouped
+// grid and V staging); per wave and chunk 32 groups.  C rows = 4 consecutive k of one o: pack
+// outputs are one 8-byte store per lane (channel o K + k innermost), unpack outputs four 2-byte
+// stores (the 4 k are the 4 sub-pixels of one output channel).
+template <int ND, int MODE>
+__global__ __launch_bounds__(NTH) void k_p3d_fwd_mfma(P3 a) {
+    constexpr bool PK = MODE == PSFM_P3D_PACK;
+    constexpr int TY = 4, TX = 16, DC = 32, LY = TY + 2, LX = TX + 2, LKP = 40;
+    constexpr int ROWS = LX * LKP + 56;
+    typedef short bf8 __attribute__((ext_vector_type(8)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint16_t sv[2][LY * ROWS];
+    const WG g = wg_coords(a);
+    const int x0 = g.bx * TX, y0 = g.by * TY;
+    const int b = g.bz / a.KG, kg = g.bz - b * a.KG;
+    const int nch = a.K / DC, c_lo = kg * nch / a.KG, c_hi = (kg + 1) * nch / a.KG;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, m = lane & 15, j = lane >> 4;
+    const uint16_t* xv = static_cast<const uint16_t*>(a.x);
+    // B fragments: column n = (o, part), contraction block j of MFMA c: shifts s = 8 c + 2 j + h
+    // (h = 0, 1), elements 4 h + dz'
+    const int o = ND == 8 ? (m & 7) : (m & 3), part = m >> 3;
+    const bool ocol = ND == 8 || (m & 7) < 4;
+    bf8 Bw[2];
+    float bias_o = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        uint32_t wd[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t hv[2];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int el = 2 * q + hh, h = el >> 2, dz = el & 3, s = 8 * c + 2 * j + h;
+                const bool live = ocol && dz < 3 && s < 9;
+                const float wf = live ? a.w[o * 27 + dz * 9 + s] : 0.0f;
+                const uint32_t u = __float_as_uint(wf);
+                const uint32_t hib = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+                const float lof = wf - __uint_as_float(hib << 16);
+                const uint32_t ul = __float_as_uint(lof);
+                const uint32_t lob = (ul + 0x7fffu + ((ul >> 16) & 1u)) >> 16;
+                hv[hh] = part ? lob : hib;
+            }
+            wd[q] = hv[0] | (hv[1] << 16);
+        }
+        Bw[c] = __builtin_bit_cast(bf8, make_uint4(wd[0], wd[1], wd[2], wd[3]));
+    }
+    if (a.bias && ocol) bias_o = a.bias[o];
+    // V staging (as k_p3d_bwd_w_mfma): (pixel, quarter) units of 8 channels, chunk-independent
+    // int32 offsets, the chunk halo k0 - 1 / k0 + 32 one element each
+    constexpr int NV = (LY * LX * 4 + NTH - 1) / NTH;
+    int vo[NV], ho;
+    uint32_t vok = 0u;
+    bool hok;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = t + u * NTH, ij = e & 3, pix = e >> 2, xx = pix % LX, yy = pix / LX;
+        const int gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        const bool ok = e < LY * LX * 4 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        vo[u] = ok ? (int)vaddr<MODE>(a, b, PK ? ij : 8 * ij, gyy, gxx) : 0;
+        vok |= ok ? 1u << u : 0u;
+    }
+    const int hi = t & 1;
+    {
+        const int pix = t >> 1, xx = pix % LX, yy = pix / LX, gyy = y0 - 1 + yy, gxx = x0 - 1 + xx;
+        hok = t < LY * LX * 2 && gyy >= 0 && gyy < a.Hv && gxx >= 0 && gxx < a.Wv;
+        ho = hok ? (int)vaddr<MODE>(a, b, hi ? 32 : -1, gyy, gxx) : 0;
+    }
+    uint4 vq[NV];
+    uint16_t hq;
+    bool hin = false;
+    auto load = [&](int ch) {
+        const int k0 = ch * DC, c0 = PK ? k0 >> 2 : k0;
+#pragma unroll
+        for (int u = 0; u < NV; ++u) vq[u] = *reinterpret_cast<const uint4*>(xv + ((vok >> u) & 1u ? vo[u] + c0 : 0));
+        hin = hok && (hi ? k0 + 32 < a.K : k0 > 0);
+        hq = xv[hin ? ho + c0 : 0];
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = t + u * NTH, ij = e & 3, pix = e >> 2;
+            if (e >= LY * LX * 4) continue;
+            const uint4 vv = (vok >> u) & 1u ? vq[u] : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+            const int base = (pix / LX) * ROWS + (pix % LX) * LKP + 1 + (PK ? 2 * (ij >> 1) + (ij & 1) : 8 * ij);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e0 = base + (PK ? 8 * q : 2 * q), e1 = base + (PK ? 8 * q + 4 : 2 * q + 1);
+                sv[0][e0] = sv[1][e0 + 1] = (uint16_t)(w[q] & 0xffffu);
+                sv[0][e1] = sv[1][e1 + 1] = (uint16_t)(w[q] >> 16);
+            }
+        }
+        if (t < LY * LX * 2) {
+            const int e = ((t >> 1) / LX) * ROWS + ((t >> 1) % LX) * LKP + ((t & 1) ? 33 : 0);
+            sv[0][e] = sv[1][e + 1] = hin ? hq : (uint16_t)0;
+        }
+    };
+    // A geometry: row m -> element kk = 16 gk + m of the pixel's run is V[k - 1]; copy (m & 1)
+    // holds it at an even index (4-byte aligned dword pair)
+    const int cp = m & 1;
+    const uint16_t* va = sv[cp] + cp + m;
+    int soff[2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int s = min(8 * c + 2 * j + h, 8);
+            soff[c][h] = (s / 3) * ROWS + (s % 3) * LKP;
+        }
+    const bool a1live = j == 0;   // MFMA 1: only block 0 (s = 8, h = 0) carries taps
+    if (c_lo < c_hi) load(c_lo);
+    for (int ch = c_lo; ch < c_hi; ++ch) {
+        __syncthreads();   // the previous chunk's reads of sv are done
+        store();
+        __syncthreads();
+        if (ch + 1 < c_hi) load(ch + 1);
+        const int k0 = ch * DC;
+        const int gy = y0 + wv;
+#pragma unroll 2
+        for (int grp = 0; grp < 2 * TX; ++grp) {
+            const int px = grp >> 1, gk = grp & 1;
+            const uint16_t* vp = va + wv * ROWS + px * LKP + 16 * gk;
+            uint32_t aw[2][4];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(vp + soff[c][h]);
+                    aw[c][2 * h] = src[0];
+                    aw[c][2 * h + 1] = src[1] & 0xffffu;   // V[k+2] sits in the zero-weight slot: masked
+                }
+            f4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, make_uint4(aw[0][0], aw[0][1], aw[0][2], aw[0][3])),
+                                                         Bw[0], acc, 0, 0, 0);
+            const uint4 a1 = a1live ? make_uint4(aw[1][0], aw[1][1], 0u, 0u) : make_uint4(0u, 0u, 0u, 0u);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a1), Bw[1], acc, 0, 0, 0);
+            // column n + 8 (lo part of o) -> lane n: DPP row rotate by 8
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float lo = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(acc[r]), 0x128, 0xf, 0xf, false));
+                v[r] = (acc[r] + lo) + bias_o;
+            }
+            const int gx = x0 + px;
+            if (part == 0 && ocol && gy < a.Hv && gx < a.Wv) {
+                const int k = k0 + 16 * gk + 4 * j;   // rows 4 j .. 4 j + 3
+                uint32_t u[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t x = __float_as_uint(v[r]);
+                    u[r] = (x + 0x7fffu + ((x >> 16) & 1u)) >> 16;
+                }
+                uint16_t* y = static_cast<uint16_t*>(a.y);
+                if constexpr (PK) {   // channels o K + k .. + 3 of pixel (gy, gx): 8 bytes (host-checked)
+                    *reinterpret_cast<uint2*>(y + yaddr<MODE>(a, b, o, k, gy, gx)) = make_uint2(u[0] | (u[1] << 16), u[2] | (u[3] << 16));
+                } else {              // channel (o K + k) / 4 at the 4 sub-pixels
+                    const int64_t base = yaddr<MODE>(a, b, o, k, gy, gx);   // sub-pixel (0, 0)
+                    y[base] = (uint16_t)u[0];
+                    y[base + a.ys[3]] = (uint16_t)u[1];
+                    y[base + a.ys[2]] = (uint16_t)u[2];
+                    y[base + a.ys[2] + a.ys[3]] = (uint16_t)u[3];
+                }
+            }
         }
     }
 }
@@ -1324,7 +1504,29 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
     const bool xcl = vst && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 && a.xs[0] % vec == 0 &&
                      a.xs[2] % vec == 0 && a.xs[3] % vec == 0 && a.xs[0] >= 0 && a.xs[2] >= 0 && a.xs[3] >= 0 &&
                      xmax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    if (xcl) {
+    // the matrix-core form (k_p3d_fwd_mfma): bf16, r = 2, channels_last x with 16-byte 8-channel runs,
+    // 32-k chunks, channels_last y (pack: 8-byte 4-channel stores); PSFM_P3D_FWD=mfma / valu (A/B)
+    const char* fe = getenv("PSFM_P3D_FWD");
+    const bool fwant = fe ? std::string(fe) == "mfma" : P3D_FWD_MFMA_DEFAULT;
+    const int64_t xmaxm = t->mode == PSFM_P3D_PACK ? xmax
+                                                   : (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(a.K - 1) * a.xs[1] +
+                                                         (int64_t)(a.Hv - 1) * a.xs[2] + (int64_t)(a.Wv - 1) * a.xs[3];
+    const bool fmfma = fwant && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 32 == 0 && a.xs[1] == 1 &&
+                       a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 && a.xs[0] >= 0 && a.xs[2] >= 0 &&
+                       a.xs[3] >= 0 && xmaxm < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                       a.ys[1] == 1 &&
+                       (t->mode == PSFM_P3D_UNPACK || (a.ys[0] % 4 == 0 && a.ys[2] % 4 == 0 && a.ys[3] % 4 == 0 &&
+                                                      (reinterpret_cast<uintptr_t>(y) & 7) == 0));
+    if (fmfma) {
+        grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);
+        if (t->mode == PSFM_P3D_PACK) {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd_mfma<4, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd_mfma<8, PSFM_P3D_PACK>), grid, dim3(NTH), 0, st, a);
+        } else {
+            if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd_mfma<4, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);
+            else hipLaunchKernelGGL((k_p3d_fwd_mfma<8, PSFM_P3D_UNPACK>), grid, dim3(NTH), 0, st, a);
+        }
+    } else if (xcl) {
         grid = grid_lin(a, 4, 16, 32, P3D_FWD_CPW);
         if (t->dtype == PSFM_P3D_BF16) {
             if (t->d == 4) hipLaunchKernelGGL((k_p3d_fwd_cl<uint16_t, 4>), grid, dim3(NTH), 0, st, a);

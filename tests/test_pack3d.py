@@ -227,3 +227,30 @@ def test_unpack_dw_matrix_core_matches_the_reference(dev, monkeypatch, d, shape)
         for got, ref in ((wg.grad, conv.weight.grad), (bg.grad, conv.bias.grad)):
             err = (got.double().cpu() - ref).abs().max().item()
             assert err <= 2e-3 * ref.abs().max().item(), (form, err, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("d", [8, 4])
+@pytest.mark.parametrize("mode,shape", [(0, (1, 40, 10, 36)), (0, (2, 16, 22, 70)), (0, (3, 8, 14, 38)),
+                                        (1, (2, 64, 10, 36)), (1, (1, 96, 7, 19)), (1, (3, 32, 12, 40))])
+def test_forward_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mode, d, shape):
+    """Forward of bf16 channels_last pack (mode 0) / unpack (mode 1) layers on the matrix cores
+    (k_p3d_fwd_mfma: im2col rows of 16 k, weights split into bf16 hi + lo columns summed by a DPP
+    rotate, the V tile staged twice for aligned reads) and on the VALU kernels (PSFM_P3D_FWD=valu):
+    both within one bf16 rounding of the float64 reference chain (layers01.py:126-282) and within
+    two bf16 ulps of each other; K = 160 / 64 / 32 (pack), 64 / 96 / 32 (unpack), partial tiles."""
+    from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
+    g = torch.Generator().manual_seed(sum(shape) + 5 * d + mode)
+    x = torch.randn(shape, generator=g).to(torch.bfloat16)
+    w = torch.randn(d, 1, 3, 3, 3, generator=g) * 0.2
+    b = torch.randn(d, generator=g) * 0.1
+    _, _, yref = _ref(mode, x.float(), w, b, 2)
+    ys = {}
+    for form in ("mfma", "valu"):
+        monkeypatch.setenv("PSFM_P3D_FWD", form)
+        xg = x.to(dev).contiguous(memory_format=torch.channels_last)
+        with torch.no_grad():
+            ys[form] = Pack3dFn.apply(xg, w.to(dev), b.to(dev), mode, 2).double().cpu()
+        err = (ys[form] - yref.detach()).abs().max().item()
+        assert err <= 1e-2 * yref.abs().max().item(), (form, err)
+    diff = (ys["mfma"] - ys["valu"]).abs()
+    assert (diff <= 2 * 2.0 ** -8 * ys["valu"].abs() + 3e-5 * ys["valu"].abs().max()).all(), diff.max().item()

@@ -20,6 +20,7 @@ ap.add_argument("--net", default="packnet", choices=["packnet", "packnet-san"],
                 help="packnet: PackNet01 (d=8, n1=64); packnet-san: PackNetSAN01 (d=4, n1=32)")
 ap.add_argument("--only", default="", help="run only the case with this key (e.g. pack64x192x640)")
 ap.add_argument("--dx", default="", help="comma list of PSFM_P3D_DX forms to A/B (mfma, cl); empty: the default")
+ap.add_argument("--fwd", default="", help="comma list of PSFM_P3D_FWD forms to A/B (mfma, valu); empty: the default")
 ap.add_argument("--dw", default="", help="comma list of PSFM_P3D_DW forms to A/B (mfma, generic); empty: the default")
 args = ap.parse_args()
 __graft_entry__.build()
@@ -59,8 +60,9 @@ def timed(fn, iters):
     return 1000.0 * e0.elapsed_time(e1) / iters
 
 
-for lib, form, dwf in [(lb, f, w) for lb in (args.lib or [None]) for f in args.dx.split(",") for w in args.dw.split(",")]:
-    for k, v in (("PSFM_P3D_DX", form), ("PSFM_P3D_DW", dwf)):
+for lib, form, dwf, fwf in [(lb, f, w, fw) for lb in (args.lib or [None]) for f in args.dx.split(",")
+                            for w in args.dw.split(",") for fw in args.fwd.split(",")]:
+    for k, v in (("PSFM_P3D_DX", form), ("PSFM_P3D_DW", dwf), ("PSFM_P3D_FWD", fwf)):
         if v:
             os.environ[k] = v
         else:
@@ -93,4 +95,4 @@ for lib, form, dwf in [(lb, f, w) for lb in (args.lib or [None]) for f in args.d
         res[key] = [round(t_f, 1), round(t_x, 1), round(t_w, 1)]
         tot = [tot[0] + t_f, tot[1] + t_x, tot[2] + t_w]
     res["total_fwd_bwdx_bwdw_us"] = [round(t, 1) for t in tot]
-    print(lib or "default", "dx=" + (form or "default"), "dw=" + (dwf or "default"), json.dumps(res), flush=True)
+    print(lib or "default", "dx=" + (form or "default"), "dw=" + (dwf or "default"), "fwd=" + (fwf or "default"), json.dumps(res), flush=True)
