@@ -43,7 +43,7 @@ constexpr int NTH = 256;
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_fma_f32)
 constexpr int P3D_WAVES = 2;
 #ifndef P3D_FWD_MFMA_DEFAULT
-#define P3D_FWD_MFMA_DEFAULT 0   // forward of bf16 channels_last layers on the matrix cores by default
+#define P3D_FWD_MFMA_DEFAULT 0   // 1: the matrix-core forward for d = 4 pack layers too
 #endif
 #ifndef P3D_DX_MFMA_DEFAULT
 #define P3D_DX_MFMA_DEFAULT 0   // 1: dx of bf16 channels_last PACK layers on the matrix cores by default too
@@ -1507,7 +1507,12 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
     // the matrix-core form (k_p3d_fwd_mfma): bf16, r = 2, channels_last x with 16-byte 8-channel runs,
     // 32-k chunks, channels_last y (pack: 8-byte 4-channel stores); PSFM_P3D_FWD=mfma / valu (A/B)
     const char* fe = getenv("PSFM_P3D_FWD");
-    const bool fwant = fe ? std::string(fe) == "mfma" : P3D_FWD_MFMA_DEFAULT;
+    // default: d = 8 (PackNet01) every layer, d = 4 (PackNetSAN01) unpack layers only — with 4 of the
+    // 16 MFMA columns useful per part the d = 4 pack layers run faster on the VALU kernel
+    // (profiles/r04/p3d/ab_fwd_*: first PackNet01 layer 449 -> 400-421 us, unpack 96x320 133 -> 62;
+    // first PackNetSAN01 layer 90 vs 124-136)
+    const bool fwant = fe ? std::string(fe) == "mfma"
+                          : (P3D_FWD_MFMA_DEFAULT || t->d == 8 || t->mode == PSFM_P3D_UNPACK);
     const int64_t xmaxm = t->mode == PSFM_P3D_PACK ? xmax
                                                    : (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(a.K - 1) * a.xs[1] +
                                                          (int64_t)(a.Hv - 1) * a.xs[2] + (int64_t)(a.Wv - 1) * a.xs[3];
