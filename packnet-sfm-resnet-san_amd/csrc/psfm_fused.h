@@ -335,7 +335,7 @@ struct K12 {
     int H, W, B, b, s, unit, y0, col, colr, lane;
     int sh, Ws, colc;  // sigmoid storage: (H >> sh, W >> sh), this lane's stored column
     uint32_t plane, pb;
-    bool pcol, qcol, border;
+    bool pcol, qcol, border_l, border_r;
     DepthChain dc;
     float l1w, gscale, cx, cy, mc, wxl, wxr;
     const float* tgt;
@@ -403,7 +403,8 @@ struct K12 {
         colr = reflect1(col, W);
         pcol = lane >= 1 && lane <= OW + 2 && col >= 0 && col < W;
         qcol = lane >= 2 && lane <= OW + 1 && col < W;
-        border = c0 <= 1 || c0 + OW >= W - 2;  // this stripe holds column 1 or W-2
+        border_l = c0 <= 1;                    // this stripe holds column 1
+        border_r = c0 + OW >= W - 2;           // ... or column W-2
         wxl = (col == 1) ? 2.0f : 1.0f;        // p = col 0 reflected onto q = col 1 (SSIM reflect pad)
         wxr = (col == W - 2) ? 2.0f : 1.0f;    // p = col W-1 reflected onto q = col W-2
         dc = depth_chain(p);
@@ -674,11 +675,20 @@ struct K12 {
     __device__ __forceinline__ void hsum_w(f2& a0, f2& a1, f2& a2) const {
         f2 b0 = a0, b1 = a1, b2 = a2;
         hsum3x3(b0, b1, b2);
-        if (border) {  // wave-uniform: only the stripes holding column 1 or W-2
-            const float el = wxl - 1.0f, er = wxr - 1.0f;
-            b0 += f2{el * from_prev(a0.x) + er * from_next(a0.x), el * from_prev(a0.y) + er * from_next(a0.y)};
-            b1 += f2{el * from_prev(a1.x) + er * from_next(a1.x), el * from_prev(a1.y) + er * from_next(a1.y)};
-            b2 += f2{el * from_prev(a2.x) + er * from_next(a2.x), el * from_prev(a2.y) + er * from_next(a2.y)};
+        // wave-uniform: only the stripes holding column 1 / W-2, and only that side's term (a border
+        // wave doing both sides' DPP terms ran 4-5 % longer than an interior one and set the span:
+        // profiles/r04/prio/stamps_mode2.txt)
+        if (border_l) {
+            const float el = wxl - 1.0f;
+            b0 += f2{el * from_prev(a0.x), el * from_prev(a0.y)};
+            b1 += f2{el * from_prev(a1.x), el * from_prev(a1.y)};
+            b2 += f2{el * from_prev(a2.x), el * from_prev(a2.y)};
+        }
+        if (border_r) {
+            const float er = wxr - 1.0f;
+            b0 += f2{er * from_next(a0.x), er * from_next(a0.y)};
+            b1 += f2{er * from_next(a1.x), er * from_next(a1.y)};
+            b2 += f2{er * from_next(a2.x), er * from_next(a2.y)};
         }
         a0 = b0;
         a1 = b1;
