@@ -538,6 +538,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.train_step(next_batch())
+    host_enqueue = time.perf_counter() - t0   # host time to issue the K steps (no sync inside)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -564,6 +565,7 @@ def main():
                 }[args.data_path]
         out = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_step_ms, 3),
+               "host_enqueue_ms_per_step": round(1000.0 * host_enqueue / args.steps, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "bf16" if args.amp == "bf16" else "fp32", "data": "synthetic",
                "config": {"workload": f"SelfSupModel {args.depth_net} + {args.pose_net}, {args.width}x{args.height}, "
