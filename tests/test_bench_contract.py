@@ -33,3 +33,30 @@ def test_stale_or_foreign_pmc_profile_is_not_attached(tmp_path, monkeypatch):
 def test_algorithmic_bytes_follow_survey():
     # 120 B/px at N=2, S=4 -> 14,745,600 B per 192x640 image
     assert bench.algorithmic_bytes_per_image(192, 640) == 14_745_600
+
+
+def test_committed_bench_lines_keep_the_contract():
+    """The committed bench lines (profiles/r04/final) carry the driver's JSON contract: the headline
+    keys, the roofline object (dominant kernel against HBM, timed in the step) and, for the default
+    config, the CPU baseline object."""
+    import glob
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "profiles", "r04", "final", "bench_*.json")))
+    assert files
+    for f in files:
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+        for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+            assert k in d, (f, k)
+        assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["value"] > 0
+        r = d["roofline"]
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+            assert k in r, (f, k)
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+        assert "workload" in d["config"]
+        if f.endswith("bench_kitti-resnet-san.json"):
+            cb = d["cpu_baseline"]
+            for k in ("value", "unit", "cores", "kind", "sample"):
+                assert k in cb, k
