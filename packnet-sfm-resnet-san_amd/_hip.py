@@ -154,6 +154,15 @@ def lib():
         "psfm_p3d_ws_floats": ([V], ctypes.c_int64),
         "psfm_p3d_bwd": ([V, V, V, V, V, V, V, V, V], c_int),
         "psfm_p3d_last_error": ([], ctypes.c_char_p),
+        # include/psfm_packconv.h
+        "psfm_pc_ws_floats": ([V], ctypes.c_int64),
+        "psfm_pc_wbuf_bytes": ([V], ctypes.c_int64),
+        "psfm_pc_weights_of": ([V, V, V], c_int),
+        "psfm_pc_compose": ([V, V, V, V, V, V], c_int),
+        "psfm_pc_compose_bwd": ([V, V, V, V, V, V, V, V, V, V, V, V, V], c_int),
+        "psfm_pc_fwd": ([V, V, V, V, V, V], c_int),
+        "psfm_pc_bwd": ([V, V, V, V, V, V, V, V, V, V, V], c_int),
+        "psfm_pc_last_error": ([], ctypes.c_char_p),
         # include/psfm_metrics.h
         "psfm_depth_metrics": ([ctypes.POINTER(MetricsParams), V, V, V, V, V], c_int),
         "psfm_metrics_last_error": ([], ctypes.c_char_p),
@@ -189,6 +198,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_upcat_ws_floats",
             "psfm_depth_metrics", "psfm_metrics_last_error",
             "psfm_p3d_fwd", "psfm_p3d_ws_floats", "psfm_p3d_bwd", "psfm_p3d_last_error",
+            "psfm_pc_ws_floats", "psfm_pc_wbuf_bytes", "psfm_pc_weights_of", "psfm_pc_compose",
+            "psfm_pc_compose_bwd", "psfm_pc_fwd", "psfm_pc_bwd", "psfm_pc_last_error",
             "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_gather_frames",
             "psfm_augment_last_error",
             "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error")
@@ -209,6 +220,8 @@ def check(rc, what):
             err = lib().psfm_pose_last_error
         elif what.startswith("psfm_p3d"):
             err = lib().psfm_p3d_last_error
+        elif what.startswith("psfm_pc_"):
+            err = lib().psfm_pc_last_error
         else:
             err = lib().psfm_last_error
         raise RuntimeError(f"{what} failed ({rc}): {err().decode()}")

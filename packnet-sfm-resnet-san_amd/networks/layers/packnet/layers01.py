@@ -11,6 +11,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..fused import ACT_ELU, gn_act
+from . import packconv
 from .pack3d import conv3d_unpack, pack_conv3d
 
 
@@ -135,7 +136,12 @@ def _conv3d_d(d):
 
 
 class PackLayerConv3d(nn.Module):
-    """pack -> Conv3d(1->d) over (channel, y, x) -> fold d into channels -> Conv2D."""
+    """pack -> Conv3d(1->d) over (channel, y, x) -> fold d into channels -> Conv2D.
+
+    On a ROCm device in bf16 (autocast or bf16 input) the whole chain up to the Conv2d runs as the
+    composed (k+2) x (k+2) convolution over the packed channels (packconv.py,
+    include/psfm_packconv.h): the d*4C-channel packed volume is never written; the Conv2d bias,
+    GroupNorm and ELU follow in the fused psfm_gn_act as before."""
 
     def __init__(self, in_channels, kernel_size, r=2, d=8):
         super().__init__()
@@ -143,8 +149,23 @@ class PackLayerConv3d(nn.Module):
         self.pack = partial(packing, r=r)
         self.conv3d = _conv3d_d(d)
         self.r = r
+        self.in_channels = in_channels
+
+    def _composed(self, x):
+        c3 = self.conv3d
+        return (self.r == 2 and x.is_cuda and x.dim() == 4 and x.shape[1] == self.in_channels
+                and (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                     or not torch.is_autocast_enabled("cuda") and x.dtype == torch.bfloat16)
+                and c3.in_channels == 1 and tuple(c3.kernel_size) == (3, 3, 3) and tuple(c3.padding) == (1, 1, 1)
+                and tuple(c3.stride) == (1, 1, 1) and self.conv.conv_base.stride == (1, 1)
+                and packconv.supported(x, self.in_channels, self.conv.kernel_size, c3.out_channels)
+                and packconv.beneficial(x, self.in_channels))
 
     def forward(self, x):
+        if self._composed(x):
+            c = self.conv
+            y = packconv.pack_conv2d(x, self.conv3d, c.conv_base, c.kernel_size)
+            return gn_act(y, c.conv_base.bias, c.normalize, act=ACT_ELU)
         return self.conv(pack_conv3d(x, self.conv3d, self.r, self.pack))
 
 
