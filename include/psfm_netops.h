@@ -74,10 +74,12 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
  * or NULL, gamma/beta fp32 [C], act PSFM_ACT_NONE / RELU / ELU.  PoseNet conv_gn (conv + GN + ReLU,
  * PoseNet.py:15-19); PackNet Conv2D (conv + GN(16) + ELU, layers01.py:10-37) and ResidualConv's
  * GN(conv2 + shortcut) + ELU (res = the conv2 branch, layers01.py:40-61).  save_mean / save_invstd
- * [N*G].  Layers whose (sample, whole-group channel block) fits one workgroup's registers (HW <= 12288
- * row vectors, 8192 with res, at C / G <= 8; PackNet below 96x320) run ONE launch (statistics and
- * apply in the workgroup); larger ones two (statistics rows, then apply with the per-sample reduction
- * in its prologue).  Environment PSFM_GN_PATH=twopass forces the two-pass kernels. */
+ * [N*G].  Layers whose (sample, channel block) fits one 256-thread workgroup's registers run ONE launch
+ * (statistics and apply in the workgroup): the block is CB = max(8, C/G) channels with C/G in
+ * {1, 2, 4, 8, 16, 32} (CV = CB/8 row vectors of 8 channels per pixel), each thread holds RPT <= 4
+ * pixels' row vectors, so HW <= 256 RPT / CV = 1024 / CV pixels (PackNet's 24x80 and smaller layers
+ * at C/G <= 8).  Larger layers take two launches (statistics rows, then apply with the per-sample
+ * reduction in its prologue). */
 int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_bf16, const float* gamma,
                     const float* beta, float eps, int N, int HW, int C, int G, int act, void* y, float* save_mean,
                     float* save_invstd, float* ws, void* stream);
@@ -91,7 +93,7 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
  * per group the exact sum is ~0 and both are noise; tests/test_netops.py pins it for cpg 1 / 2 / 4 / 8+).
  * The activation's derivative is taken at its input, recomputed from x (+ res + bias), save_mean /
  * save_invstd and gamma / beta — the forward output is not read back.  Resident layers (as the
- * forward, register budget HW <= 4096 row vectors, 2048 with res): one data launch (dy, x read once)
+ * forward, HW <= 1024 / CV pixels, 512 / CV with res): one data launch (dy, x read once)
  * + a parameter finish over per-sample rows; others: statistics rows, then apply + parameter
  * gradients (two launches). */
 int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* bias, int bias_bf16,

@@ -1349,7 +1349,9 @@ inline bool gnr_geometry(int HW, int C, int G, int cap, GNRGeo& g) {
     if (C % G) return false;
     const int cpg = C / G;
     if (cpg >= 8) {
-        if (cpg % 8 || cpg > 32) return false;
+        // CV = cpg / 8 row vectors of a pixel must be a power of two (1, 2, 4): the row-per-thread
+        // mapping (RL = 256 / CV) and the XOR butterflies of wave_colsum group lanes by lane & (CV - 1)
+        if (cpg != 8 && cpg != 16 && cpg != 32) return false;
         g.CB = cpg, g.gpw = 1;
     } else {
         if (8 % cpg || G % (8 / cpg)) return false;

@@ -464,44 +464,65 @@ __device__ __forceinline__ float dy_at(const CornerArgs& A, int cn, int b, int i
     return bf2f(A.dy[b * A.ys0 + Y * A.ys2 + X * A.ys3 + m]);
 }
 
-// forward: e{L,R}[b][Y(i)][j C + m] -= sum_kin w[cn][i][j][m][kin] P_cn[b][kin]
+// forward: e{L,R}[b][Y(i)][j C + m] -= sum_kin w[cn][i][j][m][kin] P_cn[b][kin].  One workgroup per
+// (cn, i, j): the corner pixel's packed channels of every image are staged in LDS once; a thread
+// owns one m and streams its weight row; all images accumulate at once.
+constexpr int CORNER_MAXB = 16;
 __global__ __launch_bounds__(256) void k_pc_corner_fwd(const CornerArgs A) {
-    const int pk = A.pk, n = 4 * A.B * pk * pk * A.C, K = 4 * A.C;
-    const int id = blockIdx.x * 256 + threadIdx.x;
-    if (id >= n) return;
-    int r = id;
-    const int m = r % A.C;
-    r /= A.C;
-    const int j = r % pk;
-    r /= pk;
-    const int i = r % pk;
-    r /= pk;
-    const int b = r % A.B, cn = r / A.B;
-    const float* w = A.w + (((int64_t)(cn * pk + i) * pk + j) * A.C + m) * K;
-    float s = 0.f;
-    for (int kin = 0; kin < K; ++kin) s += w[kin] * p_corner(A, cn, b, kin);
+    __shared__ float sp[CORNER_MAXB * 2048];
+    const int pk = A.pk, K = 4 * A.C, ij = blockIdx.x % (pk * pk), cn = blockIdx.x / (pk * pk), i = ij / pk, j = ij % pk;
+    for (int e = threadIdx.x; e < A.B * K; e += 256) sp[e] = p_corner(A, cn, e / K, e % K);
+    __syncthreads();
     const bool top = (cn & 1) == 0, left = cn < 2;
     const int Y = top ? pk - 1 - i : A.Ho - 1 - i;
-    float* e = left ? A.eL : A.eR;
-    e[((int64_t)b * A.Ho + Y) * A.ecs + j * A.C + m] -= s;
+    float* eo = left ? A.eL : A.eR;
+    for (int m = threadIdx.x; m < A.C; m += 256) {
+        const float* w = A.w + (((int64_t)(cn * pk + i) * pk + j) * A.C + m) * K;
+        float acc[CORNER_MAXB];
+#pragma unroll
+        for (int b = 0; b < CORNER_MAXB; ++b) acc[b] = 0.f;
+        for (int kin = 0; kin < K; ++kin) {
+            const float wv = w[kin];
+#pragma unroll
+            for (int b = 0; b < CORNER_MAXB; ++b)
+                if (b < A.B) acc[b] += wv * sp[b * K + kin];
+        }
+#pragma unroll
+        for (int b = 0; b < CORNER_MAXB; ++b)
+            if (b < A.B) eo[((int64_t)b * A.Ho + Y) * A.ecs + j * A.C + m] -= acc[b];
+    }
 }
 
-// backward: d{L,R}[b][Yp][kin] -= sum_{i, j, m} w[cn][i][j][m][kin] dy[b][Y(i)][X(j)][m]
+// backward: d{L,R}[b][Yp][kin] -= sum_{i, j, m} w[cn][i][j][m][kin] dy[b][Y(i)][X(j)][m].  One
+// workgroup per (cn, kin block of 256): the corner frame's dy values of every image are staged in
+// LDS; a thread owns one kin (coalesced weight reads) and accumulates all images.
 __global__ __launch_bounds__(256) void k_pc_corner_bwd(const CornerArgs A) {
-    const int pk = A.pk, K = 4 * A.C, n = 4 * A.B * K;
-    const int id = blockIdx.x * 256 + threadIdx.x;
-    if (id >= n) return;
-    const int kin = id % K, b = (id / K) % A.B, cn = id / (K * A.B);
-    float s = 0.f;
-    for (int i = 0; i < pk; ++i)
-        for (int j = 0; j < pk; ++j) {
-            const float* w = A.w + ((int64_t)(cn * pk + i) * pk + j) * A.C * K + kin;
-            for (int m = 0; m < A.C; ++m) s += w[(int64_t)m * K] * dy_at(A, cn, b, i, j, m);
-        }
+    __shared__ float sd[CORNER_MAXB * 4 * 512];
+    const int pk = A.pk, K = 4 * A.C, nkb = (K + 255) / 256, cn = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+    const int nv = pk * pk * A.C;
+    for (int e = threadIdx.x; e < A.B * nv; e += 256) {
+        const int b = e / nv, r = e % nv, m = r % A.C, ij = r / A.C;
+        sd[e] = dy_at(A, cn, b, ij / pk, ij % pk, m);
+    }
+    __syncthreads();
+    const int kin = kb * 256 + threadIdx.x;
+    if (kin >= K) return;
+    float acc[CORNER_MAXB];
+#pragma unroll
+    for (int b = 0; b < CORNER_MAXB; ++b) acc[b] = 0.f;
+    const float* w = A.w + (int64_t)cn * nv * K + kin;
+    for (int r = 0; r < nv; ++r) {
+        const float wv = w[(int64_t)r * K];
+#pragma unroll
+        for (int b = 0; b < CORNER_MAXB; ++b)
+            if (b < A.B) acc[b] += wv * sd[b * nv + r];
+    }
     const bool top = (cn & 1) == 0, left = cn < 2;
     const int Yp = top ? 0 : A.Ho - 1;
-    float* e = left ? A.eL : A.eR;
-    e[((int64_t)b * A.Ho + Yp) * A.ecs + kin] -= s;
+    float* eo = left ? A.eL : A.eR;
+#pragma unroll
+    for (int b = 0; b < CORNER_MAXB; ++b)
+        if (b < A.B) eo[((int64_t)b * A.Ho + Yp) * A.ecs + kin] -= acc[b];
 }
 
 // weight gradient: dw[cn][i][j][m][kin] = sum_b dy[b][Y(i)][X(j)][m] P_cn[b][kin]
@@ -557,17 +578,27 @@ __global__ __launch_bounds__(256) void k_pc_bt_rows(const uint16_t* dy, int64_t 
     }
 }
 
-// stage 2: dbt[rc][cc][m] = sum over b and the rows Y of class rc, fixed order
+// stage 2: dbt[rc][cc][m] = sum over b and the rows Y of class rc: one workgroup per (rc, cc,
+// 64-channel block), 4 row groups x 64 channels, fixed-order combine
 __global__ __launch_bounds__(256) void k_pc_bt_cols(const float* part, int B, int C, int Ho, int pk, float* dbt) {
-    const int ncls = 2 * pk + 1, n = ncls * ncls * C, id = blockIdx.x * 256 + threadIdx.x;
-    if (id >= n) return;
-    const int m = id % C, cc = (id / C) % ncls, rc = id / (C * ncls);
+    __shared__ float red[4][64];
+    const int ncls = 2 * pk + 1, ncb = (C + 63) / 64;
+    const int cb = blockIdx.x % ncb, cc = (blockIdx.x / ncb) % ncls, rc = blockIdx.x / (ncb * ncls);
+    const int m = cb * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
     const int y0 = rc < pk ? rc : (rc > pk ? Ho - 1 - (2 * pk - rc) : pk);
-    const int y1 = rc == pk ? Ho - pk : y0 + 1;
+    const int y1 = rc == pk ? Ho - pk : y0 + 1, nrow = B * (y1 - y0);
     float s = 0.f;
-    for (int b = 0; b < B; ++b)
-        for (int Y = y0; Y < y1; ++Y) s += part[(((int64_t)b * Ho + Y) * ncls + cc) * C + m];
-    dbt[id] = s;
+    if (m < C)
+        for (int r = grp; r < nrow; r += 4) {
+            const int b = r / (y1 - y0), Y = y0 + r % (y1 - y0);
+            s += part[(((int64_t)b * Ho + Y) * ncls + cc) * C + m];
+        }
+    red[grp][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (grp == 0 && m < C) {
+        const int l = threadIdx.x;
+        dbt[(rc * ncls + cc) * C + m] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -902,6 +933,7 @@ int check_desc(const psfm_pc_desc* t) {
     if (t->k != 3 && t->k != 5) return fail(-1, "k must be 3 or 5");
     if (t->d != 4 && t->d != 8) return fail(-1, "d must be 4 or 8");
     if (s.Ho < 2 * s.pk + 1 || s.Wo < 2 * s.pk + 1) return fail(-1, "image smaller than the kernel frame");
+    if (s.B > CORNER_MAXB || s.C > 512) return fail(-1, "B <= 16 and C <= 512 (corner kernels stage one corner of the batch in LDS)");
     if (t->xs[1] != 1 || t->ys[1] != 1) return fail(-1, "x and y must be channels_last (channel stride 1)");
     for (int i : {0, 2, 3})
         if (t->xs[i] % 8 || t->ys[i] % 8 || t->xs[i] < 0 || t->ys[i] < 0)
@@ -1187,8 +1219,7 @@ int psfm_pc_fwd(const psfm_pc_desc* t, const psfm_pc_weights* w, const void* x, 
         c.eL = eb[2];
         c.eR = eb[3];
         c.ecs = s.copE;
-        const int n = 4 * s.B * s.pk * s.pk * s.C;
-        hipLaunchKernelGGL(k_pc_corner_fwd, dim3((n + 255) / 256), dim3(256), 0, st, c);
+        hipLaunchKernelGGL(k_pc_corner_fwd, dim3(4 * s.pk * s.pk), dim3(256), 0, st, c);
     }
     // 3. main convolution + epilogue
     ConvArgs M{};
@@ -1258,8 +1289,7 @@ int psfm_pc_bwd(const psfm_pc_desc* t, const psfm_pc_weights* w, const void* x, 
             c.eL = db[2];
             c.eR = db[3];
             c.ecs = s.Kin;
-            const int n = 4 * s.B * s.Kin;
-            hipLaunchKernelGGL(k_pc_corner_bwd, dim3((n + 255) / 256), dim3(256), 0, st, c);
+            hipLaunchKernelGGL(k_pc_corner_bwd, dim3(4 * ((s.Kin + 255) / 256)), dim3(256), 0, st, c);
         }
         // 3. main transposed convolution into dx through the packing permutation
         ConvArgs M{};
@@ -1361,9 +1391,8 @@ int psfm_pc_bwd(const psfm_pc_desc* t, const psfm_pc_weights* w, const void* x, 
         float* part = ws + L.bt_part;
         hipLaunchKernelGGL(k_pc_bt_rows, dim3(s.B * s.Ho), dim3(256), 0, st, gb, t->ys[0], t->ys[2], t->ys[3], s.C,
                            s.Ho, s.Wo, s.pk, part);
-        const int n = (2 * s.pk + 1) * (2 * s.pk + 1) * s.C;
-        hipLaunchKernelGGL(k_pc_bt_cols, dim3((n + 255) / 256), dim3(256), 0, st, (const float*)part, s.B, s.C, s.Ho,
-                           s.pk, dbt);
+        const int n = (2 * s.pk + 1) * (2 * s.pk + 1) * ((s.C + 63) / 64);
+        hipLaunchKernelGGL(k_pc_bt_cols, dim3(n), dim3(256), 0, st, (const float*)part, s.B, s.C, s.Ho, s.pk, dbt);
     }
     const hipError_t er = hipGetLastError();
     return er == hipSuccess ? 0 : fail((int)er, std::string("launch: ") + hipGetErrorString(er));

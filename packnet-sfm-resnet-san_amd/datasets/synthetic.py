@@ -173,8 +173,14 @@ class ResidentLoader:
             nchw.append(pair["nchw"])
             nhwc.append(pair["nhwc"])
         H, W = srcs[0].shape[-2:]
-        if (len(srcs) > 4 or (H * W) % 4 or srcs[0].shape[-3] != 3 or not all(s_.is_contiguous() for s_ in srcs)
-                or not dst["intrinsics"].is_contiguous() or not st["intrinsics"].is_contiguous()):
+        if (len(srcs) > 4 or (H * W) % 4 or srcs[0].shape[-3] != 3 or not all(s_.is_contiguous() for s_ in srcs)):
+            return False
+        # the kernel reads / writes intrinsics as float32 [*, 9] rows indexed by idx * cams + cam
+        di, si = dst["intrinsics"], st["intrinsics"]
+        n_store = srcs[0].shape[0]
+        if (di.dtype != torch.float32 or si.dtype != torch.float32 or not di.is_contiguous() or not si.is_contiguous()
+                or tuple(di.shape[-2:]) != (3, 3) or di.numel() != self.B * self.cameras * 9
+                or si.numel() != n_store * self.cameras * 9 or di.device != idx.device or si.device != idx.device):
             return False
         from .. import _hip
         P = ctypes.c_void_p * len(srcs)

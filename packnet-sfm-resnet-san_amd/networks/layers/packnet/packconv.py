@@ -48,7 +48,8 @@ class PcWeights(ctypes.Structure):
 def supported(x, C, k, d):
     B, _, H, W = x.shape
     pk = k // 2
-    return (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and C % 32 == 0 and H % 2 == 0 and W % 2 == 0
+    return (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and C % 32 == 0 and C <= 512 and B <= 16
+            and H % 2 == 0 and W % 2 == 0
             and H // 2 >= 2 * pk + 1 and W // 2 >= 2 * pk + 1)
 
 
@@ -70,10 +71,13 @@ def _desc(x, y, k, d):
     return t
 
 
-def _check_param(p, shape):
-    if p.dtype != torch.float32 or not p.is_contiguous() or tuple(p.shape) != tuple(shape) or not p.is_cuda:
-        raise RuntimeError(f"packconv: parameter must be a contiguous fp32 ROCm tensor of shape {tuple(shape)}, "
+def _param32(p, shape):
+    """The parameter as the contiguous fp32 tensor the composer reads (bf16 weights of the
+    mixed-precision trainer are widened exactly)."""
+    if p.dtype not in (torch.float32, torch.bfloat16) or tuple(p.shape) != tuple(shape) or not p.is_cuda:
+        raise RuntimeError(f"packconv: parameter must be an fp32 / bf16 ROCm tensor of shape {tuple(shape)}, "
                            f"got {p.dtype} {tuple(p.shape)} on {p.device}")
+    return p.detach().float().contiguous()
 
 
 class PackConvFn(torch.autograd.Function):
@@ -85,10 +89,10 @@ class PackConvFn(torch.autograd.Function):
     def forward(ctx, x, W2, w3, b3, k):
         B, C, H, W = x.shape
         d = w3.shape[0]
-        _check_param(W2, (C, 4 * C * d, k, k))
-        _check_param(w3, (d, 1, 3, 3, 3))
-        if b3 is not None:
-            _check_param(b3, (d,))
+        ctx.dtypes = (W2.dtype, w3.dtype, b3.dtype if b3 is not None else None)
+        W2 = _param32(W2, (C, 4 * C * d, k, k))
+        w3 = _param32(w3, (d, 1, 3, 3, 3))
+        b3 = _param32(b3, (d,)) if b3 is not None else None
         y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=torch.bfloat16,
                         memory_format=torch.channels_last)
         t = _desc(x, y, k, d)
@@ -140,6 +144,9 @@ class PackConvFn(torch.autograd.Function):
             _hip.check(L.psfm_pc_compose_bwd(ctypes.byref(t), _hip.ptr(W2), _hip.ptr(w3), _hip.ptr(b3), _hip.ptr(dwm),
                                              _hip.ptr(de), _hip.ptr(dc), _hip.ptr(dbt), _hip.ptr(gW2), _hip.ptr(gw3),
                                              _hip.ptr(gb3), _hip.ptr(ws), st), "psfm_pc_compose_bwd")
+            dt = ctx.dtypes
+            gW2, gw3 = gW2.to(dt[0]), gw3.to(dt[1])
+            gb3 = gb3.to(dt[2]) if gb3 is not None else None
         return dx, gW2, gw3, gb3, None
 
 

@@ -44,6 +44,7 @@ class GradBuckets:
             self.buckets.append((i, j))
             i = j
         self.params, self.offsets = list(params), list(offsets)
+        self.presence = None       # agreed once (agree_presence): which params have gradients
         self.bucket_of = {}
         for b, (i, j) in enumerate(self.buckets):
             for k in range(i, j):
@@ -194,19 +195,35 @@ class GradBuckets:
         if self.fused is not None:
             self._pending = []
 
-    def unpack(self, scale):
-        """Plain-optimizer path: averaged slices back into the parameters' .grad.  Whether a
-        parameter has a gradient is agreed across ranks first (one small all-reduce of a flag per
-        parameter): one that has a gradient on ANY rank gets the average on every rank (its slice
-        summed zeros where it had none), one with no gradient anywhere stays None everywhere (the
-        optimizer skips it, as for a single process).  Otherwise a rank whose gradient was None would
-        skip an update the other ranks apply, and the replicas would drift apart."""
+    def agree_presence(self):
+        """Which parameters have a gradient, agreed across ranks (one small all-reduce of a flag per
+        parameter and a host sync).  A parameter with a gradient on ANY rank gets the average on
+        every rank (its slice summed zeros where it had none); one with no gradient anywhere stays
+        None everywhere (the optimizer skips it, as for a single process)."""
         has = torch.tensor([p.grad is not None for p in self.params], dtype=torch.int32)
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             has = has.to(self.device if dist.get_backend() == "nccl" else torch.device("cpu"))
             dist.all_reduce(has, op=dist.ReduceOp.SUM)
-        for p, off, h in zip(self.params, self.offsets, has.tolist()):
+        self.presence = [bool(h) for h in has.tolist()]
+
+    def unpack(self, scale):
+        """Plain-optimizer path: averaged slices back into the parameters' .grad.  Eager steps agree
+        on gradient presence every step (the set may change: a head that stops receiving
+        gradients); inside a stream capture a pageable H2D copy, a collective on the capture stream
+        and a .tolist() are not allowed, so a captured unpack is device ops only and uses the
+        presence agreed by the last eager step (the trainer's warm-up): a graph replays one fixed
+        backward, so its set is that step's."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            if self.presence is None:
+                raise RuntimeError("grad_buckets.unpack: gradient presence must be agreed in an eager step "
+                                   "before the capture (agree_presence)")
+        else:
+            self.agree_presence()
+        for p, off, h in zip(self.params, self.offsets, self.presence):
             if not h:
+                if p.grad is not None:
+                    raise RuntimeError("grad_buckets.unpack: a parameter without a gradient in the agreed set "
+                                       "has one now (the set of parameters with gradients must be static)")
                 continue
             avg = self.flat[off:off + p.numel()].view(p.shape) * scale
             if p.grad is None:

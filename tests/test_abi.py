@@ -19,8 +19,7 @@ def hip():
 
 def declared_functions():
     names = set()
-    for h in ("psfm.h", "psfm_optim.h", "psfm_netops.h", "psfm_metrics.h", "psfm_pack3d.h", "psfm_augment.h",
-              "psfm_pose.h"):
+    for h in sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h")):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(psfm_[a-z_0-9]+)\s*\(", src))
@@ -34,6 +33,30 @@ def test_every_declared_symbol_is_exported(hip):
     for name in decl:
         assert hasattr(L, name), name
     assert sorted(hip.EXPORTED) == decl
+
+
+def test_packconv_abi_validates_without_a_gpu(hip):
+    """psfm_packconv.h: workspace / weight-buffer sizes and descriptor validation are host-only."""
+    from packnet_sfm_amd.networks.layers.packnet import packconv
+    L = hip.lib()
+    t = packconv.PcDesc(B=6, C=64, H=192, W=640, k=5, d=8)
+    t.xs[:] = [64 * 192 * 640, 1, 640 * 64, 64]
+    t.ys[:] = [64 * 96 * 320, 1, 320 * 64, 64]
+    ws, wb = L.psfm_pc_ws_floats(ctypes.byref(t)), L.psfm_pc_wbuf_bytes(ctypes.byref(t))
+    assert ws > 6 * 320 * 4 * 256 and wb > 2 * 64 * 256 * 49 * 2
+    w = packconv.PcWeights()
+    assert L.psfm_pc_weights_of(ctypes.byref(t), ctypes.c_void_p(4096), ctypes.byref(w)) == 0
+    assert w.wf == 4096 and w.wb > w.wf and w.bt > w.corner
+    for bad in (dict(k=7), dict(d=2), dict(C=48), dict(H=191), dict(H=8, W=8)):
+        tb = packconv.PcDesc(**{**dict(B=6, C=64, H=192, W=640, k=5, d=8), **bad})
+        tb.xs[:] = list(t.xs)
+        tb.ys[:] = list(t.ys)
+        assert L.psfm_pc_ws_floats(ctypes.byref(tb)) == -1
+        assert hip.lib().psfm_pc_last_error()
+    tc = packconv.PcDesc(B=6, C=64, H=192, W=640, k=5, d=8)
+    tc.xs[:] = [64 * 192 * 640, 640, 1, 192 * 640]   # NCHW: refused (channels_last only)
+    tc.ys[:] = list(t.ys)
+    assert L.psfm_pc_ws_floats(ctypes.byref(tc)) == -1
 
 
 def test_workspace_sizes(hip):

@@ -150,7 +150,8 @@ def gn_path(request, monkeypatch):
 # 256-thread workgroup) and channel block (cpg 1 / 2 / 4 -> 8-channel blocks of 8 / 4 / 2 groups,
 # cpg 16 / 32 -> 2 / 4 vector columns), resident forward + two-pass backward (res, RPT 4)
 GN_SHAPES = [(4, 16, 96, 320), (4, 64, 24, 80), (4, 256, 3, 10), (2, 32, 5, 7), (6, 16, 24, 80),
-             (6, 32, 12, 40), (6, 128, 48, 160), (6, 512, 12, 40), (6, 512, 6, 20), (3, 64, 60, 160)]
+             (6, 32, 12, 40), (6, 128, 48, 160), (6, 512, 12, 40), (6, 512, 6, 20), (3, 64, 60, 160),
+             (2, 384, 6, 20)]   # 24 channels per group: not a resident geometry, two-pass kernels
 
 
 @gpu
