@@ -104,8 +104,8 @@ struct Args {
     // Wave-pair balance (psfm_photometric.hip k12_priority): the workgroups of an XCD are dealt
     // round-robin to its SIMDs, so in a one-round launch the in-XCD index i = L >> 3 >= young_from
     // (= the XCD's SIMD count) marks the SECOND wave on its SIMD, which loses every VALU
-    // arbitration tie to the older one by age.  prio_mode 1: the younger wave runs one priority
-    // level higher in every phase; 2: in the p-eval only; 0: off.
+    // arbitration tie to the older one by age.  prio_mode 2: the younger wave runs one priority
+    // level higher in the p-eval; 0: off.
     int young_from, prio_mode;
     int xcd_parts;   // sweep::work_item_parts: parts per image in an XCD's run (k12_dealing)
 };
@@ -352,11 +352,10 @@ struct K12 {
     int prio_mode;
 
     // phase priorities: 2 (issue / q-eval / resolve) and 0 (p-eval), the younger wave of a SIMD
-    // pair one level up per Args::prio_mode
-    __device__ __forceinline__ void prio_hi() const {
-        if (young && prio_mode == 1) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(2);
-    }
+    // pair one level up in its p-eval (Args::prio_mode 2; the round-4 mode 1, younger +1 in every
+    // phase, only put a wave-uniform branch around each setprio: profiles/r05/k12/variants_ab.log,
+    // 97.7 -> 96.5 us per launch without it)
+    __device__ __forceinline__ void prio_hi() const { __builtin_amdgcn_s_setprio(2); }
     __device__ __forceinline__ void prio_lo() const {
         if (young) __builtin_amdgcn_s_setprio(1);
         else __builtin_amdgcn_s_setprio(0);

@@ -464,65 +464,87 @@ __device__ __forceinline__ float dy_at(const CornerArgs& A, int cn, int b, int i
     return bf2f(A.dy[b * A.ys0 + Y * A.ys2 + X * A.ys3 + m]);
 }
 
-// forward: e{L,R}[b][Y(i)][j C + m] -= sum_kin w[cn][i][j][m][kin] P_cn[b][kin].  One workgroup per
-// (cn, i, j): the corner pixel's packed channels of every image are staged in LDS once; a thread
-// owns one m and streams its weight row; all images accumulate at once.
+// forward: e{L,R}[b][Y(i)][j C + m] -= sum_kin w[cn][i][j][m][kin] P_cn[b][kin].  A workgroup per
+// (cn, i, j, 4 channels m): the corner pixel's packed channels of the batch are staged in LDS; wave
+// w owns m = 4 mb + w, its lanes split kin (coalesced weight reads) and every image is reduced
+// across the wave at the end.
 constexpr int CORNER_MAXB = 16;
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 __global__ __launch_bounds__(256) void k_pc_corner_fwd(const CornerArgs A) {
-    __shared__ float sp[CORNER_MAXB * 2048];
-    const int pk = A.pk, K = 4 * A.C, ij = blockIdx.x % (pk * pk), cn = blockIdx.x / (pk * pk), i = ij / pk, j = ij % pk;
+    extern __shared__ float sp[];   // [B][K]
+    const int pk = A.pk, K = 4 * A.C, nmb = (A.C + 3) / 4;
+    const int mb = blockIdx.x % nmb, r = blockIdx.x / nmb, ij = r % (pk * pk), cn = r / (pk * pk), i = ij / pk, j = ij % pk;
     for (int e = threadIdx.x; e < A.B * K; e += 256) sp[e] = p_corner(A, cn, e / K, e % K);
     __syncthreads();
+    const int lane = threadIdx.x & 63, m = mb * 4 + (threadIdx.x >> 6);
+    if (m >= A.C) return;
+    const float* w = A.w + (((int64_t)(cn * pk + i) * pk + j) * A.C + m) * K;
+    float acc[CORNER_MAXB];
+#pragma unroll
+    for (int b = 0; b < CORNER_MAXB; ++b) acc[b] = 0.f;
+    for (int kin = lane; kin < K; kin += 64) {
+        const float wv = w[kin];
+#pragma unroll
+        for (int b = 0; b < CORNER_MAXB; ++b)
+            if (b < A.B) acc[b] += wv * sp[b * K + kin];
+    }
     const bool top = (cn & 1) == 0, left = cn < 2;
     const int Y = top ? pk - 1 - i : A.Ho - 1 - i;
     float* eo = left ? A.eL : A.eR;
-    for (int m = threadIdx.x; m < A.C; m += 256) {
-        const float* w = A.w + (((int64_t)(cn * pk + i) * pk + j) * A.C + m) * K;
-        float acc[CORNER_MAXB];
 #pragma unroll
-        for (int b = 0; b < CORNER_MAXB; ++b) acc[b] = 0.f;
-        for (int kin = 0; kin < K; ++kin) {
-            const float wv = w[kin];
-#pragma unroll
-            for (int b = 0; b < CORNER_MAXB; ++b)
-                if (b < A.B) acc[b] += wv * sp[b * K + kin];
+    for (int b = 0; b < CORNER_MAXB; ++b)
+        if (b < A.B) {
+            const float v = wave_sum(acc[b]);
+            if (lane == 0) eo[((int64_t)b * A.Ho + Y) * A.ecs + j * A.C + m] -= v;
         }
-#pragma unroll
-        for (int b = 0; b < CORNER_MAXB; ++b)
-            if (b < A.B) eo[((int64_t)b * A.Ho + Y) * A.ecs + j * A.C + m] -= acc[b];
-    }
 }
 
-// backward: d{L,R}[b][Yp][kin] -= sum_{i, j, m} w[cn][i][j][m][kin] dy[b][Y(i)][X(j)][m].  One
-// workgroup per (cn, kin block of 256): the corner frame's dy values of every image are staged in
-// LDS; a thread owns one kin (coalesced weight reads) and accumulates all images.
+// backward: d{L,R}[b][Yp][kin] -= sum_{i, j, m} w[cn][i][j][m][kin] dy[b][Y(i)][X(j)][m].  A workgroup
+// per (cn, 64 kin): the corner frame's dy values of the batch are staged in LDS; lane = kin
+// (coalesced weight reads), the 4 waves split the (i, j, m) rows, fixed-order combine in LDS.
 __global__ __launch_bounds__(256) void k_pc_corner_bwd(const CornerArgs A) {
-    __shared__ float sd[CORNER_MAXB * 4 * 512];
-    const int pk = A.pk, K = 4 * A.C, nkb = (K + 255) / 256, cn = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+    extern __shared__ float sd[];   // [B][pk pk C] then the 4-wave combine [4][B][64]
+    const int pk = A.pk, K = 4 * A.C, nkb = (K + 63) / 64, cn = blockIdx.x / nkb, kb = blockIdx.x % nkb;
     const int nv = pk * pk * A.C;
     for (int e = threadIdx.x; e < A.B * nv; e += 256) {
         const int b = e / nv, r = e % nv, m = r % A.C, ij = r / A.C;
         sd[e] = dy_at(A, cn, b, ij / pk, ij % pk, m);
     }
     __syncthreads();
-    const int kin = kb * 256 + threadIdx.x;
-    if (kin >= K) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, kin = kb * 64 + lane;
     float acc[CORNER_MAXB];
 #pragma unroll
     for (int b = 0; b < CORNER_MAXB; ++b) acc[b] = 0.f;
-    const float* w = A.w + (int64_t)cn * nv * K + kin;
-    for (int r = 0; r < nv; ++r) {
-        const float wv = w[(int64_t)r * K];
+    if (kin < K) {
+        const float* w = A.w + (int64_t)cn * nv * K + kin;
+        const int r0 = wv * nv / 4, r1 = (wv + 1) * nv / 4;
+        for (int r = r0; r < r1; ++r) {
+            const float wvv = w[(int64_t)r * K];
 #pragma unroll
-        for (int b = 0; b < CORNER_MAXB; ++b)
-            if (b < A.B) acc[b] += wv * sd[b * nv + r];
+            for (int b = 0; b < CORNER_MAXB; ++b)
+                if (b < A.B) acc[b] += wvv * sd[b * nv + r];
+        }
     }
-    const bool top = (cn & 1) == 0, left = cn < 2;
-    const int Yp = top ? 0 : A.Ho - 1;
-    float* eo = left ? A.eL : A.eR;
+    float* cmb = sd + A.B * nv;
+    __syncthreads();
 #pragma unroll
     for (int b = 0; b < CORNER_MAXB; ++b)
-        if (b < A.B) eo[((int64_t)b * A.Ho + Yp) * A.ecs + kin] -= acc[b];
+        if (b < A.B) cmb[(wv * A.B + b) * 64 + lane] = acc[b];
+    __syncthreads();
+    if (wv == 0 && kin < K) {
+        const bool top = (cn & 1) == 0, left = cn < 2;
+        const int Yp = top ? 0 : A.Ho - 1;
+        float* eo = left ? A.eL : A.eR;
+        for (int b = 0; b < A.B; ++b) {
+            const float v = (cmb[(0 * A.B + b) * 64 + lane] + cmb[(1 * A.B + b) * 64 + lane]) +
+                            (cmb[(2 * A.B + b) * 64 + lane] + cmb[(3 * A.B + b) * 64 + lane]);
+            eo[((int64_t)b * A.Ho + Yp) * A.ecs + kin] -= v;
+        }
+    }
 }
 
 // weight gradient: dw[cn][i][j][m][kin] = sum_b dy[b][Y(i)][X(j)][m] P_cn[b][kin]
@@ -933,7 +955,10 @@ int check_desc(const psfm_pc_desc* t) {
     if (t->k != 3 && t->k != 5) return fail(-1, "k must be 3 or 5");
     if (t->d != 4 && t->d != 8) return fail(-1, "d must be 4 or 8");
     if (s.Ho < 2 * s.pk + 1 || s.Wo < 2 * s.pk + 1) return fail(-1, "image smaller than the kernel frame");
-    if (s.B > CORNER_MAXB || s.C > 512) return fail(-1, "B <= 16 and C <= 512 (corner kernels stage one corner of the batch in LDS)");
+    // the corner kernels stage one corner of the batch in (dynamic) LDS: <= 64 KB
+    if (s.B > CORNER_MAXB || (int64_t)s.B * s.Kin * 4 > 65536 ||
+        ((int64_t)s.B * s.pk * s.pk * s.C + 4 * s.B * 64) * 4 > 65536)
+        return fail(-1, "B <= 16 and B * 4C * 4 bytes <= 64 KB (corner kernels stage the batch's corner pixels in LDS)");
     if (t->xs[1] != 1 || t->ys[1] != 1) return fail(-1, "x and y must be channels_last (channel stride 1)");
     for (int i : {0, 2, 3})
         if (t->xs[i] % 8 || t->ys[i] % 8 || t->xs[i] < 0 || t->ys[i] < 0)
@@ -1219,7 +1244,8 @@ int psfm_pc_fwd(const psfm_pc_desc* t, const psfm_pc_weights* w, const void* x, 
         c.eL = eb[2];
         c.eR = eb[3];
         c.ecs = s.copE;
-        hipLaunchKernelGGL(k_pc_corner_fwd, dim3(4 * s.pk * s.pk), dim3(256), 0, st, c);
+        const size_t lds = (size_t)s.B * s.Kin * sizeof(float);
+        hipLaunchKernelGGL(k_pc_corner_fwd, dim3(4 * s.pk * s.pk * ((s.C + 3) / 4)), dim3(256), lds, st, c);
     }
     // 3. main convolution + epilogue
     ConvArgs M{};
@@ -1289,7 +1315,8 @@ int psfm_pc_bwd(const psfm_pc_desc* t, const psfm_pc_weights* w, const void* x, 
             c.eL = db[2];
             c.eR = db[3];
             c.ecs = s.Kin;
-            hipLaunchKernelGGL(k_pc_corner_bwd, dim3(4 * ((s.Kin + 255) / 256)), dim3(256), 0, st, c);
+            const size_t lds = ((size_t)s.B * s.pk * s.pk * s.C + 4 * s.B * 64) * sizeof(float);
+            hipLaunchKernelGGL(k_pc_corner_bwd, dim3(4 * ((s.Kin + 63) / 64)), dim3(256), lds, st, c);
         }
         // 3. main transposed convolution into dx through the packing permutation
         ConvArgs M{};

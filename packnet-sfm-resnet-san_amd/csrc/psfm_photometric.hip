@@ -29,8 +29,7 @@
 #ifndef PSFM_K12_PRIO_DEFAULT
 // fused::Args::prio_mode when PSFM_K12_PRIO is unset: 2 = the younger wave of a SIMD pair one
 // level up in its p-eval (A/B on one box, profiles/r04/prio: kbench B=4 101.0 -> 98.0 us, B=6
-// 141.3 -> 135.4 us; in the step 95.6-97.3 -> 93.8-94.1 us); 1 (younger up everywhere) only swaps
-// which wave of the pair finishes last
+// 141.3 -> 135.4 us; in the step 95.6-97.3 -> 93.8-94.1 us); 0 = off
 #define PSFM_K12_PRIO_DEFAULT 2
 #endif
 
@@ -1051,8 +1050,8 @@ int rb_for(const psfm_params* p) {
     return cost(fused::RB_HI) < cost(fused::RB_LO) ? fused::RB_HI : fused::RB_LO;
 }
 // K12 wave-pair balance (fused::Args young_from / prio_mode): the XCD's SIMD count, and the mode
-// from PSFM_K12_PRIO (0 off, 1 younger +1 everywhere, 2 younger +1 in the p-eval; read per launch so
-// an A/B can switch it in one process); only meaningful when the launch fits one wave round
+// from PSFM_K12_PRIO (0 off, 2 younger +1 in the p-eval); only meaningful when the launch fits one
+// wave round
 int simd_count() {
     static int simds[64] = {0};
     int dev = 0;
@@ -1069,7 +1068,7 @@ void k12_priority(fused::Args& fa, long waves) {
     const char* e = getenv("PSFM_K12_PRIO");
     fa.prio_mode = e ? atoi(e) : PSFM_K12_PRIO_DEFAULT;
     fa.young_from = simds / 8;  // SIMDs per XCD (8 XCDs)
-    if (waves > 2L * simds || fa.prio_mode < 0 || fa.prio_mode > 2) fa.prio_mode = 0;
+    if (waves > 2L * simds || fa.prio_mode != 2) fa.prio_mode = 0;
     // XCD dealing: with fewer than 8 images each image's bands are split over 8 / B XCDs, every
     // XCD sweeping its part for all scales (sweep::work_item_parts); PSFM_K12_PARTS overrides (A/B)
     const char* pe = getenv("PSFM_K12_PARTS");

@@ -48,7 +48,7 @@ class PcWeights(ctypes.Structure):
 def supported(x, C, k, d):
     B, _, H, W = x.shape
     pk = k // 2
-    return (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and C % 32 == 0 and C <= 512 and B <= 16
+    return (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and C % 32 == 0 and B <= 16 and B * 4 * C * 4 <= 65536
             and H % 2 == 0 and W % 2 == 0
             and H // 2 >= 2 * pk + 1 and W // 2 >= 2 * pk + 1)
 
