@@ -88,11 +88,21 @@ def parse(argv=None):
     ap.add_argument("--amp", default=None, choices=["bf16", "fp32"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N>1 on one GPU (ranks share the device, host all-reduce)")
-    ap.add_argument("--comm", default="split", choices=["split", "graph", "overlap"],
-                    help="split: all_reduce between two graph replays (default: no collective inside a "
-                         "graph); graph: captured into the step graph after the backward; overlap: "
-                         "bucketed, launched from gradient hooks during the backward on a side stream "
-                         "inside the step graph")
+    ap.add_argument("--comm", default="auto", choices=["auto", "split", "graph", "overlap"],
+                    help="split: all_reduce between two graph replays (no collective inside a graph); "
+                         "graph: captured into the step graph after the backward; overlap: bucketed, "
+                         "launched from gradient hooks during the backward on a side stream inside the "
+                         "step graph; auto (default): at N > 1 over RCCL every rank first runs one "
+                         "short-lived child that checks the overlap path on this node "
+                         "(trainers/comm_probe.py) — overlap if all pass, split otherwise (config.comm "
+                         "says which and why); N = 1 has no collective")
+    ap.add_argument("--comm-probe", action="store_true", help=argparse.SUPPRESS)   # the probe child
+    ap.add_argument("--comm-probe-timeout", type=float, default=240.0,
+                    help="seconds before a hung probe child is killed (-> split)")
+    ap.add_argument("--probe-only", action="store_true",
+                    help="run the --comm auto selection, print it as JSON on rank 0, exit (no training)")
+    ap.add_argument("--probe-backend", default=None, choices=["nccl", "gloo"],
+                    help="backend of the probe children (default: --dist-backend; gloo = CPU, tests)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the all-reduce path at N=1 too (world-size-1 RCCL group): its cost on one GPU")
     ap.add_argument("--bucket-mb", type=float, default=16.0, help="comm=overlap bucket size")
@@ -114,10 +124,12 @@ def parse(argv=None):
                          "partition of a synthetic dataset resident in HBM; resident: one fixed batch; "
                          "gpu-augment: the reference's train_transforms on the GPU from raw 375x1242 uint8 "
                          "frames inside every timed step")
-    ap.add_argument("--fused-nets", default="bias,gn",
+    ap.add_argument("--fused-nets", default="bias,gn,bn",
                     help="net epilogues as fused HIP kernels (psfm_netops): none | all | a comma list of "
-                         "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU), gn (GroupNorm + ReLU); "
-                         "default: the measured winners (networks/layers/fused.py FUSE)")
+                         "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU [+ identity]: the one-launch "
+                         "resident kernels where they hold the layer, MIOpen elsewhere), bnall (the fused "
+                         "BatchNorm on every layer), gn (GroupNorm + ReLU); default: the measured winners "
+                         "(networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
     ap.add_argument("--no-hip-gather", action="store_true",
@@ -159,6 +171,70 @@ def relaunch_distributed(args):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.call(cmd, env=env)
+
+
+def launch_comm_probe(args, rank, world, local_rank, port, backend):
+    """Start THIS rank's probe child (bench.py --comm-probe: trainers/comm_probe.py) in its own
+    session and return its exit status (124 after a kill at --comm-probe-timeout).  The children
+    form their own process group on `port`; nothing of theirs lives on in this process."""
+    import signal
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+    env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local_rank), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = [sys.executable, os.path.abspath(__file__), "--comm-probe", "--gpus", str(world),
+           "--dist-backend", backend]
+    p = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=sys.stderr, stderr=sys.stderr)
+    try:
+        return p.wait(timeout=args.comm_probe_timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        return 124
+
+
+def choose_comm(store, rank, world, run_child):
+    """--comm auto at N > 1: rank 0 publishes a free port for the probe children's own process
+    group, every rank runs its child (run_child(port) -> exit status) and publishes the status, and
+    every rank reads all of them — so all ranks pick the same path: 'overlap' when every child
+    passed, else 'split'.  Returns (comm, note for config.comm)."""
+    if rank == 0:
+        store.set("psfm_probe_port", str(_free_port()))
+    port = int(store.get("psfm_probe_port"))
+    rc = run_child(port)
+    store.set(f"psfm_probe_rc_{rank}", str(int(rc)))
+    rcs = [int(store.get(f"psfm_probe_rc_{r}")) for r in range(world)]
+    bad = {r: c for r, c in enumerate(rcs) if c != 0}
+    if not bad:
+        return "overlap", f"auto: overlap probe passed on {world} ranks"
+    return "split", f"auto: overlap probe failed (rank: exit status {bad}), split"
+
+
+def comm_probe_main(args, world, rank, local_rank):
+    """The probe child: its own process group, trainers/comm_probe.run_probe, exit status."""
+    if os.environ.get("PSFM_TEST_PROBE_FAIL_RANK") == str(rank):   # tests/test_distributed.py: a failing child
+        print(f"[comm probe] rank {rank}: failing on request (test)", file=sys.stderr, flush=True)
+        return 3
+    backend = args.dist_backend
+    if backend == "nccl":
+        device = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        dist.init_process_group("nccl", device_id=device)
+    else:
+        device = torch.device("cpu")
+        dist.init_process_group("gloo")
+    rc = 0
+    try:
+        import __graft_entry__
+        __graft_entry__.build()
+        from packnet_sfm_amd.trainers.comm_probe import run_probe
+        info = run_probe(device)
+        print(f"[comm probe] rank {rank}: {json.dumps(info)}", file=sys.stderr, flush=True)
+    except Exception as e:  # noqa: BLE001  (any failure means: do not use the overlap path)
+        print(f"[comm probe] rank {rank}: FAILED {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        rc = 1
+    finally:
+        dist.destroy_process_group()
+    return rc
 
 
 def synthetic_batch(B, H, W, device, seed, channels_last=False):
@@ -475,6 +551,28 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.comm_probe:
+        sys.exit(comm_probe_main(args, world, rank, local_rank))
+    # --comm auto: decided before this process touches the GPU (the probe children do)
+    store, comm_note = None, None
+    if args.comm == "auto":
+        args.comm = "split"
+        probe_backend = args.probe_backend or args.dist_backend
+        if (world > 1 and probe_backend == "nccl") or args.probe_backend is not None:
+            if world > 1:   # torch.distributed.run's store (the training process group reuses it)
+                from torch.distributed.rendezvous import rendezvous
+                store, _, _ = next(rendezvous("env://", rank, world))
+            args.comm, comm_note = choose_comm(
+                store if store is not None else dist.HashStore(), rank, world,
+                lambda port: launch_comm_probe(args, rank, world, local_rank, port, probe_backend))
+            if args.dist_backend == "gloo":   # a gloo run cannot capture its collectives
+                args.comm, comm_note = "split", comm_note + " (gloo run: split)"
+        else:
+            comm_note = "auto: split (" + ("one rank: no collective" if world == 1 else "gloo") + ")"
+    if args.probe_only:
+        if rank == 0:
+            print(json.dumps({"comm": args.comm, "comm_note": comm_note, "world": world}), flush=True)
+        return
     ndev = torch.cuda.device_count()
     if args.dist_backend == "nccl" and world > ndev:
         raise SystemExit(f"{world} ranks need {world} GPUs for RCCL, {ndev} visible "
@@ -488,10 +586,12 @@ def main():
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
     elif world > 1:
+        # the store --comm auto rendezvoused on: prefixed as init_process_group's own env:// path does
+        kw = dict(store=dist.PrefixStore("default_pg", store), rank=rank, world_size=world) if store is not None else {}
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, **kw)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **kw)
 
     import __graft_entry__
     if rank == 0 or world == 1:
@@ -505,7 +605,8 @@ def main():
 
     from packnet_sfm_amd.networks.layers import fused
     kinds = {"none": set(), "all": {"bias", "bn", "gn"}}.get(args.fused_nets, set(args.fused_nets.split(",")))
-    fused.FUSE.update(bias="bias" in kinds, bn="bn" in kinds, gn="gn" in kinds)
+    fused.FUSE.update(bias="bias" in kinds, bn=True if "bnall" in kinds else ("resident" if "bn" in kinds else False),
+                      gn="gn" in kinds)
     fused.UPCAT = not args.no_upcat
     fused.ADD_RELU = not args.no_add_relu
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
@@ -601,7 +702,7 @@ def main():
                           "dist_backend": args.dist_backend if world > 1 else None,
                           "comm": (f"{args.comm}" + (f" ({args.bucket_mb:g} MB buckets)" if args.comm == "overlap" else "")
                                    + (" (forced at N=1)" if world == 1 else "")) if (world > 1 or args.force_comm)
-                          else None, "data_path": data,
+                          else None, "comm_selection": comm_note, "data_path": data,
                           "net_dtype": args.amp, "loss_dtype": "fp32",
                           "net_layout": "NCHW" if args.nchw else "channels_last",
                           "step": "eager" if args.eager else "hip_graph",
@@ -609,10 +710,13 @@ def main():
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
                           "net_epilogues": (f"fused HIP (psfm_netops: {args.fused_nets}), the rest the reference "
-                                            f"op chain (MIOpen BN)" if args.fused_nets != "none" else "reference op chain"),
+                                            f"op chain (MIOpen BN on the layers the resident BN does not hold)"
+                                            if args.fused_nets != "none" else "reference op chain"),
                           "decoder_upcat": "torch op chain" if args.no_upcat else "HIP (psfm_upcat)",
                           "weights": "random init (no network / checkpoints)", "config_key": config_key(args)}}
         out["library"] = __graft_entry__.library_hash()
+        from packnet_sfm_amd import _hip as _hipmod
+        out["config"]["knobs"] = _hipmod.nondefault_knobs()   # kernel-selection knobs off their defaults
         if ktimes:
             out["roofline"] = roofline(args, ktimes, instep)
         elif instep:

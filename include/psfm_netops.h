@@ -57,12 +57,18 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
                       int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
- * three launches each way (statistics rows, per-channel finish, apply),
+ * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there), else three
+ * (statistics rows, per-channel finish, apply),
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
  * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
                     float* save_invstd, float* ws, void* stream);
+
+/* 1 when an [M, C] BatchNorm runs the resident one-launch kernels (a workgroup owns 8 channels and
+ * all M rows: C % 8 == 0 and M <= 8192, the ResNet encoder's layer2-4 at 192x640), else 0.  Callers
+ * keep MIOpen's BatchNorm for the other shapes (the three-pass kernels lose to it). */
+int psfm_bn_act_resident(int M, int C);
 
 /* Backward of psfm_bn_act_fwd: dx (bf16), dres (bf16, = ReLU-masked dy; may be NULL),
  * dgamma / dbeta (fp32 [C], written). */

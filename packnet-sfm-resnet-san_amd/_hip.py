@@ -8,6 +8,7 @@ shared with PyTorch-ROCm).
 """
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -137,6 +138,7 @@ def lib():
         "psfm_bias_act_bwd": ([V, V, c_int, c_int, c_int, V, V, c_int, V, V], c_int),
         "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V], c_int),
         "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
+        "psfm_bn_act_resident": ([c_int, c_int], c_int),
         "psfm_gn_act_fwd": ([V, V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V],
                             c_int),
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,
@@ -177,6 +179,12 @@ def lib():
         "psfm_pose_from_vec_bwd": ([V, c_int, c_int, V, V, V], c_int),
         "psfm_pinhole_cam_records": ([V, V, V, c_int, c_int, c_int, c_int, c_float, V, V], c_int),
         "psfm_pose_last_error": ([], ctypes.c_char_p),
+        # include/psfm_knobs.h
+        "psfm_knob_count": ([], c_int),
+        "psfm_knob_name": ([c_int], ctypes.c_char_p),
+        "psfm_knob_default": ([c_int], c_int),
+        "psfm_knob_value": ([c_int], c_int),
+        "psfm_knob_set": ([ctypes.c_char_p, c_int], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -192,7 +200,7 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_tiles_per_image", "psfm_last_error", "psfm_version", "psfm_k12_stamps",
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
-            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
+            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_bn_act_resident", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
             "psfm_add_relu_fwd", "psfm_relu_mask_bwd",
             "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",
             "psfm_upcat_ws_floats",
@@ -202,7 +210,29 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_pc_compose_bwd", "psfm_pc_fwd", "psfm_pc_bwd", "psfm_pc_last_error",
             "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_gather_frames",
             "psfm_augment_last_error",
-            "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error")
+            "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error",
+            "psfm_knob_count", "psfm_knob_name", "psfm_knob_default", "psfm_knob_value", "psfm_knob_set")
+
+
+def knobs():
+    """{name: (value, default)} of the library's kernel-selection knobs (include/psfm_knobs.h): read
+    once from PSFM_<NAME> when the library loaded, changed only through set_knob."""
+    L = lib()
+    return {L.psfm_knob_name(i).decode(): (L.psfm_knob_value(i), L.psfm_knob_default(i))
+            for i in range(L.psfm_knob_count())}
+
+
+def nondefault_knobs():
+    """The knobs whose value differs from the default ({} on the product configuration)."""
+    return {k: v for k, (v, d) in knobs().items() if v != d}
+
+
+def set_knob(name, value):
+    """Set a knob (A/B tools, tests of a non-default form); returns the previous value."""
+    prev = knobs()[name][0]
+    if lib().psfm_knob_set(name.encode(), int(value)) != 0:
+        raise ValueError(f"knob {name}: value {value} out of range")
+    return prev
 
 
 def check(rc, what):
@@ -239,7 +269,51 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+# HIP-graph captures in progress in this process (any thread: autograd runs CUDA backward nodes on
+# its own device threads).  torch.cuda.CUDAGraph.capture_begin / capture_end are wrapped once, at
+# import, to count them.
+_ACTIVE_CAPTURES = 0
+_CAPTURE_LOCK = threading.Lock()
+
+
+def _install_capture_hooks():
+    G = torch.cuda.CUDAGraph
+    if getattr(G, "_psfm_counted", False):
+        return
+    begin, end = G.capture_begin, G.capture_end
+
+    def capture_begin(self, *a, **k):
+        global _ACTIVE_CAPTURES
+        r = begin(self, *a, **k)
+        with _CAPTURE_LOCK:
+            _ACTIVE_CAPTURES += 1
+        return r
+
+    def capture_end(self, *a, **k):
+        global _ACTIVE_CAPTURES
+        with _CAPTURE_LOCK:
+            _ACTIVE_CAPTURES = max(0, _ACTIVE_CAPTURES - 1)
+        return end(self, *a, **k)
+
+    G.capture_begin, G.capture_end, G._psfm_counted = capture_begin, capture_end, True
+
+
+_install_capture_hooks()
+
+
 def stream(device):
+    """torch's current HIP stream of `device`, for a launch through the C-ABI.  Refuses (Python
+    RuntimeError, before anything is launched) to launch on a stream that is NOT capturing while a
+    HIP-graph capture is in progress: that is a backward whose forward ran outside the capture
+    (PyTorch-ROCm runs a node's backward on its forward's stream) — HIP would otherwise record
+    nothing for it and segfault in capture_end."""
+    if _ACTIVE_CAPTURES and not torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(
+            "psfm: a HIP kernel would launch on a stream outside the HIP-graph capture in progress "
+            f"(stream {torch.cuda.current_stream(device).cuda_stream:#x} is not capturing).  This happens when an "
+            "op's backward is captured but its forward ran on another stream (autograd runs the backward "
+            "on the forward's stream): run the forward inside the same capture (or on the capture stream), "
+            "as DDPTrainer.capture does")
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

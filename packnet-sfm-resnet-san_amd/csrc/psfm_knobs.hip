@@ -1,0 +1,100 @@
+// psfm_knobs.hip — the kernel-selection knobs (include/psfm_knobs.h): one table, filled from
+// PSFM_<NAME> once when the library is loaded, changed afterwards only through psfm_knob_set.
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/psfm_knobs.h"
+#include "psfm_knobs.h"
+
+#ifndef PSFM_K12_PRIO_DEFAULT
+// K12 wave priority: mode 2 (p-eval at priority 0, the rest at 2; profiles/r04/prio)
+#define PSFM_K12_PRIO_DEFAULT 2
+#endif
+
+#ifndef PSFM_BN_RES_MAXM_DEFAULT
+#define PSFM_BN_RES_MAXM_DEFAULT 8192
+#endif
+
+namespace {
+
+struct KnobDef {
+    const char* name;
+    int def, lo, hi;
+    const char* values;  // comma-separated names of the values lo.. (empty: integers only)
+    int value;
+};
+
+#ifdef PSFM_AB_VARIANTS
+constexpr int P3D_DX_HI = 3;
+#else
+constexpr int P3D_DX_HI = 2;
+#endif
+
+KnobDef g_knobs[psfm::KNOB_COUNT] = {
+    {"K12_PRIO", PSFM_K12_PRIO_DEFAULT, 0, 2, "", PSFM_K12_PRIO_DEFAULT},
+    {"K12_PARTS", 0, 0, 8, "auto", 0},
+    {"P3D_FWD", 0, 0, 2, "auto,mfma,valu", 0},
+    {"P3D_DX", 0, 0, P3D_DX_HI, "auto,mfma,cl,mfmag", 0},
+    {"P3D_DW", 0, 0, 1, "auto,generic", 0},
+    {"GN_PATH", 0, 0, 1, "resident,twopass", 0},
+    {"BN_PATH", 0, 0, 1, "resident,threepass", 0},
+    {"BN_RES_MAXM", PSFM_BN_RES_MAXM_DEFAULT, 0, 8192, "", PSFM_BN_RES_MAXM_DEFAULT},
+};
+
+// value of a knob's environment string: one of its names (position = value) or an integer
+bool parse(const KnobDef& k, const char* s, int& out) {
+    const size_t n = strlen(s);
+    int idx = k.lo;
+    for (const char* p = k.values; *p; ++idx) {
+        const char* e = strchr(p, ',');
+        const size_t len = e ? (size_t)(e - p) : strlen(p);
+        if (len == n && strncmp(p, s, n) == 0) {
+            out = idx;
+            return true;
+        }
+        if (!e) break;
+        p = e + 1;
+    }
+    char* end = nullptr;
+    const long v = strtol(s, &end, 10);
+    if (end == s || *end) return false;
+    out = (int)v;
+    return true;
+}
+
+__attribute__((constructor)) void load_knobs() {
+    for (KnobDef& k : g_knobs) {
+        char var[64] = "PSFM_";
+        strncat(var, k.name, sizeof(var) - 6);
+        const char* s = getenv(var);
+        int v;
+        if (s && parse(k, s, v) && v >= k.lo && v <= k.hi) k.value = v;
+    }
+}
+
+}  // namespace
+
+namespace psfm {
+int knob(Knob k) { return g_knobs[k].value; }
+}  // namespace psfm
+
+extern "C" {
+
+int psfm_knob_count(void) { return psfm::KNOB_COUNT; }
+const char* psfm_knob_name(int i) { return i >= 0 && i < psfm::KNOB_COUNT ? g_knobs[i].name : nullptr; }
+int psfm_knob_default(int i) { return i >= 0 && i < psfm::KNOB_COUNT ? g_knobs[i].def : 0; }
+int psfm_knob_value(int i) { return i >= 0 && i < psfm::KNOB_COUNT ? g_knobs[i].value : 0; }
+
+int psfm_knob_set(const char* name, int value) {
+    if (!name) return -1;
+    for (KnobDef& k : g_knobs) {
+        if (strcmp(k.name, name) == 0) {
+            if (value < k.lo || value > k.hi) return -1;
+            k.value = value;
+            return 0;
+        }
+    }
+    return -1;
+}
+
+}  // extern "C"

@@ -20,6 +20,9 @@
 #include <string>
 
 #include "../../include/psfm_netops.h"
+#include "psfm_knobs.h"
+
+using namespace psfm;
 
 namespace {
 
@@ -620,6 +623,285 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
     }
     ROW_LOOP_END
 }
+
+// ------------------------------------------------------------------------------------------
+// Resident BatchNorm: ONE launch each way for the small encoder layers (ResNet layer2-4 at
+// 192x640: M = N*H*W <= 7680 rows).  A workgroup owns 8 channels and ALL M rows of them: thread t
+// holds rows t, t + NTH, ... (RPT 16-byte row vectors, <= 8 per tensor) in registers, so the batch
+// statistics (two passes over the registers: mean, then sum (x - mean)^2 — no E[x^2] - mean^2
+// cancellation), the running-stat update and the apply need no other workgroup, and the backward's
+// dgamma / dbeta are complete in the workgroup (no partial rows, no finish kernel).  Reductions: xor
+// butterflies within the wave, then the waves' rows in order in fp64 — fixed order, deterministic.
+// The workgroup -> channel-block map is XCD-aware (workgroup w runs on XCD w % 8; an XCD gets a
+// contiguous channel range, so the blocks sharing a 128-byte row line mostly share an L2).
+// Replaces MIOpen's 3 + 3 BN kernels and the ReLU / add+ReLU / ReLU-mask passes around them.
+// ------------------------------------------------------------------------------------------
+constexpr int BNR_MAXT = 1024;  // threads per workgroup (<= 16 waves)
+constexpr int BNR_MAXM = 8 * BNR_MAXT;
+
+struct BNRArgs {
+    const uint16_t* x;
+    const uint16_t* res;
+    const uint16_t* dy;
+    const uint16_t* y;
+    const float* gamma;
+    const float* beta;
+    float* run_mean;
+    float* run_var;
+    float* save_mean;
+    float* save_invstd;
+    uint16_t* out;   // y (fwd) / dx (bwd)
+    uint16_t* dres;  // bwd, may be null
+    float* dgamma;
+    float* dbeta;
+    float momentum, eps;
+    int M, C, relu, nb;  // nb = C / 8 channel blocks = workgroups
+};
+
+__device__ __forceinline__ int bnr_block(int w, int nb) { return (nb % 8 == 0) ? (w % 8) * (nb / 8) + w / 8 : w; }
+
+// per-channel totals over the workgroup of K per-thread partials -> tot[K] (fp64, every thread
+// reads them after the call).  Within a wave: xor butterflies 1 / 2 (DPP quad_perm), 4 (DPP
+// row_half_mirror), 8 (DPP row_mirror) — every lane of a 16-lane row then holds the row sum — and
+// 16 / 32 (lane shuffles); then the waves' sums in order in fp64.  Fixed order: deterministic.
+// red: LDS [16][K] floats.
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+    switch (ctrl_sel) {  // compile-time after unrolling
+        case 0: return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+        case 1: return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+        case 2: return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+        default: return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void bnr_reduce(float (&v)[K], float* red, double* tot) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = dpp_add(v[k], st);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        v[k] += __shfl_xor(v[k], 16, 64);
+        v[k] += __shfl_xor(v[k], 32, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[w * K + k] = v[k];
+    }
+    __syncthreads();
+    if (t < K) {
+        float part[BNR_MAXT / 64];
+#pragma unroll
+        for (int ww = 0; ww < BNR_MAXT / 64; ++ww) part[ww] = ww < nw ? red[ww * K + t] : 0.0f;
+        double s = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < BNR_MAXT / 64; ++ww) s += (double)part[ww];
+        tot[t] = s;
+    }
+    __syncthreads();
+}
+
+// relu-mask a packed bf16 row vector by the forward output: ATen threshold_backward (y <= 0 -> 0)
+__device__ __forceinline__ uint4 relu_mask4(uint4 g, uint4 y) {
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, vw[4] = {y.x, y.y, y.z, y.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t lo = (__uint_as_float(vw[k] << 16) <= 0.0f) ? 0u : 0x0000ffffu;
+        const uint32_t hi = (__uint_as_float(vw[k] & 0xffff0000u) <= 0.0f) ? 0u : 0xffff0000u;
+        o[k] = gw[k] & (lo | hi);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ void unpack8f(const uint4 q, float (&v)[8]) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+}
+
+template <int RPT, bool RES>
+__global__ __launch_bounds__(BNR_MAXT) void k_bnr_fwd(BNRArgs a) {
+    __shared__ float red[16 * 16];
+    __shared__ double tot[16];
+    const int t = threadIdx.x, NTH = blockDim.x;
+    const int c0 = bnr_block(blockIdx.x, a.nb) * 8;
+    uint4 xv[RPT], rv[RES ? RPT : 1];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {  // every load issued before the first use (clamped rows, masked below)
+        const size_t o = (size_t)min(t + k * NTH, a.M - 1) * a.C + c0;
+        xv[k] = *reinterpret_cast<const uint4*>(a.x + o);
+        if constexpr (RES) rv[k] = *reinterpret_cast<const uint4*>(a.res + o);
+    }
+    // one reduction of sums shifted by the channel's first value K (sum (x - K), sum (x - K)^2): the
+    // variance E[(x-K)^2] - E[x-K]^2 keeps no E[x^2] - mean^2 cancellation when |mean| >> std
+    float kk[8];
+    unpack8f(*reinterpret_cast<const uint4*>(a.x + c0), kk);
+    float s[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        if (t + k * NTH >= a.M) break;
+        float v[8];
+        unpack8f(xv[k], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float d = v[i] - kk[i];
+            s[i] += d;
+            s[8 + i] += d * d;
+        }
+    }
+    bnr_reduce<16>(s, red, tot);
+    const double inv_m = 1.0 / (double)a.M;
+    float mu[8];
+    double var8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double m1 = tot[i] * inv_m;
+        mu[i] = (float)((double)kk[i] + m1);
+        var8[i] = fmax(tot[8 + i] * inv_m - m1 * m1, 0.0);
+    }
+    float sc[8], sh[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double var = var8[i];
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        sc[i] = a.gamma[c0 + i] * invstd;
+        sh[i] = a.beta[c0 + i] - mu[i] * sc[i];
+        if (t == i) {
+            a.save_mean[c0 + i] = mu[i];
+            a.save_invstd[c0 + i] = invstd;
+            if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
+                const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
+                a.run_mean[c0 + i] = (float)((1.0 - a.momentum) * a.run_mean[c0 + i] + a.momentum * (double)mu[i]);
+                a.run_var[c0 + i] = (float)((1.0 - a.momentum) * a.run_var[c0 + i] + a.momentum * unb);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = t + k * NTH;
+        if (row >= a.M) break;
+        float v[8];
+        unpack8f(xv[k], v);
+        float r[8];
+        if constexpr (RES) unpack8f(rv[k], r);
+        Vec<8> o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float w = v[i] * sc[i] + sh[i];
+            if constexpr (RES) w = bfround(w) + r[i];  // autocast: bn(x) is a bf16 tensor before the add
+            if (a.relu) w = w <= 0.0f ? 0.0f : w;      // ATen relu (NaN propagates)
+            o.v[i] = w;
+        }
+        st_bf<8>(a.out + (size_t)row * a.C + c0, o);
+    }
+}
+
+// backward: x and the masked dy held (16 VGPRs per row vector pair): RPT >= 8 runs 512-thread
+// workgroups (256 VGPRs; 1024 threads x RPT 8 spilled at the 128-VGPR limit)
+constexpr int bnr_bwd_maxt(int rpt) { return rpt >= 8 ? BNR_MAXT / 2 : BNR_MAXT; }
+
+template <int RPT>
+__global__ __launch_bounds__(bnr_bwd_maxt(RPT)) void k_bnr_bwd(BNRArgs a) {
+    __shared__ float red[16 * 16];
+    __shared__ double tot[16];
+    const int t = threadIdx.x, NTH = blockDim.x;
+    const int c0 = bnr_block(blockIdx.x, a.nb) * 8;
+    uint4 gv[RPT], xv[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const size_t o = (size_t)min(t + k * NTH, a.M - 1) * a.C + c0;
+        gv[k] = *reinterpret_cast<const uint4*>(a.dy + o);
+        xv[k] = *reinterpret_cast<const uint4*>(a.x + o);
+        if (a.relu) gv[k] = relu_mask4(gv[k], *reinterpret_cast<const uint4*>(a.y + o));
+    }
+    float mu[8], is[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        mu[i] = a.save_mean[c0 + i];
+        is[i] = a.save_invstd[c0 + i];
+    }
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        if (t + k * NTH >= a.M) break;
+        float g[8], v[8];
+        unpack8f(gv[k], g);
+        unpack8f(xv[k], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            acc[i] += g[i];
+            acc[8 + i] += g[i] * (v[i] - mu[i]);
+        }
+    }
+    bnr_reduce<16>(acc, red, tot);
+    // dx = k1 (g - k2 - (x - mu) k3) with k1 = gamma invstd, k2 = sum g / M, k3 = sum g (x - mu) invstd^2 / M,
+    // folded (fp64) into dx = kg g + kx x + k0: three live coefficients per channel instead of five
+    const double inv_m = 1.0 / (double)a.M;
+    float kg[8], kx[8], k0[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double isd = is[i], k1 = (double)(a.gamma[c0 + i] * is[i]);
+        const double k2 = tot[i] * inv_m, k3 = tot[8 + i] * isd * isd * inv_m;
+        kg[i] = (float)k1;
+        kx[i] = (float)(-k1 * k3);
+        k0[i] = (float)(k1 * (k3 * (double)mu[i] - k2));
+        if (t == i) {
+            a.dbeta[c0 + i] = (float)tot[i];
+            a.dgamma[c0 + i] = (float)(tot[8 + i] * isd);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int row = t + k * NTH;
+        if (row >= a.M) break;
+        const size_t o = (size_t)row * a.C + c0;
+        float g[8], v[8];
+        unpack8f(gv[k], g);
+        unpack8f(xv[k], v);
+        Vec<8> d;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d.v[i] = fmaf(kg[i], g[i], fmaf(kx[i], v[i], k0[i]));
+        st_bf<8>(a.out + o, d);
+        if (a.dres) *reinterpret_cast<uint4*>(a.dres + o) = gv[k];
+    }
+}
+
+// resident geometry: RPT = the fewest row vectors per thread with RPT x (the direction's thread
+// limit) >= M (forward RPT 1-8 at <= 1024 threads; backward RPT 1-4 at 1024, 8 / 16 at 512), NTH =
+// ceil(M / RPT) rounded up to whole waves; false when the layer does not fit
+struct BNRGeo {
+    int rpt, nth;
+};
+inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
+    if (C % 8 || M < 1 || M > std::min(BNR_MAXM, knob(KNOB_BN_RES_MAXM))) return false;
+    for (int r = 1; r <= (bwd ? 16 : 8); r *= 2) {
+        const int maxt = bwd ? bnr_bwd_maxt(r) : BNR_MAXT;
+        if ((long long)r * maxt >= M) {
+            g.rpt = r;
+            g.nth = std::max(64, ((M + r - 1) / r + 63) / 64 * 64);
+            return true;
+        }
+    }
+    return false;
+}
+
+#define BNR_FWD_CASE(R)                                                                                  \
+    case R:                                                                                              \
+        if (res) hipLaunchKernelGGL((k_bnr_fwd<R, true>), dim3(a.nb), dim3(g.nth), 0, st, a);           \
+        else hipLaunchKernelGGL((k_bnr_fwd<R, false>), dim3(a.nb), dim3(g.nth), 0, st, a);              \
+        break
+#define BNR_BWD_CASE(R)                                                                                  \
+    case R: hipLaunchKernelGGL((k_bnr_bwd<R>), dim3(a.nb), dim3(g.nth), 0, st, a); break
 
 // ------------------------------------------------------------------------------------------
 // GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW),
@@ -1727,10 +2009,16 @@ __global__ __launch_bounds__(NT) void k_gnp_bwd_apply(GNArgs a) {
     }
 }
 
-// PSFM_GN_PIPE=0 (A/B): the unpipelined two-pass kernels
+// the software-pipelined two-pass GroupNorm (k_gnp_*) is the product's form for VEC = 8; the
+// unpipelined k_gn_*<8> (bitwise the same results, 208 vs 211 img/s on PackNet01,
+// profiles/r04/gn) is built into A/B variant libraries only (tools/build_variants.sh)
 static bool gnp_enabled() {
+#ifdef PSFM_AB_VARIANTS
     const char* e = getenv("PSFM_GN_PIPE");
     return !(e && e[0] == '0');
+#else
+    return true;
+#endif
 }
 
 template <typename A>
@@ -1752,13 +2040,7 @@ inline int check_vec(int C, const char* what) {
 
 // GN geometry: the grid stays <= TARGET_BLOCKS workgroups over the N samples
 inline Geo gn_geometry(int N, int HW, int C) {
-    // PSFM_GN_BLOCKS (A/B): the two-pass grid target, TARGET_BLOCKS by default
-    static const int tb = [] {
-        const char* e = getenv("PSFM_GN_BLOCKS");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 ? v : TARGET_BLOCKS;
-    }();
-    return geometry(HW, C, pick_vec(C), std::max(1, tb / N));
+    return geometry(HW, C, pick_vec(C), std::max(1, TARGET_BLOCKS / N));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2049,13 +2331,37 @@ int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void
     return 0;
 }
 
+// the resident path where it fits is the default; the BN_PATH knob = 1 forces the three-pass kernels
+static bool bnr_path() { return knob(KNOB_BN_PATH) == 0; }
+
+int psfm_bn_act_resident(int M, int C) {
+    BNRGeo g;
+    return bnr_path() && bnr_geometry(M, C, g) ? 1 : 0;
+}
+
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
                     float* save_invstd, float* ws, void* stream) {
-    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !ws || M < 1 || C < 1)
+    if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || M < 1 || C < 1)
         return fail(-1, "bn_act_fwd: bad arguments");
     if ((run_mean == nullptr) != (run_var == nullptr)) return fail(-1, "bn_act_fwd: running stats must pair");
     if (int e = check_vec(C, "bn_act_fwd")) return e;
+    BNRGeo rgeo;
+    if (bnr_path() && bnr_geometry(M, C, rgeo)) {  // one launch (resident)
+        BNRArgs a{};
+        a.x = static_cast<const uint16_t*>(x);
+        a.res = static_cast<const uint16_t*>(res);
+        a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
+        a.save_mean = save_mean, a.save_invstd = save_invstd;
+        a.out = static_cast<uint16_t*>(y);
+        a.momentum = momentum, a.eps = eps, a.M = M, a.C = C, a.relu = relu, a.nb = C / 8;
+        hipStream_t st = (hipStream_t)stream;
+        const BNRGeo& g = rgeo;
+        switch (g.rpt) { BNR_FWD_CASE(1); BNR_FWD_CASE(2); BNR_FWD_CASE(4); BNR_FWD_CASE(8); }
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
+    if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
     BNArgs a{};
@@ -2085,10 +2391,27 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, void* stream) {
-    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta || !ws ||
+    if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta ||
         M < 1 || C < 1 || (relu && !y))
         return fail(-1, "bn_act_bwd: bad arguments");
     if (int e = check_vec(C, "bn_act_bwd")) return e;
+    BNRGeo rgeo;
+    if (bnr_path() && bnr_geometry(M, C, rgeo, true)) {  // one launch (resident)
+        BNRArgs a{};
+        a.dy = static_cast<const uint16_t*>(dy);
+        a.y = static_cast<const uint16_t*>(y);
+        a.x = static_cast<const uint16_t*>(x);
+        a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
+        a.out = static_cast<uint16_t*>(dx);
+        a.dres = static_cast<uint16_t*>(dres);
+        a.dgamma = dgamma, a.dbeta = dbeta, a.M = M, a.C = C, a.relu = relu, a.nb = C / 8;
+        hipStream_t st = (hipStream_t)stream;
+        const BNRGeo& g = rgeo;
+        switch (g.rpt) { BNR_BWD_CASE(1); BNR_BWD_CASE(2); BNR_BWD_CASE(4); BNR_BWD_CASE(8); BNR_BWD_CASE(16); }
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
+    if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
     BNArgs a{};
@@ -2116,11 +2439,8 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
     return 0;
 }
 
-// the resident path is the default; PSFM_GN_PATH=twopass forces the two-pass kernels (A/B, tests)
-static bool gnr_enabled() {
-    const char* e = getenv("PSFM_GN_PATH");
-    return !(e && std::string(e) == "twopass");
-}
+// the resident path is the default; the GN_PATH knob = 1 forces the two-pass kernels (A/B, tests)
+static bool gnr_enabled() { return knob(KNOB_GN_PATH) == 0; }
 static void gnr_common(GNRArgs& r, const GNRGeo& rg, const GNArgs& a) {
     r.x = a.x, r.res = a.res, r.bias = a.bias, r.bias_bf16 = a.bias_bf16, r.gamma = a.gamma, r.beta = a.beta;
     r.save_mean = a.save_mean, r.save_invstd = a.save_invstd, r.out = a.out, r.eps = a.eps;

@@ -29,6 +29,9 @@
 #include <string>
 
 #include "../../include/psfm_pack3d.h"
+#include "psfm_knobs.h"
+
+using namespace psfm;
 
 namespace {
 
@@ -1506,13 +1509,12 @@ int psfm_p3d_fwd(const psfm_p3d_desc* t, const void* x, const float* w, const fl
                      xmax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     // the matrix-core form (k_p3d_fwd_mfma): bf16, r = 2, channels_last x with 16-byte 8-channel runs,
     // 32-k chunks, channels_last y (pack: 8-byte 4-channel stores); PSFM_P3D_FWD=mfma / valu (A/B)
-    const char* fe = getenv("PSFM_P3D_FWD");
+    const int fknob = knob(KNOB_P3D_FWD);
     // default: d = 8 (PackNet01) every layer, d = 4 (PackNetSAN01) unpack layers only — with 4 of the
     // 16 MFMA columns useful per part the d = 4 pack layers run faster on the VALU kernel
     // (profiles/r04/p3d/ab_fwd_*: first PackNet01 layer 449 -> 400-421 us, unpack 96x320 133 -> 62;
     // first PackNetSAN01 layer 90 vs 124-136)
-    const bool fwant = fe ? std::string(fe) == "mfma"
-                          : (P3D_FWD_MFMA_DEFAULT || t->d == 8 || t->mode == PSFM_P3D_UNPACK);
+    const bool fwant = fknob ? fknob == 1 : (P3D_FWD_MFMA_DEFAULT || t->d == 8 || t->mode == PSFM_P3D_UNPACK);
     const int64_t xmaxm = t->mode == PSFM_P3D_PACK ? xmax
                                                    : (int64_t)(t->B - 1) * a.xs[0] + (int64_t)(a.K - 1) * a.xs[1] +
                                                          (int64_t)(a.Hv - 1) * a.xs[2] + (int64_t)(a.Wv - 1) * a.xs[3];
@@ -1591,14 +1593,13 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         // with even strides (else two 2-byte stores)
         const bool xpair = a.xs[1] != 1 || (a.xs[0] % 2 == 0 && a.xs[2] % 2 == 0 && a.xs[3] % 2 == 0 &&
                                             (reinterpret_cast<uintptr_t>(dx) & 3) == 0);
-        // A/B knob: "mfma" (or "mfma1" / "mfma2" / "mfma4": chunks per workgroup) / "cl" (the VALU k-pair kernel)
-        const char* env = getenv("PSFM_P3D_DX");
-        const std::string form = env ? env : "";
+        // the P3D_DX knob (A/B): 1 the matrix-core form, 2 the VALU k-pair kernel (3 grouped staging, A/B builds)
+        const int dknob = knob(KNOB_P3D_DX);
         // default: the matrix-core form for unpack layers (2x the generic kernel at every PackNet
         // shape), the VALU k-pair kernel for pack layers (the matrix-core form's staging issues 1.5x
         // its per-lane line accesses: 0.85-1.0 vs 0.54 ms on the first PackNet01 layer,
         // profiles/r04/p3d/)
-        const bool want = env ? form.compare(0, 4, "mfma") == 0 : t->mode == PSFM_P3D_UNPACK || P3D_DX_MFMA_DEFAULT;
+        const bool want = dknob ? dknob != 2 : t->mode == PSFM_P3D_UNPACK || P3D_DX_MFMA_DEFAULT;
         // unpack layers: channels_last dy (2 Hv x 2 Wv, d K / 4 channels), 4-byte sub-pixel words
         const int64_t umax = (int64_t)(t->d * a.K / 4 - 1) * a.ys[1] + (int64_t)(2 * a.Hv - 1) * a.ys[2] +
                              (int64_t)(2 * a.Wv - 1) * a.ys[3];
@@ -1611,10 +1612,12 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
             // 8-k chunks per workgroup: 2 when that still leaves >= 1024 workgroups (unpack 96x320 / 48x160
             // layers: 128 vs 138 us), else 1 (the small layers want the workgroups)
             int cpw = a.K % 16 == 0 && (int64_t)gxn * gyn * a.B * (a.K / 16) >= 1024 ? 2 : 1;
-            if (form.size() == 5 && (form[4] == '1' || form[4] == '2' || form[4] == '4') && a.K % (8 * (form[4] - '0')) == 0)
-                cpw = form[4] - '0';
-            const bool grp = t->mode == PSFM_P3D_PACK && a.K % 32 == 0 && form == "mfmag";
+#ifdef PSFM_AB_VARIANTS
+            const bool grp = t->mode == PSFM_P3D_PACK && a.K % 32 == 0 && dknob == 3;
             if (grp) cpw = 4;
+#else
+            constexpr bool grp = false;
+#endif
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / (8 * cpw))));
 #define P3D_DXM(ND, CPW)                                                                                              \
     do {                                                                                                              \
@@ -1624,15 +1627,15 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
             hipLaunchKernelGGL((k_p3d_bwd_x_mfma<ND, CPW, PSFM_P3D_UNPACK>), g1, dim3(256), 0, st, a, gxn, gyn);      \
     } while (0)
             if (grp) {
+#ifdef PSFM_AB_VARIANTS
                 if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_mfma<4, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
                 else hipLaunchKernelGGL((k_p3d_bwd_x_mfma<8, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
+#endif
             } else if (t->d == 4) {
-                if (cpw == 4) P3D_DXM(4, 4);
-                else if (cpw == 2) P3D_DXM(4, 2);
+                if (cpw == 2) P3D_DXM(4, 2);
                 else P3D_DXM(4, 1);
             } else {
-                if (cpw == 4) P3D_DXM(8, 4);
-                else if (cpw == 2) P3D_DXM(8, 2);
+                if (cpw == 2) P3D_DXM(8, 2);
                 else P3D_DXM(8, 1);
             }
 #undef P3D_DXM
@@ -1677,13 +1680,13 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
                               (int64_t)(a.Hv - 1) * a.xs[2] + (int64_t)(a.Wv - 1) * a.xs[3];
         const int64_t uymax = (int64_t)(t->B - 1) * a.ys[0] + (int64_t)(t->d * a.K / 4 - 1) * a.ys[1] +
                               (int64_t)(2 * a.Hv - 1) * a.ys[2] + (int64_t)(2 * a.Wv - 1) * a.ys[3];
-        const char* dwe = getenv("PSFM_P3D_DW");
+        const bool dw_generic = knob(KNOB_P3D_DW) == 1;
         const bool umfma = t->mode == PSFM_P3D_UNPACK && t->dtype == PSFM_P3D_BF16 && t->r == 2 && a.K % 32 == 0 &&
                            a.xs[1] == 1 && a.xs[0] % 8 == 0 && a.xs[2] % 8 == 0 && a.xs[3] % 8 == 0 && a.xs[0] >= 0 &&
                            a.xs[2] >= 0 && a.xs[3] >= 0 && a.ys[1] == 1 && a.ys[0] % 8 == 0 && a.ys[2] % 8 == 0 &&
                            a.ys[3] % 8 == 0 && a.ys[0] >= 0 && a.ys[2] >= 0 && a.ys[3] >= 0 && uxmax < INT32_MAX - 64 &&
                            uymax < INT32_MAX - 64 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-                           (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && MFMA_DW && !(dwe && std::string(dwe) == "generic");
+                           (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && MFMA_DW && !dw_generic;
         if (mfma) {
             grid = grid_lin(aw, 4, 16, 32, P3D_DW_CPW);
             if (t->d == 4) hipLaunchKernelGGL(k_p3d_bwd_w_mfma<4>, grid, dim3(NTH), 0, st, aw);

@@ -26,12 +26,10 @@
 #include "psfm_sweep.h"
 #include "psfm_fused.h"
 
-#ifndef PSFM_K12_PRIO_DEFAULT
-// fused::Args::prio_mode when PSFM_K12_PRIO is unset: 2 = the younger wave of a SIMD pair one
-// level up in its p-eval (A/B on one box, profiles/r04/prio: kbench B=4 101.0 -> 98.0 us, B=6
-// 141.3 -> 135.4 us; in the step 95.6-97.3 -> 93.8-94.1 us); 0 = off
-#define PSFM_K12_PRIO_DEFAULT 2
-#endif
+// fused::Args::prio_mode = the K12_PRIO knob (psfm_knobs.hip, default 2 = the younger wave of a SIMD
+// pair one level up in its p-eval; A/B on one box, profiles/r04/prio: kbench B=4 101.0 -> 98.0 us,
+// B=6 141.3 -> 135.4 us; in the step 95.6-97.3 -> 93.8-94.1 us); 0 = off
+#include "psfm_knobs.h"
 
 using namespace psfm;
 
@@ -1065,15 +1063,13 @@ int simd_count() {
 }
 void k12_priority(fused::Args& fa, long waves) {
     const int simds = simd_count();
-    const char* e = getenv("PSFM_K12_PRIO");
-    fa.prio_mode = e ? atoi(e) : PSFM_K12_PRIO_DEFAULT;
+    fa.prio_mode = knob(KNOB_K12_PRIO);
     fa.young_from = simds / 8;  // SIMDs per XCD (8 XCDs)
     if (waves > 2L * simds || fa.prio_mode != 2) fa.prio_mode = 0;
     // XCD dealing: with fewer than 8 images each image's bands are split over 8 / B XCDs, every
-    // XCD sweeping its part for all scales (sweep::work_item_parts); PSFM_K12_PARTS overrides (A/B)
-    const char* pe = getenv("PSFM_K12_PARTS");
-    const int B = fa.p.B;
-    fa.xcd_parts = pe ? std::max(1, atoi(pe)) : (B < 8 ? 8 / B : 1);
+    // XCD sweeping its part for all scales (sweep::work_item_parts); the K12_PARTS knob overrides (A/B)
+    const int B = fa.p.B, parts = knob(KNOB_K12_PARTS);
+    fa.xcd_parts = parts > 0 ? parts : (B < 8 ? 8 / B : 1);
 }
 
 int fwd_units(const psfm_params* p) {

@@ -24,9 +24,11 @@ from ... import _hip
 ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
 # Which layer kinds run fused, from the A/B of the ResNetSAN01 + PoseNet step on MI355X
 # (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
-# chain (972 -> 1025 img/s together); BatchNorm + ReLU loses to MIOpen's BN kernels (-> 981), so
-# BN stays on MIOpen.  bench.py --fused-nets overrides.
-FUSE = {"bias": True, "gn": True, "bn": False}
+# chain (972 -> 1025 img/s together).  BatchNorm: "resident" = the one-launch kernels where a
+# workgroup holds the layer (psfm_bn_act_resident: ResNet layer2-4), MIOpen's BatchNorm elsewhere
+# (the three-pass kernels lose to it on the large layers, profiles/r02/netops_ab); True = the fused
+# kernels on every shape; False = MIOpen everywhere.  bench.py --fused-nets overrides.
+FUSE = {"bias": True, "gn": True, "bn": "resident"}
 
 
 def _fusable(x, kind):
@@ -102,7 +104,8 @@ class _BNAct(torch.autograd.Function):
         mean = torch.empty(C, device=dev, dtype=torch.float32)
         invstd = torch.empty(C, device=dev, dtype=torch.float32)
         L = _hip.lib()
-        ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
+        ws = None if L.psfm_bn_act_resident(M, C) else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev,
+                                                                   dtype=torch.float32)
         _hip.check(L.psfm_bn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(weight), _hip.ptr(bias),
                                      _hip.ptr(running_mean), _hip.ptr(running_var), ctypes.c_float(momentum),
                                      ctypes.c_float(eps), M, C, int(relu), _hip.ptr(y), _hip.ptr(mean),
@@ -123,7 +126,8 @@ class _BNAct(torch.autograd.Function):
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         dw = torch.empty(C, device=dev, dtype=torch.float32)
         db = torch.empty(C, device=dev, dtype=torch.float32)
-        ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
+        ws = None if L.psfm_bn_act_resident(M, C) else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev,
+                                                                   dtype=torch.float32)
         _hip.check(L.psfm_bn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(mean),
                                      _hip.ptr(invstd), M, C, int(ctx.relu), _hip.ptr(dx), _hip.ptr(dres),
                                      _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_bwd")
@@ -171,10 +175,21 @@ def add_relu(a, b):
     return torch.relu(a + b)
 
 
+def _bn_fused_shape(x):
+    """FUSE["bn"] == "resident": only the shapes the one-launch kernels hold (psfm_bn_act_resident)."""
+    if FUSE["bn"] != "resident":
+        return True
+    N, C, H, W = x.shape
+    return bool(_hip.lib().psfm_bn_act_resident(N * H * W, C))
+
+
 def bn_act(x, bn, relu=True, residual=None):
-    """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn`."""
+    """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn` (torchvision BasicBlock
+    conv -> bn -> relu and conv -> bn -> +identity -> relu, resnet_encoder.py:61-98): ONE HIP launch
+    each way where FUSE["bn"] takes the shape, else MIOpen's BatchNorm + the add / ReLU passes."""
     if (_fusable(x, "bn") and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
-            and bn.running_mean is not None):
+            and bn.running_mean is not None and (residual is None or residual.shape == x.shape)
+            and _bn_fused_shape(x)):
         if bn.num_batches_tracked is not None:  # the graph trainer keeps these off the step
             bn.num_batches_tracked.add_(1)
         return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, float(bn.momentum),

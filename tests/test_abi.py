@@ -166,3 +166,45 @@ def test_library_carries_the_source_hash():
     assert G.library_hash() == G.source_hash(), "libpsfm_hip.so is stale: run __graft_entry__.build()"
     from packnet_sfm_amd import _hip
     assert _hip.lib().psfm_version().decode().endswith("src=" + G.source_hash())
+
+
+def test_bn_resident_shapes(hip):
+    """psfm_bn_act_resident (host-only): the one-launch BatchNorm holds 8-channel blocks of up to
+    8192 rows — ResNet18 layer2-4 at B = 4, 192x640 — and nothing wider or larger."""
+    L = hip.lib()
+    for M, C in ((7680, 128), (1920, 256), (480, 512), (8192, 8), (1, 8)):
+        assert L.psfm_bn_act_resident(M, C) == 1, (M, C)
+    for M, C in ((8193, 8), (30720, 64), (122880, 64), (480, 12), (0, 64)):
+        assert L.psfm_bn_act_resident(M, C) == 0, (M, C)
+
+
+def test_knobs_are_read_once_and_set_explicitly(hip):
+    """include/psfm_knobs.h: every kernel-selection knob has a name, a default and a range; the
+    product configuration has no non-default knob; set / restore work; out-of-range values and
+    unknown names are refused."""
+    k = hip.knobs()
+    assert set(k) == {"K12_PRIO", "K12_PARTS", "P3D_FWD", "P3D_DX", "P3D_DW", "GN_PATH", "BN_PATH", "BN_RES_MAXM"}
+    assert hip.nondefault_knobs() == {}
+    prev = hip.set_knob("BN_PATH", 1)
+    try:
+        assert hip.knobs()["BN_PATH"] == (1, 0) and hip.nondefault_knobs() == {"BN_PATH": 1}
+    finally:
+        hip.set_knob("BN_PATH", prev)
+    assert hip.nondefault_knobs() == {}
+    L = hip.lib()
+    assert L.psfm_knob_set(b"BN_PATH", 7) == -1 and L.psfm_knob_set(b"NO_SUCH", 0) == -1
+    with pytest.raises(ValueError):
+        hip.set_knob("P3D_DX", 3)   # the grouped-staging dx form exists in A/B variant builds only
+
+
+def test_knob_environment_is_parsed_at_load():
+    """PSFM_<NAME> is read when the library loads (names or integers; invalid values keep the
+    default) — in a fresh process, since this one has loaded the library already."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import torch, packnet_sfm_amd; "
+            "from packnet_sfm_amd import _hip; print(sorted(_hip.nondefault_knobs().items()))" % ROOT)
+    env = dict(os.environ, PSFM_P3D_FWD="valu", PSFM_K12_PRIO="0", PSFM_GN_PATH="bogus", PSFM_BN_PATH="9")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "[('K12_PRIO', 0), ('P3D_FWD', 2)]"

@@ -477,3 +477,62 @@ def test_captured_bucket_unpack_uses_the_eagerly_agreed_presence():
         assert "must be agreed in an eager step" in r["msgs"][0]
         assert r["n_eager"] == 1 and r["n_capt"] == 0
     assert torch.equal(res[0]["g2"], res[1]["g2"])   # rank 1 had no gradient: it gets the average too
+
+
+# ---------------------------------------------------------------------------------------------
+# bench.py --comm auto: the overlap path is chosen only when every rank's
+# short-lived probe child (trainers/comm_probe.py) passed; every rank picks the same path.
+def test_choose_comm_every_rank_reads_every_probe_status():
+    import threading
+
+    import bench
+    for rcs, want in (((0, 0), "overlap"), ((0, 1), "split"), ((124, 0), "split")):
+        store, out = dist.HashStore(), {}
+
+        def rank_fn(r):
+            out[r] = bench.choose_comm(store, r, 2, lambda port: rcs[r])
+
+        th = [threading.Thread(target=rank_fn, args=(r,)) for r in (1, 0)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert out[0] == out[1] and out[0][0] == want, (rcs, out)
+        if want == "split":
+            assert "failed" in out[0][1]
+
+
+def _torchrun_probe(extra_env, *extra):
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"), "--gpus", "2",
+           "--dist-backend", "gloo", "--probe-backend", "gloo", "--probe-only", *extra]
+    env = dict(os.environ, OMP_NUM_THREADS="1", **extra_env)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout.strip().splitlines()[-1]), out.stderr
+
+
+def test_comm_auto_probe_children_over_gloo_world2():
+    """The whole selection on CPU: two torch.distributed.run ranks, each starting its probe child
+    (own process group, the bucketed overlap path eagerly over gloo); both pass.  The run itself is
+    gloo, so it must still train with split — and says why."""
+    res, err = _torchrun_probe({})
+    assert res["world"] == 2 and res["comm"] == "split", res
+    assert "probe passed on 2 ranks" in res["comm_note"] and "gloo run" in res["comm_note"], res
+    assert err.count("[comm probe] rank") == 2, err[-2000:]
+
+
+def test_comm_auto_probe_failure_and_hang_select_split():
+    """Rank 1's child fails at once; rank 0's child then waits for its peer and is killed at the
+    timeout: both ranks see the failures and pick split."""
+    res, err = _torchrun_probe({"PSFM_TEST_PROBE_FAIL_RANK": "1"}, "--comm-probe-timeout", "20")
+    assert res["comm"] == "split" and "failed" in res["comm_note"], res
+    assert "3" in res["comm_note"] and "124" in res["comm_note"], res

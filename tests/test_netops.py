@@ -92,14 +92,31 @@ def test_bias_act_matches_torch(dev, shape, act, bias_bf16):
     assert b.grad.dtype == b.dtype
 
 
+@pytest.fixture(params=["resident", "threepass"])
+def bn_path(request, knob):
+    """Both fused BatchNorm implementations: the one-launch resident kernels (where a workgroup holds
+    the layer: M = N*H*W <= 8192, C % 8 == 0) and the three-pass kernels (knob BN_PATH = 1; the
+    only fused form of the larger layers)."""
+    knob("BN_PATH", 1 if request.param == "threepass" else 0)
+    return request.param
+
+
 @gpu
 @pytest.mark.parametrize("shape,relu,residual", [((2, 64, 48, 160), True, False),
                                                   ((4, 64, 96, 320), True, False),  # stem: 480 workgroups
                                                   ((2, 64, 24, 80), True, True),
                                                   ((4, 512, 6, 20), True, True),
                                                   ((2, 128, 12, 40), False, False),
-                                                  ((2, 12, 10, 30), True, True)])
-def test_bn_act_matches_torch(dev, shape, relu, residual):
+                                                  ((2, 12, 10, 30), True, True),
+                                                  # ResNet18 layer2-4 at B = 4, 192x640 (resident: forward
+                                                  # RPT 8 x 960 threads, backward RPT 16 x 512; RPT 2 / 1)
+                                                  ((4, 128, 24, 80), True, False),
+                                                  ((4, 128, 24, 80), True, True),
+                                                  ((4, 256, 12, 40), True, True),
+                                                  ((4, 512, 6, 20), False, False),
+                                                  ((3, 64, 7, 9), True, True),     # M = 189: a partial wave
+                                                  ((2, 8, 64, 64), True, False)])  # M = 8192: the resident limit
+def test_bn_act_matches_torch(dev, shape, relu, residual, bn_path):
     g = torch.Generator(device="cpu").manual_seed(2)
     C = shape[1]
     bn = nn.BatchNorm2d(C).to(dev).train()
@@ -135,14 +152,11 @@ def test_bn_act_matches_torch(dev, shape, relu, residual):
 
 
 @pytest.fixture(params=["resident", "twopass"])
-def gn_path(request, monkeypatch):
+def gn_path(request, knob):
     """Both GroupNorm implementations: the one-pass resident kernels (default wherever the layer
-    fits a workgroup's registers) and the two-pass statistics-rows kernels (PSFM_GN_PATH=twopass;
+    fits a workgroup's registers) and the two-pass statistics-rows kernels (knob GN_PATH = 1;
     always used for the large layers)."""
-    if request.param == "twopass":
-        monkeypatch.setenv("PSFM_GN_PATH", "twopass")
-    else:
-        monkeypatch.delenv("PSFM_GN_PATH", raising=False)
+    knob("GN_PATH", 1 if request.param == "twopass" else 0)
     return request.param
 
 
@@ -203,6 +217,70 @@ def test_fused_reductions_are_deterministic_and_rearm(dev):
     for o in outs[1:]:
         for a, b in zip(o, outs[0]):
             assert torch.equal(a, b)
+
+
+@gpu
+@pytest.mark.parametrize("shape,residual", [((4, 128, 24, 80), True), ((4, 512, 6, 20), False)])
+def test_resident_bn_is_bitwise_deterministic_and_captures(dev, shape, residual):
+    """The resident BatchNorm (one launch each way, fixed-order reductions, no atomics): eager calls
+    repeat bit for bit, and a HIP-graph capture of forward + backward replays the eager results
+    bit for bit (running statistics included)."""
+    from packnet_sfm_amd import _hip
+    N, C, H, W = shape
+    assert _hip.lib().psfm_bn_act_resident(N * H * W, C) == 1
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = _cl(torch.randn(shape, generator=g) + 0.2).to(dev, torch.bfloat16)
+    r = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) if residual else None
+    dy = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    bn = nn.BatchNorm2d(C).to(dev).train()
+    bn.num_batches_tracked = None   # as the graph trainer keeps it (no host-side counter in the graph)
+    state = [bn.running_mean.clone(), bn.running_var.clone()]
+
+    def reset():
+        bn.running_mean.copy_(state[0])
+        bn.running_var.copy_(state[1])
+
+    def step(xi):
+        y = FU.bn_act(xi, bn, relu=True, residual=r)
+        dx, dw, db = torch.autograd.grad(y, (xi, bn.weight, bn.bias), dy)
+        return [y, dx, dw, db, bn.running_mean.clone(), bn.running_var.clone()]
+
+    outs = []
+    for _ in range(2):
+        reset()
+        outs.append([t.detach().clone() for t in step(x.clone().requires_grad_(True))])
+        torch.cuda.synchronize()
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    reset()
+    xs = x.clone().requires_grad_(True)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            cap = step(xs)
+    torch.cuda.current_stream().wait_stream(side)
+    reset()
+    graph.replay()
+    torch.cuda.synchronize()
+    for a_, b_ in zip(cap, outs[0]):
+        assert torch.equal(a_, b_)
+
+
+@gpu
+def test_resident_bn_policy_keeps_miopen_for_the_large_layers(dev, monkeypatch):
+    """FUSE["bn"] == "resident" (the product default): the layers the resident kernels hold run them
+    (one HIP launch), the larger ones MIOpen's BatchNorm — the three-pass kernels lose to it there."""
+    calls = []
+    orig = FU._BNAct.apply
+    monkeypatch.setattr(FU._BNAct, "apply", lambda *a: calls.append(tuple(a[0].shape)) or orig(*a))
+    FU.FUSE["bn"] = "resident"
+    for shape in ((4, 128, 24, 80), (4, 64, 48, 160)):
+        bn = nn.BatchNorm2d(shape[1]).to(dev).train()
+        x = _cl(torch.randn(shape)).to(dev, torch.bfloat16)
+        FU.bn_act(x, bn, relu=True)
+    assert calls == [(4, 128, 24, 80)]
 
 
 @gpu
@@ -489,32 +567,45 @@ def test_gn_backward_captures_when_its_forward_ran_on_the_capture_stream(dev):
     assert torch.equal(out, ref)
 
 
+
+_CAPTURE_MISUSE = r"""
+import sys, torch, torch.nn as nn
+sys.path.insert(0, {root!r})
+import packnet_sfm_amd
+from packnet_sfm_amd.networks.layers import fused as FU
+dev = torch.device("cuda", 0)
+gn = nn.GroupNorm(16, 64).to(dev)
+x = torch.randn(6, 64, 48, 160, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+x.requires_grad_(True)
+y = FU.gn_act(x, None, gn, act=FU.ACT_ELU)          # forward on the default stream, outside any capture
+dy = torch.randn_like(y)
+torch.cuda.synchronize()
+side = torch.cuda.Stream()
+side.wait_stream(torch.cuda.current_stream())
+g = torch.cuda.CUDAGraph()
+try:
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            torch.autograd.grad(y, x, dy)           # its backward captured: the round-4 segfault sequence
+except RuntimeError as e:
+    print("REFUSED:", "outside the HIP-graph capture" in str(e) or "outside the HIP-graph capture" in repr(e.__context__))
+    sys.exit(0)
+print("NOT REFUSED")
+sys.exit(2)
+"""
+
+
 @gpu
-@pytest.mark.parametrize("residual", [False, True])
-def test_pipelined_two_pass_gn_is_bitwise_the_unpipelined_one(dev, monkeypatch, residual):
-    """The software-pipelined two-pass GroupNorm kernels (k_gnp_*, the default for 8-wide channel
-    vectors) keep the unpipelined kernels' arithmetic and order: every output and gradient bitwise
-    equal (PSFM_GN_PIPE=0 selects the unpipelined ones), at a large PackNet shape."""
-    g = torch.Generator(device="cpu").manual_seed(10)
-    shape, C = (6, 64, 96, 320), 64
-    gn = nn.GroupNorm(16, C).to(dev)
-    with torch.no_grad():
-        gn.weight.copy_(torch.rand(C, generator=g) + 0.5)
-        gn.bias.copy_(torch.randn(C, generator=g) * 0.1)
-    b = torch.randn(C, generator=g).to(dev, torch.bfloat16)
-    x = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
-    r = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) if residual else None
-    dy = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
-    outs = []
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("PSFM_GN_PIPE", pipe)
-        xi, bi = x.clone().requires_grad_(True), b.clone().requires_grad_(True)
-        ri = r.clone().requires_grad_(True) if residual else None
-        gn.zero_grad(set_to_none=True)
-        y = FU.gn_act(xi, bi, gn, act=FU.ACT_ELU, residual=ri)
-        y.backward(dy)
-        torch.cuda.synchronize()
-        outs.append([t.detach().clone() for t in (y, xi.grad, bi.grad, gn.weight.grad, gn.bias.grad)
-                     + ((ri.grad,) if residual else ())])
-    for a_, b_ in zip(*outs):
-        assert torch.equal(a_, b_)
+def test_backward_captured_for_a_forward_on_another_stream_raises(dev):
+    """capturing the backward of a fused op whose forward ran outside the capture
+    (the sequence that segfaulted HIP's capture_end in round 4) raises a Python RuntimeError from the
+    launch helper before any kernel is enqueued (_hip.stream).  Run in a child process: a regression
+    would crash the interpreter, not just fail."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _CAPTURE_MISUSE.format(root=root)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-3000:])
+    assert "REFUSED: True" in out.stdout, out.stdout

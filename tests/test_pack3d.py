@@ -171,14 +171,14 @@ def test_real_layer_shapes_match_torch_chain(dev, mode, d, shape):
 @pytest.mark.parametrize("mode,shape", [(0, (1, 40, 10, 36)), (0, (2, 16, 22, 70)), (0, (1, 10, 8, 20)), (0, (3, 12, 30, 34)),
                                         (0, (2, 32, 14, 38)),
                                         (1, (1, 40, 10, 36)), (1, (2, 16, 11, 35)), (1, (1, 8, 8, 20)), (1, (3, 48, 6, 34))])
-def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mode, d, shape):
+def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, knob, mode, d, shape):
     """dV of bf16 channels_last pack (mode 0) and unpack (mode 1) layers: the matrix-core form
     (k_p3d_bwd_x_mfma: 8-k chunks, weights split into bf16 hi + lo, fp32 shift-sum) and the VALU
-    form (PSFM_P3D_DX=cl: the k-pair kernel for pack layers with K % 16 == 0, the generic kernel
+    form (knob P3D_DX = 2: the k-pair kernel for pack layers with K % 16 == 0, the generic kernel
     otherwise) both within one bf16 rounding of the float64 reference chain (layers01.py:213-282),
     and within two bf16 ulps of each other.  Pack K = 160 / 64 / 40 / 48 and unpack K = 40 / 16 /
-    8 / 48: 4, 4 (2), 1 and 2 chunks per workgroup, partial edge tiles, first / last chunk halos;
-    PSFM_P3D_DX=mfmag: the grouped staging (pack layers with K % 32 == 0: K = 160 / 64 / 128)."""
+    8 / 48: 2 and 1 chunks per workgroup, partial edge tiles, first / last chunk halos.  (The
+    grouped-staging form lost the A/B and is built into variant libraries only.)"""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
     g = torch.Generator().manual_seed(sum(shape) + d + 10 * mode)
     x = torch.randn(shape, generator=g).to(torch.bfloat16)
@@ -188,8 +188,8 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
     gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
     (yref * gy.double()).sum().backward()
     grads = {}
-    for form in ("mfma", "mfmag", "cl"):
-        monkeypatch.setenv("PSFM_P3D_DX", form)
+    for form, value in (("mfma", 1), ("cl", 2)):
+        knob("P3D_DX", value)
         xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
         y = Pack3dFn.apply(xg, w.to(dev), b.to(dev), mode, 2)
         y.backward(gy.to(dev).contiguous(memory_format=torch.channels_last))
@@ -197,17 +197,17 @@ def test_dx_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mod
         ref = xd.grad
         err = (grads[form] - ref).abs().max().item()
         assert err <= 1e-2 * ref.abs().max().item(), (form, err, ref.abs().max().item())
-    for form in ("mfma", "mfmag"):
+    for form in ("mfma",):
         diff = (grads[form] - grads["cl"]).abs()
         assert (diff <= 2 * 2.0 ** -8 * grads["cl"].abs() + 3e-5 * grads["cl"].abs().max()).all(), (form, diff.max().item())
 
 
 @pytest.mark.parametrize("d", [8, 4])
 @pytest.mark.parametrize("shape", [(2, 64, 10, 36), (1, 96, 7, 19), (3, 32, 12, 40), (1, 128, 4, 6)])
-def test_unpack_dw_matrix_core_matches_the_reference(dev, monkeypatch, d, shape):
+def test_unpack_dw_matrix_core_matches_the_reference(dev, knob, d, shape):
     """Weight / bias gradient of bf16 channels_last UNPACK layers (layers01.py:226-282) on the
     matrix cores (k_p3d_bwd_w_mfma<d, UNPACK>: V = x staged as contiguous 8-k runs, pixel-shuffled
-    dy staged per sub-pixel and interleaved) and on the VALU kernel (PSFM_P3D_DW=generic): both
+    dy staged per sub-pixel and interleaved) and on the VALU kernel (knob P3D_DW = 1): both
     within 2e-3 relative of the float64 reference chain; K = 64 / 96 / 32 / 128 (1 .. 4 chunks of
     32), partial edge tiles."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
@@ -218,8 +218,8 @@ def test_unpack_dw_matrix_core_matches_the_reference(dev, monkeypatch, d, shape)
     xd, conv, yref = _ref(1, x.float(), w, b, 2)
     gy = torch.randn(yref.shape, generator=g).to(torch.bfloat16)
     (yref * gy.double()).sum().backward()
-    for form in ("mfma", "generic"):
-        monkeypatch.setenv("PSFM_P3D_DW", form)
+    for form, value in (("mfma", 0), ("generic", 1)):
+        knob("P3D_DW", value)
         xg = x.to(dev).contiguous(memory_format=torch.channels_last).requires_grad_(True)
         wg, bg = w.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
         y = Pack3dFn.apply(xg, wg, bg, 1, 2)
@@ -232,10 +232,10 @@ def test_unpack_dw_matrix_core_matches_the_reference(dev, monkeypatch, d, shape)
 @pytest.mark.parametrize("d", [8, 4])
 @pytest.mark.parametrize("mode,shape", [(0, (1, 40, 10, 36)), (0, (2, 16, 22, 70)), (0, (3, 8, 14, 38)),
                                         (1, (2, 64, 10, 36)), (1, (1, 96, 7, 19)), (1, (3, 32, 12, 40))])
-def test_forward_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch, mode, d, shape):
+def test_forward_matrix_core_and_valu_forms_match_the_reference(dev, knob, mode, d, shape):
     """Forward of bf16 channels_last pack (mode 0) / unpack (mode 1) layers on the matrix cores
     (k_p3d_fwd_mfma: im2col rows of 16 k, weights split into bf16 hi + lo columns summed by a DPP
-    rotate, the V tile staged twice for aligned reads) and on the VALU kernels (PSFM_P3D_FWD=valu):
+    rotate, the V tile staged twice for aligned reads) and on the VALU kernels (knob P3D_FWD = 2):
     both within one bf16 rounding of the float64 reference chain (layers01.py:126-282) and within
     two bf16 ulps of each other; K = 160 / 64 / 32 (pack), 64 / 96 / 32 (unpack), partial tiles."""
     from packnet_sfm_amd.networks.layers.packnet.pack3d import Pack3dFn
@@ -245,8 +245,8 @@ def test_forward_matrix_core_and_valu_forms_match_the_reference(dev, monkeypatch
     b = torch.randn(d, generator=g) * 0.1
     _, _, yref = _ref(mode, x.float(), w, b, 2)
     ys = {}
-    for form in ("mfma", "valu"):
-        monkeypatch.setenv("PSFM_P3D_FWD", form)
+    for form, value in (("mfma", 1), ("valu", 2)):
+        knob("P3D_FWD", value)
         xg = x.to(dev).contiguous(memory_format=torch.channels_last)
         with torch.no_grad():
             ys[form] = Pack3dFn.apply(xg, w.to(dev), b.to(dev), mode, 2).double().cpu()

@@ -1,0 +1,12 @@
+set -o pipefail
+T=gpurun_out/r5_bn2; mkdir -p $T
+timeout -k 10 500 python -u -m pytest tests/test_netops.py tests/test_pack3d.py tests/test_abi.py tests/test_comm_gpu.py -m gpu -q --timeout 200 --timeout-method thread > $T/tests.log 2>&1; rc=$?
+tail -3 $T/tests.log; grep -E "^(FAILED|ERROR)" $T/tests.log | head
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u bench.py --probe-only --probe-backend nccl > $T/probe_n1.json 2> $T/probe_n1.err; rc=$?
+echo "[probe] rc=$rc"; cat $T/probe_n1.json
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u bench.py --gpus 2 --dist-backend gloo --probe-backend gloo --steps 5 --warmup 3 --no-cpu-baseline --no-kernel-timing > $T/bench_g2_gloo.json 2> $T/bench_g2_gloo.err; rc=$?
+echo "[g2 gloo] rc=$rc"; tail -c 600 $T/bench_g2_gloo.json
+[ $rc -ne 0 ] && exit $rc
+PROF=1 bash tools/r5_ab.sh r5_bn2 kitti-resnet-san 2 "bnres:" "bnres2048:PSFM_BN_RES_MAXM=2048@@" "miopen:--fused-nets bias,gn"
