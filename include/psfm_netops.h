@@ -66,8 +66,9 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
                     float* save_invstd, float* ws, void* stream);
 
 /* 1 when an [M, C] BatchNorm runs the resident one-launch kernels (a workgroup owns 8 channels and
- * all M rows: C % 8 == 0 and M <= 8192, the ResNet encoder's layer2-4 at 192x640), else 0.  Callers
- * keep MIOpen's BatchNorm for the other shapes (the three-pass kernels lose to it). */
+ * all M rows: C % 8 == 0 and M <= the BN_RES_MAXM knob, 2048 by default = the ResNet encoder's
+ * layer3-4 at B = 4, 192x640; at most 8192), else 0.  Callers keep MIOpen's BatchNorm for the other
+ * shapes (the three-pass kernels lose to it, and so does the resident form at larger M: DESIGN.md). */
 int psfm_bn_act_resident(int M, int C);
 
 /* Backward of psfm_bn_act_fwd: dx (bf16), dres (bf16, = ReLU-masked dy; may be NULL),

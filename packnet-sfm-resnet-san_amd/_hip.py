@@ -301,19 +301,28 @@ def _install_capture_hooks():
 _install_capture_hooks()
 
 
+def capture_guard():
+    """Raise before anything is allocated or launched when this thread is not capturing while a
+    HIP-graph capture is in progress — called first thing in every HIP backward: PyTorch-ROCm runs a
+    node's backward on its forward's stream, so a backward captured for a forward that ran outside
+    the capture would otherwise allocate and launch on a stream the capture does not own, and HIP
+    segfaults in capture_end."""
+    if _ACTIVE_CAPTURES and not torch.cuda.is_current_stream_capturing():
+        raise RuntimeError(
+            "psfm: a HIP op would run on a stream outside the HIP-graph capture in progress (stream "
+            f"{torch.cuda.current_stream().cuda_stream:#x} is not capturing).  This happens when an op's "
+            "backward is captured but its forward ran on another stream (autograd runs the backward on "
+            "the forward's stream): run the forward inside the same capture (or on the capture stream), "
+            "as DDPTrainer.capture does")
+
+
 def stream(device):
     """torch's current HIP stream of `device`, for a launch through the C-ABI.  Refuses (Python
     RuntimeError, before anything is launched) to launch on a stream that is NOT capturing while a
     HIP-graph capture is in progress: that is a backward whose forward ran outside the capture
     (PyTorch-ROCm runs a node's backward on its forward's stream) — HIP would otherwise record
     nothing for it and segfault in capture_end."""
-    if _ACTIVE_CAPTURES and not torch.cuda.is_current_stream_capturing():
-        raise RuntimeError(
-            "psfm: a HIP kernel would launch on a stream outside the HIP-graph capture in progress "
-            f"(stream {torch.cuda.current_stream(device).cuda_stream:#x} is not capturing).  This happens when an "
-            "op's backward is captured but its forward ran on another stream (autograd runs the backward "
-            "on the forward's stream): run the forward inside the same capture (or on the capture stream), "
-            "as DDPTrainer.capture does")
+    capture_guard()
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

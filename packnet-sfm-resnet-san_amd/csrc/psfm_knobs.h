@@ -14,6 +14,7 @@ enum Knob {
     KNOB_GN_PATH,       // 0 resident where it fits, 1 two-pass
     KNOB_BN_PATH,       // 0 resident where it fits, 1 three-pass
     KNOB_BN_RES_MAXM,   // largest M = N*H*W the resident BatchNorm takes (<= 8192)
+    KNOB_GN_RES_RPT,    // most row vectors per thread of the resident GroupNorm (1, 2, 4, 8)
     KNOB_COUNT
 };
 

@@ -12,7 +12,11 @@
 #endif
 
 #ifndef PSFM_BN_RES_MAXM_DEFAULT
-#define PSFM_BN_RES_MAXM_DEFAULT 8192
+// resident BatchNorm up to M = 2048 rows (ResNet18 layer3 / layer4 at B = 4, 192x640): interleaved
+// A/B of the kitti-resnet-san step on one box (profiles/r05/bn): 2048 1076-1082 img/s, 8192 (layer2
+// too: its 7680 rows x 16-byte per-lane row loads on 16 CUs run 22 / 41 us a launch) 1031, MIOpen's
+// BatchNorm everywhere 1045-1048
+#define PSFM_BN_RES_MAXM_DEFAULT 2048
 #endif
 
 namespace {
@@ -39,6 +43,7 @@ KnobDef g_knobs[psfm::KNOB_COUNT] = {
     {"GN_PATH", 0, 0, 1, "resident,twopass", 0},
     {"BN_PATH", 0, 0, 1, "resident,threepass", 0},
     {"BN_RES_MAXM", PSFM_BN_RES_MAXM_DEFAULT, 0, 8192, "", PSFM_BN_RES_MAXM_DEFAULT},
+    {"GN_RES_RPT", 8, 1, 8, "", 8},
 };
 
 // value of a knob's environment string: one of its names (position = value) or an integer

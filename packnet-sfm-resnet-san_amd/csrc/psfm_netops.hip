@@ -1644,7 +1644,7 @@ inline bool gnr_geometry(int HW, int C, int G, int cap, GNRGeo& g) {
     // 256-thread workgroups only: in the PackNet step the 512 / 1024-thread forms were slower than
     // the two-pass kernels (a whole-CU workgroup waits for a CU to drain beside the concurrent pose
     // branch, and RPT row vectors per thread are one long latency chain; profiles/r04/gn)
-    static const int tmpl[] = {1, 2, 4};
+    static const int tmpl[] = {1, 2, 4, 8};
     const int nthr = 256, RL = nthr / g.CV;
     const int need = (HW + RL - 1) / RL;
     for (int r : tmpl) {
@@ -1656,12 +1656,13 @@ inline bool gnr_geometry(int HW, int C, int G, int cap, GNRGeo& g) {
     }
     return false;
 }
-// row vectors per thread: <= 4 (the resident path only pays for small layers, see gnr_geometry);
-// backward with res 2 (RPT 4 + res spills: compiler resource report, -Rpass-analysis=kernel-resource-usage)
-inline int gnr_cap_fwd(bool res) { (void)res; return 4; }
-inline int gnr_cap_bwd(bool res) { return res ? 2 : 4; }
+// row vectors per thread: <= 8 (RPT 8 takes PackNetSAN01's 24x80 layers, HW 1920 at 8 channels per
+// block; the resident path only pays for small layers, see gnr_geometry); backward with res 2
+// (RPT 4 + res spills: compiler resource report, -Rpass-analysis=kernel-resource-usage)
+inline int gnr_cap_fwd(bool res) { (void)res; return knob(KNOB_GN_RES_RPT); }
+inline int gnr_cap_bwd(bool res) { return res ? std::min(2, knob(KNOB_GN_RES_RPT)) : knob(KNOB_GN_RES_RPT); }
 
-// RPT instantiations: forward 1, 2, 4, backward 1, 2, 4 (res <= 2), see gnr_cap_*
+// RPT instantiations: forward 1, 2, 4, 8, backward 1, 2, 4, 8 (res <= 2), see gnr_cap_*
 #define GNR_CASE(KERNEL, R, RES_, grid, nthr, st, a)                                   \
     case R:                                                                          \
         if (RES_) hipLaunchKernelGGL((KERNEL<R, true>), grid, dim3(nthr), 0, st, a);   \
@@ -1673,6 +1674,7 @@ inline int gnr_cap_bwd(bool res) { return res ? 2 : 4; }
             GNR_CASE(k_gnr_fwd, 1, RES_, grid, nthr, st, a);                         \
             GNR_CASE(k_gnr_fwd, 2, RES_, grid, nthr, st, a);                         \
             GNR_CASE(k_gnr_fwd, 4, RES_, grid, nthr, st, a);                         \
+            GNR_CASE(k_gnr_fwd, 8, RES_, grid, nthr, st, a);                         \
         }                                                                            \
     } while (0)
 #define GNR_LAUNCH_BWD(RPT_, RES_, grid, nthr, st, a)                                  \
@@ -1680,7 +1682,8 @@ inline int gnr_cap_bwd(bool res) { return res ? 2 : 4; }
         switch (RPT_) {                                                              \
             GNR_CASE(k_gnr_bwd, 1, RES_, grid, nthr, st, a);                         \
             GNR_CASE(k_gnr_bwd, 2, RES_, grid, nthr, st, a);                         \
-            default: hipLaunchKernelGGL((k_gnr_bwd<4, false>), grid, dim3(nthr), 0, st, a); break; \
+            case 4: hipLaunchKernelGGL((k_gnr_bwd<4, false>), grid, dim3(nthr), 0, st, a); break; \
+            default: hipLaunchKernelGGL((k_gnr_bwd<8, false>), grid, dim3(nthr), 0, st, a); break; \
         }                                                                            \
     } while (0)
 

@@ -26,6 +26,7 @@ class PoseFromVecFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        _hip.capture_guard()
         vec, = ctx.saved_tensors
         B, N = vec.shape[0], vec.shape[1]
         gs = [None if g is None else g.float().contiguous() for g in grads]

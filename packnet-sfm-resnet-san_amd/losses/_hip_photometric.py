@@ -260,6 +260,7 @@ class PhotometricLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, g_photo, g_smooth):
+        _hip.capture_guard()
         calls, cfg = ctx.calls, ctx.cfg
         dev = calls[0].image.device
         gout = (g_loss if g_loss is not None else torch.zeros(1, device=dev)).reshape(1).float().contiguous()
@@ -337,6 +338,7 @@ class ViewSynthesisFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        _hip.capture_guard()
         ref_image, depth, cam = ctx.saved_tensors
         B, _, H, W = ref_image.shape
         g = g.contiguous().float()

@@ -58,6 +58,7 @@ class _BiasAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _hip.capture_guard()
         (y,) = ctx.saved_tensors
         dy = _rows(dy.to(y.dtype))
         N, C, H, W = y.shape
@@ -116,6 +117,7 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _hip.capture_guard()
         x, y, weight, mean, invstd = ctx.saved_tensors
         dy = _rows(dy.to(x.dtype))
         N, C, H, W = x.shape
@@ -149,6 +151,7 @@ class _AddReLU(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _hip.capture_guard()
         (y,) = ctx.saved_tensors
         dy = dy.contiguous(memory_format=_fmt(y))
         dz = torch.empty_like(y)
@@ -226,6 +229,7 @@ class _GNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _hip.capture_guard()
         x, res, bias, weight, beta, mean, invstd = ctx.saved_tensors
         dy = _rows(dy.to(x.dtype))
         N, C, H, W = x.shape
@@ -297,6 +301,7 @@ class _UpCat(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _hip.capture_guard()
         N, C1, C2, h, w = ctx.dims
         dout = _rows(dout)
         dx = torch.empty((N, C1, h, w), device=dout.device, dtype=dout.dtype, memory_format=torch.channels_last)
@@ -347,6 +352,7 @@ class _UpCatBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _hip.capture_guard()
         (out,) = ctx.saved_tensors
         N, C1, C2, h, w = ctx.dims
         dout = _rows(dout)

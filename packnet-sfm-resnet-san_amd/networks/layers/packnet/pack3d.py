@@ -60,6 +60,7 @@ class Pack3dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        _hip.capture_guard()
         x, wf = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last).to(x.dtype)
         d = wf.shape[0]

@@ -112,6 +112,7 @@ class PackConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        _hip.capture_guard()
         x, W2, w3, b3, wbuf = ctx.saved_tensors
         k = ctx.k
         B, C, H, W = x.shape

@@ -172,10 +172,17 @@ def test_bn_resident_shapes(hip):
     """psfm_bn_act_resident (host-only): the one-launch BatchNorm holds 8-channel blocks of up to
     8192 rows — ResNet18 layer2-4 at B = 4, 192x640 — and nothing wider or larger."""
     L = hip.lib()
-    for M, C in ((7680, 128), (1920, 256), (480, 512), (8192, 8), (1, 8)):
+    assert hip.knobs()["BN_RES_MAXM"] == (2048, 2048)   # product policy: layer3 / layer4
+    for M, C in ((1920, 256), (480, 512), (2048, 8), (1, 8)):
         assert L.psfm_bn_act_resident(M, C) == 1, (M, C)
-    for M, C in ((8193, 8), (30720, 64), (122880, 64), (480, 12), (0, 64)):
+    for M, C in ((7680, 128), (2049, 8), (30720, 64), (122880, 64), (480, 12), (0, 64)):
         assert L.psfm_bn_act_resident(M, C) == 0, (M, C)
+    prev = hip.set_knob("BN_RES_MAXM", 8192)   # the kernels themselves hold up to 8192 rows
+    try:
+        assert L.psfm_bn_act_resident(7680, 128) == 1 and L.psfm_bn_act_resident(8192, 8) == 1
+        assert L.psfm_bn_act_resident(8193, 8) == 0
+    finally:
+        hip.set_knob("BN_RES_MAXM", prev)
 
 
 def test_knobs_are_read_once_and_set_explicitly(hip):
@@ -183,7 +190,8 @@ def test_knobs_are_read_once_and_set_explicitly(hip):
     product configuration has no non-default knob; set / restore work; out-of-range values and
     unknown names are refused."""
     k = hip.knobs()
-    assert set(k) == {"K12_PRIO", "K12_PARTS", "P3D_FWD", "P3D_DX", "P3D_DW", "GN_PATH", "BN_PATH", "BN_RES_MAXM"}
+    assert set(k) == {"K12_PRIO", "K12_PARTS", "P3D_FWD", "P3D_DX", "P3D_DW", "GN_PATH", "BN_PATH", "BN_RES_MAXM",
+                      "GN_RES_RPT"}
     assert hip.nondefault_knobs() == {}
     prev = hip.set_knob("BN_PATH", 1)
     try:
