@@ -132,6 +132,9 @@ def parse(argv=None):
                          "(networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
+    ap.add_argument("--no-fork", action="store_true",
+                    help="tensors with several consumers as the plain op output (autograd sums their gradients "
+                         "with add kernels) instead of forked views summed by the producer's backward kernel")
     ap.add_argument("--no-hip-gather", action="store_true",
                     help="resident batch gather as index_select + layout copies instead of psfm_gather_frames")
     ap.add_argument("--no-upcat", action="store_true",
@@ -609,6 +612,7 @@ def main():
                       gn="gn" in kinds)
     fused.UPCAT = not args.no_upcat
     fused.ADD_RELU = not args.no_add_relu
+    fused.FORK = not args.no_fork
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     torch.backends.cudnn.deterministic = args.deterministic != "none"

@@ -16,7 +16,7 @@
  *   GN_PATH    GroupNorm: 0 resident where it fits, 1 two-pass everywhere   psfm_netops.hip
  *   BN_PATH    BatchNorm: 0 resident where it fits, 1 three-pass everywhere  psfm_netops.hip
  *   BN_RES_MAXM  the largest M = N*H*W the resident BatchNorm takes (<= 8192) psfm_netops.hip
- *   GN_RES_RPT   most row vectors per thread of the resident GroupNorm (default 8) psfm_netops.hip
+ *   GN_RES_RPT   most row vectors per thread of the resident GroupNorm (default 4) psfm_netops.hip
  * The environment accepts the integer or the value's name (e.g. PSFM_P3D_FWD=mfma).
  *
  * Conventions as include/psfm.h.

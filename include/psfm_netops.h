@@ -55,6 +55,11 @@ int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int
  * Two launches: dx + per-workgroup partial rows, then the column totals. */
 int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void* dx, void* dbias,
                       int bias_bf16, float* ws, void* stream);
+/* The same with dy := bf16(dy + dy1): the two gradients of an output that has two consumers (the
+ * DepthDecoder's up-stage output feeds the next stage and a disparity head), summed in the load as
+ * autograd's accumulation would (one bf16 rounding) — no separate add kernel.  ReLU / NONE only. */
+int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M, int C, int act, void* dx,
+                          void* dbias, int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
  * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there), else three
@@ -76,6 +81,12 @@ int psfm_bn_act_resident(int M, int C);
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, void* stream);
+/* The same with dy := bf16(bf16(dy + dy1) + dy2) (dy1 / dy2 may be NULL): the gradients of a block
+ * output with several consumers (next block's conv1 and identity / downsample, the decoder skip),
+ * summed inside the kernel instead of by autograd's add kernels.  Resident shapes only. */
+int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, const void* x,
+                        const float* gamma, const float* save_mean, const float* save_invstd, int M, int C, int relu,
+                        void* dx, void* dres, float* dgamma, float* dbeta, float* ws, void* stream);
 
 /* y = act(GroupNorm(G)(x [+ res] + bias)) per sample: x / res bf16 [N, HW, C], conv bias bf16/fp32 [C]
  * or NULL, gamma/beta fp32 [C], act PSFM_ACT_NONE / RELU / ELU.  PoseNet conv_gn (conv + GN + ReLU,
@@ -114,6 +125,11 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
  * pass; and its backward dz = (y <= 0) ? 0 : dy, ATen's threshold_backward (both inputs get dz). */
 int psfm_add_relu_fwd(const void* a, const void* b, long long n, void* y, void* stream);
 int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, void* stream);
+/* b may be NULL in psfm_add_relu_fwd (y = relu(a): the stem's BatchNorm + ReLU, whose output has two
+ * consumers); psfm_relu_mask_bwd_sum masks bf16(bf16(dy + dy1) + dy2) (dy1 / dy2 may be NULL): the
+ * gradients of an output with several consumers, summed in the mask pass. */
+int psfm_relu_mask_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, long long n, void* dz,
+                           void* stream);
 
 const char* psfm_netops_last_error(void);
 

@@ -136,9 +136,11 @@ def lib():
         "psfm_gn_ws_floats": ([c_int, c_int, c_int, c_int], c_size_t),
         "psfm_bias_act_fwd": ([V, V, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_bias_act_bwd": ([V, V, c_int, c_int, c_int, V, V, c_int, V, V], c_int),
+        "psfm_bias_act_bwd_sum": ([V, V, V, c_int, c_int, c_int, V, V, c_int, V, V], c_int),
         "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V], c_int),
         "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
         "psfm_bn_act_resident": ([c_int, c_int], c_int),
+        "psfm_bn_act_bwd_sum": ([V, V, V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
         "psfm_gn_act_fwd": ([V, V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V],
                             c_int),
         "psfm_gn_act_bwd": ([V, V, V, V, c_int, V, V, V, V, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V, V,
@@ -146,6 +148,7 @@ def lib():
         "psfm_netops_last_error": ([], ctypes.c_char_p),
         "psfm_add_relu_fwd": ([V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_relu_mask_bwd": ([V, V, ctypes.c_longlong, V, V], c_int),
+        "psfm_relu_mask_bwd_sum": ([V, V, V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_upcat_bwd": ([V, c_int, c_int, c_int, c_int, c_int, V, V, V], c_int),
         "psfm_upcat_bias_relu_fwd": ([V, V, c_int, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
@@ -201,7 +204,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_bn_act_resident", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
-            "psfm_add_relu_fwd", "psfm_relu_mask_bwd",
+            "psfm_add_relu_fwd", "psfm_relu_mask_bwd", "psfm_relu_mask_bwd_sum", "psfm_bias_act_bwd_sum",
+            "psfm_bn_act_bwd_sum",
             "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",
             "psfm_upcat_ws_floats",
             "psfm_depth_metrics", "psfm_metrics_last_error",
@@ -273,6 +277,7 @@ def ptr(t):
 # its own device threads).  torch.cuda.CUDAGraph.capture_begin / capture_end are wrapped once, at
 # import, to count them.
 _ACTIVE_CAPTURES = 0
+_CAPTURE_STREAMS = []   # the streams the captures in progress began on (innermost last)
 _CAPTURE_LOCK = threading.Lock()
 
 
@@ -287,12 +292,15 @@ def _install_capture_hooks():
         r = begin(self, *a, **k)
         with _CAPTURE_LOCK:
             _ACTIVE_CAPTURES += 1
+            _CAPTURE_STREAMS.append(torch.cuda.current_stream())
         return r
 
     def capture_end(self, *a, **k):
         global _ACTIVE_CAPTURES
         with _CAPTURE_LOCK:
             _ACTIVE_CAPTURES = max(0, _ACTIVE_CAPTURES - 1)
+            if _CAPTURE_STREAMS:
+                _CAPTURE_STREAMS.pop()
         return end(self, *a, **k)
 
     G.capture_begin, G.capture_end, G._psfm_counted = capture_begin, capture_end, True
@@ -308,6 +316,15 @@ def capture_guard():
     the capture would otherwise allocate and launch on a stream the capture does not own, and HIP
     segfaults in capture_end."""
     if _ACTIVE_CAPTURES and not torch.cuda.is_current_stream_capturing():
+        # Refuse — but first join this stream into the capture and straight back (an empty fork), so
+        # the capture is still well formed when the error unwinds through torch.cuda.graph: the
+        # autograd engine syncs the backward's stream with the caller's (capturing) stream on the way
+        # out, and a wait on a stream outside the capture makes HIP's capture_end segfault.
+        cur = torch.cuda.current_stream()
+        cap = _CAPTURE_STREAMS[-1] if _CAPTURE_STREAMS else None
+        if cap is not None and cap.cuda_stream != cur.cuda_stream:
+            cur.wait_stream(cap)
+            cap.wait_stream(cur)
         raise RuntimeError(
             "psfm: a HIP op would run on a stream outside the HIP-graph capture in progress (stream "
             f"{torch.cuda.current_stream().cuda_stream:#x} is not capturing).  This happens when an op's "

@@ -43,7 +43,10 @@ KnobDef g_knobs[psfm::KNOB_COUNT] = {
     {"GN_PATH", 0, 0, 1, "resident,twopass", 0},
     {"BN_PATH", 0, 0, 1, "resident,threepass", 0},
     {"BN_RES_MAXM", PSFM_BN_RES_MAXM_DEFAULT, 0, 8192, "", PSFM_BN_RES_MAXM_DEFAULT},
-    {"GN_RES_RPT", 8, 1, 8, "", 8},
+    // resident GroupNorm up to 4 row vectors per thread: RPT 8 (PackNetSAN01's 24x80 layers) ran
+    // 18 / 29 us a launch and lost the interleaved A/B (profiles/r05/gn: kitti-packnet-san 373.3 vs
+    // 375.6-376.7 img/s, kitti-packnet 286.9 vs 287.3)
+    {"GN_RES_RPT", 4, 1, 8, "", 4},
 };
 
 // value of a knob's environment string: one of its names (position = value) or an integer

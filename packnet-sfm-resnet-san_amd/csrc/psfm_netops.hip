@@ -211,6 +211,7 @@ struct BiasArgs {
     const uint16_t* x;
     const void* bias;
     const void* dy;
+    const void* dy1;  // bwd (ReLU, bf16): a second gradient of y summed into dy (its other consumer); may be null
     const void* y;
     void* out;  // y (fwd) / dx (bwd)
     float* ws;  // bwd: per-workgroup partial rows of the bias gradient [nblk][C]
@@ -266,6 +267,11 @@ __global__ __launch_bounds__(NT) void k_bias_act_bwd(BiasArgs a) {
             if (row < row1) {
                 dy[u] = sig ? ld_f<VEC>(static_cast<const float*>(a.dy) + o)
                             : ld_bf<VEC>(static_cast<const uint16_t*>(a.dy) + o);
+                if (a.dy1) {   // autograd's bf16 accumulation of the two gradients, in the load
+                    const Vec<VEC> d1 = ld_bf<VEC>(static_cast<const uint16_t*>(a.dy1) + o);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) dy[u].v[i] = bfround(dy[u].v[i] + d1.v[i]);
+                }
                 y[u] = sig ? ld_f<VEC>(static_cast<const float*>(a.y) + o)
                            : ld_bf<VEC>(static_cast<const uint16_t*>(a.y) + o);
             } else {
@@ -652,6 +658,8 @@ struct BNRArgs {
     float* save_invstd;
     uint16_t* out;   // y (fwd) / dx (bwd)
     uint16_t* dres;  // bwd, may be null
+    const uint16_t* dy1;  // bwd: more gradients of the output (its other consumers), summed into dy; may be null
+    const uint16_t* dy2;
     float* dgamma;
     float* dbeta;
     float momentum, eps;
@@ -701,6 +709,20 @@ __device__ __forceinline__ void bnr_reduce(float (&v)[K], float* red, double* to
         tot[t] = s;
     }
     __syncthreads();
+}
+
+// a + b of two packed bf16 row vectors, rounded to bf16: what autograd's accumulation of two bf16
+// gradients of one tensor computes (CUDAFunctor_add<bf16>: fp32 sum, one rounding)
+__device__ __forceinline__ uint4 add_bf16x8(const uint4 a, const uint4 b) {
+    const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(aw[k] << 16) + __uint_as_float(bw[k] << 16);
+        const float hi = __uint_as_float(aw[k] & 0xffff0000u) + __uint_as_float(bw[k] & 0xffff0000u);
+        o[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // relu-mask a packed bf16 row vector by the forward output: ATen threshold_backward (y <= 0 -> 0)
@@ -820,6 +842,8 @@ __global__ __launch_bounds__(bnr_bwd_maxt(RPT)) void k_bnr_bwd(BNRArgs a) {
         const size_t o = (size_t)min(t + k * NTH, a.M - 1) * a.C + c0;
         gv[k] = *reinterpret_cast<const uint4*>(a.dy + o);
         xv[k] = *reinterpret_cast<const uint4*>(a.x + o);
+        if (a.dy1) gv[k] = add_bf16x8(gv[k], *reinterpret_cast<const uint4*>(a.dy1 + o));   // wave-uniform
+        if (a.dy2) gv[k] = add_bf16x8(gv[k], *reinterpret_cast<const uint4*>(a.dy2 + o));
         if (a.relu) gv[k] = relu_mask4(gv[k], *reinterpret_cast<const uint4*>(a.y + o));
     }
     float mu[8], is[8];
@@ -1656,9 +1680,10 @@ inline bool gnr_geometry(int HW, int C, int G, int cap, GNRGeo& g) {
     }
     return false;
 }
-// row vectors per thread: <= 8 (RPT 8 takes PackNetSAN01's 24x80 layers, HW 1920 at 8 channels per
-// block; the resident path only pays for small layers, see gnr_geometry); backward with res 2
-// (RPT 4 + res spills: compiler resource report, -Rpass-analysis=kernel-resource-usage)
+// row vectors per thread: the GN_RES_RPT knob, 4 by default (the resident path only pays for
+// small layers, see gnr_geometry; RPT 8 — PackNetSAN01's 24x80 layers — lost the step A/B,
+// psfm_knobs.hip); backward with res at most 2 (RPT 4 + res spills: compiler resource report,
+// -Rpass-analysis=kernel-resource-usage)
 inline int gnr_cap_fwd(bool res) { (void)res; return knob(KNOB_GN_RES_RPT); }
 inline int gnr_cap_bwd(bool res) { return res ? std::min(2, knob(KNOB_GN_RES_RPT)) : knob(KNOB_GN_RES_RPT); }
 
@@ -1699,7 +1724,7 @@ __global__ __launch_bounds__(256) void k_add_relu_fwd(const uint4* __restrict__ 
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n8) return;
     const Vec<8> va = ld_bf<8>(reinterpret_cast<const uint16_t*>(a + i));
-    const Vec<8> vb = ld_bf<8>(reinterpret_cast<const uint16_t*>(b + i));
+    const Vec<8> vb = b ? ld_bf<8>(reinterpret_cast<const uint16_t*>(b + i)) : zero<8>();   // b null: relu(a)
     Vec<8> o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {   // ATen relu: NaN propagates (fmaxf would drop it)
@@ -1708,20 +1733,17 @@ __global__ __launch_bounds__(256) void k_add_relu_fwd(const uint4* __restrict__ 
     }
     st_bf<8>(reinterpret_cast<uint16_t*>(y + i), o);
 }
-__global__ __launch_bounds__(256) void k_relu_mask_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ y,
+// dz = (y <= 0) ? 0 : dy [+ dy1 [+ dy2]] (each sum rounded to bf16, as autograd accumulates the
+// gradients of a tensor with several consumers; dy1 / dy2 may be null)
+__global__ __launch_bounds__(256) void k_relu_mask_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ dy1,
+                                                        const uint4* __restrict__ dy2, const uint4* __restrict__ y,
                                                         uint4* __restrict__ dz, long long n8) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n8) return;
-    const uint4 g = dy[i], v = y[i];
-    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, vw[4] = {v.x, v.y, v.z, v.w};
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // ATen threshold_backward: dz = (y <= 0) ? 0 : dy (NaN passes)
-        const uint32_t lo = (__uint_as_float(vw[k] << 16) <= 0.0f) ? 0u : 0x0000ffffu;
-        const uint32_t hi = (__uint_as_float(vw[k] & 0xffff0000u) <= 0.0f) ? 0u : 0xffff0000u;
-        o[k] = gw[k] & (lo | hi);
-    }
-    dz[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    uint4 g = dy[i];
+    if (dy1) g = add_bf16x8(g, dy1[i]);
+    if (dy2) g = add_bf16x8(g, dy2[i]);
+    dz[i] = relu_mask4(g, y[i]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2272,7 +2294,7 @@ size_t psfm_gn_ws_floats(int N, int HW, int C, int G) {
 }
 
 int psfm_add_relu_fwd(const void* a, const void* b, long long n, void* y, void* stream) {
-    if (!a || !b || !y || n < 0 || n % 8 || (((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) & 15))
+    if (!a || !y || n < 0 || n % 8 || (((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) & 15))
         return fail(-1, "add_relu_fwd: n a multiple of 8, 16-byte aligned bf16 buffers");
     const long long n8 = n / 8;
     if (n8) hipLaunchKernelGGL(k_add_relu_fwd, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
@@ -2281,14 +2303,21 @@ int psfm_add_relu_fwd(const void* a, const void* b, long long n, void* y, void* 
     return 0;
 }
 
-int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, void* stream) {
-    if (!dy || !y || !dz || n < 0 || n % 8 || (((uintptr_t)dy | (uintptr_t)y | (uintptr_t)dz) & 15))
+int psfm_relu_mask_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, long long n, void* dz,
+                           void* stream) {
+    if (!dy || !y || !dz || n < 0 || n % 8 ||
+        (((uintptr_t)dy | (uintptr_t)dy1 | (uintptr_t)dy2 | (uintptr_t)y | (uintptr_t)dz) & 15))
         return fail(-1, "relu_mask_bwd: n a multiple of 8, 16-byte aligned bf16 buffers");
     const long long n8 = n / 8;
     if (n8) hipLaunchKernelGGL(k_relu_mask_bwd, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                               static_cast<const uint4*>(dy), static_cast<const uint4*>(y), static_cast<uint4*>(dz), n8);
+                               static_cast<const uint4*>(dy), static_cast<const uint4*>(dy1),
+                               static_cast<const uint4*>(dy2), static_cast<const uint4*>(y), static_cast<uint4*>(dz), n8);
     NETOPS_LAUNCH_CHECK();
     return 0;
+}
+
+int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, void* stream) {
+    return psfm_relu_mask_bwd_sum(dy, nullptr, nullptr, y, n, dz, stream);
 }
 
 int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int C, int act, void* y, void* stream) {
@@ -2312,12 +2341,19 @@ int psfm_bias_act_fwd(const void* x, const void* bias, int bias_bf16, int M, int
 
 int psfm_bias_act_bwd(const void* dy, const void* y, int M, int C, int act, void* dx, void* dbias, int bias_bf16,
                       float* ws, void* stream) {
-    if (!dy || !y || !dx || !dbias || !ws || M < 1 || C < 1) return fail(-1, "bias_act_bwd: bad arguments");
+    return psfm_bias_act_bwd_sum(dy, nullptr, y, M, C, act, dx, dbias, bias_bf16, ws, stream);
+}
+
+int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M, int C, int act, void* dx, void* dbias,
+                          int bias_bf16, float* ws, void* stream) {
+    if (!dy || !y || !dx || !dbias || !ws || M < 1 || C < 1 || (dy1 && act == PSFM_ACT_SIGMOID))
+        return fail(-1, "bias_act_bwd: bad arguments");
     if (int e = check_vec(C, "bias_act_bwd")) return e;
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
     BiasArgs a{};
     a.dy = dy;
+    a.dy1 = dy1;
     a.y = y;
     a.out = dx;
     a.ws = ws;
@@ -2394,6 +2430,13 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
                     const float* save_invstd, int M, int C, int relu, void* dx, void* dres, float* dgamma,
                     float* dbeta, float* ws, void* stream) {
+    return psfm_bn_act_bwd_sum(dy, nullptr, nullptr, y, x, gamma, save_mean, save_invstd, M, C, relu, dx, dres, dgamma,
+                               dbeta, ws, stream);
+}
+
+int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, const void* x,
+                        const float* gamma, const float* save_mean, const float* save_invstd, int M, int C, int relu,
+                        void* dx, void* dres, float* dgamma, float* dbeta, float* ws, void* stream) {
     if (!dy || !x || !gamma || !save_mean || !save_invstd || !dx || !dgamma || !dbeta ||
         M < 1 || C < 1 || (relu && !y))
         return fail(-1, "bn_act_bwd: bad arguments");
@@ -2407,6 +2450,7 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
         a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
         a.out = static_cast<uint16_t*>(dx);
         a.dres = static_cast<uint16_t*>(dres);
+        a.dy1 = static_cast<const uint16_t*>(dy1), a.dy2 = static_cast<const uint16_t*>(dy2);
         a.dgamma = dgamma, a.dbeta = dbeta, a.M = M, a.C = C, a.relu = relu, a.nb = C / 8;
         hipStream_t st = (hipStream_t)stream;
         const BNRGeo& g = rgeo;
@@ -2415,6 +2459,7 @@ int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* g
         return 0;
     }
     if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
+    if (dy1 || dy2) return fail(-1, "bn_act_bwd: extra gradients (dy1 / dy2) need the resident shapes");
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
     BNArgs a{};

@@ -40,10 +40,40 @@ def _rows(t):
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
+# Forked outputs.  A tensor read by k consumers gets k gradients, which autograd sums with k - 1
+# bf16 add kernels (CUDAFunctor_add) before the producer's backward runs.  A fused op asked for
+# `nout` outputs returns its result plus nout - 1 views of it (the same memory, no copy): each
+# consumer takes its own, autograd hands the producer's backward one gradient per view, and the
+# backward kernel sums them in its load (one bf16 rounding per sum, as autograd's add).
+FORK = True   # bench.py --no-fork: the plain output handed to every consumer (autograd's adds)
+
+
+def _fork(y, nout):
+    return y if nout == 1 else (y,) + tuple(y.view_as(y) for _ in range(nout - 1))
+
+
+def _apply_fork(fn, nout, *args):
+    """fn.apply(*args, nout) — or, FORK off, the single output handed to nout consumers."""
+    if FORK or nout == 1:
+        return fn.apply(*args, nout)
+    return fork_plain(fn.apply(*args, 1), nout)
+
+
+def _grads(dys, like):
+    """The non-None gradients of a forked output (at least one; zeros if autograd passed none)."""
+    gs = [g for g in dys if g is not None]
+    return gs if gs else [torch.zeros_like(like)]
+
+
+def fork_plain(y, nout):
+    """The reference op chain's result handed to nout consumers (autograd sums their gradients)."""
+    return y if nout == 1 else (y,) * nout
+
+
 # ----------------------------------------------------------------------------------------------
 class _BiasAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, act):
+    def forward(ctx, x, bias, act, nout=1):
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -54,37 +84,41 @@ class _BiasAct(torch.autograd.Function):
                                        _hip.ptr(y), _hip.stream(x.device)), "psfm_bias_act_fwd")
         ctx.save_for_backward(y)
         ctx.act, ctx.bias_dtype, ctx.x_dtype = act, bias.dtype, x.dtype
-        return y
+        return _fork(y, nout)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *dys):
         _hip.capture_guard()
         (y,) = ctx.saved_tensors
-        dy = _rows(dy.to(y.dtype))
+        gs = [_rows(g.to(y.dtype)) for g in _grads(dys, y)]
+        while len(gs) > 2:   # (a decoder output has at most two consumers)
+            gs = [gs[0] + gs[1]] + gs[2:]
         N, C, H, W = y.shape
         M = N * H * W
         L = _hip.lib()
         dx = torch.empty_like(y, dtype=ctx.x_dtype, memory_format=torch.channels_last)
         db = torch.empty(C, device=y.device, dtype=ctx.bias_dtype)
         ws = torch.empty(L.psfm_netops_ws_floats(M, C), device=y.device, dtype=torch.float32)
-        _hip.check(L.psfm_bias_act_bwd(_hip.ptr(dy), _hip.ptr(y), M, C, ctx.act, _hip.ptr(dx), _hip.ptr(db),
-                                       int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws), _hip.stream(y.device)),
-                   "psfm_bias_act_bwd")
-        return dx, db, None
+        _hip.check(L.psfm_bias_act_bwd_sum(_hip.ptr(gs[0]), _hip.ptr(gs[1] if len(gs) > 1 else None), _hip.ptr(y),
+                                           M, C, ctx.act, _hip.ptr(dx), _hip.ptr(db),
+                                           int(ctx.bias_dtype == torch.bfloat16), _hip.ptr(ws),
+                                           _hip.stream(y.device)), "psfm_bias_act_bwd")
+        return dx, db, None, None
 
 
-def bias_act(x, bias, act, module=None):
+def bias_act(x, bias, act, module=None, nout=1):
     """act(x + bias): x = conv output WITHOUT its bias (F.conv2d(..., None)).  Sigmoid outputs are
-    fp32 (they feed the fp32 photometric loss).  `module` (unused: the reductions need no device
-    state) is kept for the call sites."""
-    if _fusable(x, "bias") and bias is not None:
-        return _BiasAct.apply(x, bias, act)
+    fp32 (they feed the fp32 photometric loss).  nout > 1 (ReLU / none): a tuple of nout views for
+    nout consumers, whose gradients the backward kernel sums (_fork).  `module` (unused: the
+    reductions need no device state) is kept for the call sites."""
+    if _fusable(x, "bias") and bias is not None and (nout == 1 or act != ACT_SIGMOID):
+        return _apply_fork(_BiasAct, nout, x, bias, act)
     y = x if bias is None else x + bias.to(x.dtype).view(1, -1, 1, 1)
     if act == ACT_RELU:
-        return torch.relu(y)
-    if act == ACT_SIGMOID:
-        return torch.sigmoid(y.float()) if x.is_cuda else torch.sigmoid(y)
-    return y
+        y = torch.relu(y)
+    elif act == ACT_SIGMOID:
+        y = torch.sigmoid(y.float()) if x.is_cuda else torch.sigmoid(y)
+    return fork_plain(y, nout)
 
 
 def conv_nobias(conv, x):
@@ -95,7 +129,7 @@ def conv_nobias(conv, x):
 # ----------------------------------------------------------------------------------------------
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, nout=1):
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -113,51 +147,63 @@ class _BNAct(torch.autograd.Function):
                                      _hip.ptr(invstd), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_fwd")
         ctx.save_for_backward(x, y, weight, mean, invstd)
         ctx.relu, ctx.has_res = relu, residual is not None
-        return y
+        return _fork(y, nout)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *dys):
         _hip.capture_guard()
         x, y, weight, mean, invstd = ctx.saved_tensors
-        dy = _rows(dy.to(x.dtype))
+        gs = [_rows(g.to(x.dtype)) for g in _grads(dys, y)]
         N, C, H, W = x.shape
         M = N * H * W
         dev = x.device
         L = _hip.lib()
+        resident = bool(L.psfm_bn_act_resident(M, C))
+        if not resident or len(gs) > 3:   # the three-pass kernels take one gradient: autograd's sum
+            while len(gs) > (3 if resident else 1):
+                gs = [gs[0] + gs[1]] + gs[2:]
+        dy = gs[0]
+        dy1, dy2 = (gs + [None, None])[1:3]
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         dw = torch.empty(C, device=dev, dtype=torch.float32)
         db = torch.empty(C, device=dev, dtype=torch.float32)
-        ws = None if L.psfm_bn_act_resident(M, C) else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev,
-                                                                   dtype=torch.float32)
-        _hip.check(L.psfm_bn_act_bwd(_hip.ptr(dy), _hip.ptr(y), _hip.ptr(x), _hip.ptr(weight), _hip.ptr(mean),
-                                     _hip.ptr(invstd), M, C, int(ctx.relu), _hip.ptr(dx), _hip.ptr(dres),
-                                     _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_bwd")
-        return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None
+        ws = None if resident else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
+        _hip.check(L.psfm_bn_act_bwd_sum(_hip.ptr(dy), _hip.ptr(dy1), _hip.ptr(dy2), _hip.ptr(y), _hip.ptr(x),
+                                         _hip.ptr(weight), _hip.ptr(mean), _hip.ptr(invstd), M, C, int(ctx.relu),
+                                         _hip.ptr(dx), _hip.ptr(dres), _hip.ptr(dw), _hip.ptr(db), _hip.ptr(ws),
+                                         _hip.stream(dev)), "psfm_bn_act_bwd")
+        return dx, dw.to(weight.dtype), db.to(weight.dtype), dres, None, None, None, None, None, None
 
 
 class _AddReLU(torch.autograd.Function):
-    """relu(a + b) on bf16 (include/psfm_netops.h psfm_add_relu_fwd / psfm_relu_mask_bwd): the
-    BasicBlock tail after MIOpen's BatchNorm, one pass each way instead of add + relu / the ReLU
-    backward (the add's backward is the identity to both inputs)."""
+    """relu(a [+ b]) on bf16 (include/psfm_netops.h psfm_add_relu_fwd / psfm_relu_mask_bwd_sum): the
+    BasicBlock tail after MIOpen's BatchNorm (and, b = None, the stem's ReLU), one pass each way
+    instead of add + relu / the ReLU backward (the add's backward is the identity to both inputs);
+    nout > 1 forks the output (_fork) and the mask pass sums its gradients."""
 
     @staticmethod
-    def forward(ctx, a, b):
+    def forward(ctx, a, b, nout=1):
         y = torch.empty_like(a)
         _hip.check(_hip.lib().psfm_add_relu_fwd(_hip.ptr(a), _hip.ptr(b), a.numel(), _hip.ptr(y),
                                                 _hip.stream(a.device)), "psfm_add_relu_fwd")
         ctx.save_for_backward(y)
-        return y
+        ctx.has_b = b is not None
+        return _fork(y, nout)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, *dys):
         _hip.capture_guard()
         (y,) = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=_fmt(y))
+        gs = [g.contiguous(memory_format=_fmt(y)) for g in _grads(dys, y)]
+        while len(gs) > 3:
+            gs = [gs[0] + gs[1]] + gs[2:]
+        dy1, dy2 = (gs + [None, None])[1:3]
         dz = torch.empty_like(y)
-        _hip.check(_hip.lib().psfm_relu_mask_bwd(_hip.ptr(dy), _hip.ptr(y), y.numel(), _hip.ptr(dz),
-                                                 _hip.stream(y.device)), "psfm_relu_mask_bwd")
-        return dz, dz
+        _hip.check(_hip.lib().psfm_relu_mask_bwd_sum(_hip.ptr(gs[0]), _hip.ptr(dy1), _hip.ptr(dy2), _hip.ptr(y),
+                                                     y.numel(), _hip.ptr(dz), _hip.stream(y.device)),
+                   "psfm_relu_mask_bwd")
+        return dz, (dz if ctx.has_b else None), None
 
 
 def _fmt(t):
@@ -168,14 +214,16 @@ def _fmt(t):
 ADD_RELU = True   # the BasicBlock tail on HIP (bench.py --no-add-relu: the op chain)
 
 
-def add_relu(a, b):
-    """relu(a + b): ONE HIP pass each way for bf16 tensors of the same shape and layout on a ROCm
-    device (the ResNet BasicBlock's `out += identity; relu(out)`); otherwise the op chain."""
-    if (ADD_RELU and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.shape == b.shape
-            and a.numel() % 8 == 0 and a.device == b.device and _fmt(a) == _fmt(b)
-            and a.is_contiguous(memory_format=_fmt(a)) and b.is_contiguous(memory_format=_fmt(b))):
-        return _AddReLU.apply(a, b)
-    return torch.relu(a + b)
+def add_relu(a, b, nout=1):
+    """relu(a + b) (b None: relu(a)): ONE HIP pass each way for bf16 tensors of the same shape and
+    layout on a ROCm device (the ResNet BasicBlock's `out += identity; relu(out)`); otherwise the op
+    chain.  nout > 1: a tuple for nout consumers (_fork)."""
+    if (ADD_RELU and a.is_cuda and a.dtype == torch.bfloat16 and a.numel() % 8 == 0
+            and a.is_contiguous(memory_format=_fmt(a))
+            and (b is None or (b.dtype == torch.bfloat16 and a.shape == b.shape and a.device == b.device
+                               and _fmt(a) == _fmt(b) and b.is_contiguous(memory_format=_fmt(b))))):
+        return _apply_fork(_AddReLU, nout, a, b)
+    return fork_plain(torch.relu(a if b is None else a + b), nout)
 
 
 def _bn_fused_shape(x):
@@ -186,23 +234,24 @@ def _bn_fused_shape(x):
     return bool(_hip.lib().psfm_bn_act_resident(N * H * W, C))
 
 
-def bn_act(x, bn, relu=True, residual=None):
+def bn_act(x, bn, relu=True, residual=None, nout=1):
     """act(bn(x) [+ residual]) with the reference's BatchNorm2d module `bn` (torchvision BasicBlock
     conv -> bn -> relu and conv -> bn -> +identity -> relu, resnet_encoder.py:61-98): ONE HIP launch
-    each way where FUSE["bn"] takes the shape, else MIOpen's BatchNorm + the add / ReLU passes."""
+    each way where FUSE["bn"] takes the shape, else MIOpen's BatchNorm + the add / ReLU passes.
+    nout > 1: a tuple of nout views for nout consumers, whose gradients the backward sums (_fork)."""
     if (_fusable(x, "bn") and bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine
             and bn.running_mean is not None and (residual is None or residual.shape == x.shape)
             and _bn_fused_shape(x)):
         if bn.num_batches_tracked is not None:  # the graph trainer keeps these off the step
             bn.num_batches_tracked.add_(1)
-        return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, float(bn.momentum),
-                            float(bn.eps), bool(relu))
+        return _apply_fork(_BNAct, nout, x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                           float(bn.momentum), float(bn.eps), bool(relu))
     y = bn(x)
+    if relu and (residual is None or residual.dtype == y.dtype):
+        return add_relu(y, residual, nout)
     if residual is not None:
-        if relu and residual.dtype == y.dtype:
-            return add_relu(y, residual)
         y = y + residual
-    return torch.relu(y) if relu else y
+    return fork_plain(torch.relu(y) if relu else y, nout)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -38,10 +38,15 @@ class DepthDecoder(nn.Module):
             # cat([upsample(upconv_i0(x)), skip]) with upconv_i0's bias + ReLU folded in: one fused
             # op each way after the convolution (fused.conv_block_up_cat)
             skip = input_features[i - 1] if (self.use_skips and i > 0) else None
-            x = self.convs[("upconv", i, 1)](conv_block_up_cat(self.convs[("upconv", i, 0)], x, skip))
+            # upconv_i1's output feeds the next up-stage and, at a head scale > 0, the disparity head:
+            # forked (fused._fork), so the bias + ReLU backward sums the two gradients itself
+            fork = i in self.scales and i > 0
+            x = self.convs[("upconv", i, 1)](conv_block_up_cat(self.convs[("upconv", i, 0)], x, skip),
+                                             nout=2 if fork else 1)
+            x, xh = x if fork else (x, x)
             if i in self.scales:
                 head = self.convs[("dispconv", i)]  # Conv3x3 + sigmoid, fused epilogue (fp32 maps)
-                xin = head.pad(x) if head.pad is not None else x
+                xin = head.pad(xh) if head.pad is not None else xh
                 out[("disp", i)] = bias_act(conv_nobias(head.conv, xin), head.conv.bias, ACT_SIGMOID, head)
         # not kept on the module (the reference stores self.outputs): a reference held between steps
         # keeps the previous step's autograd graph alive, and with it its AccumulateGrad nodes

@@ -29,11 +29,12 @@ class ConvBlock(nn.Module):
         self.conv = Conv3x3(in_channels, out_channels)
         self.nonlin = nn.ReLU(inplace=True)
 
-    def forward(self, x):
-        # Conv3x3 without its bias + fused (bias + ReLU) epilogue with the bias-gradient reduction
+    def forward(self, x, nout=1):
+        # Conv3x3 without its bias + fused (bias + ReLU) epilogue with the bias-gradient reduction;
+        # nout > 1: forked output for several consumers (fused._fork)
         c = self.conv
         x = c.pad(x) if c.pad is not None else x
-        return bias_act(conv_nobias(c.conv, x), c.conv.bias, ACT_RELU, self)
+        return bias_act(conv_nobias(c.conv, x), c.conv.bias, ACT_RELU, self, nout=nout)
 
 
 def upsample(x):

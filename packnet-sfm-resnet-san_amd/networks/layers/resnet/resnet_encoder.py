@@ -33,11 +33,14 @@ class BasicBlock(nn.Module):
         self.bn2 = nn.BatchNorm2d(planes)
         self.downsample = downsample
 
-    def forward(self, x):
-        # conv -> BN -> ReLU, conv -> BN -> +identity -> ReLU as fused BN epilogues (fused.py)
-        idt = x if self.downsample is None else bn_act(self.downsample[0](x), self.downsample[1], relu=False)
+    def forward(self, x, x_idt=None, nout=1):
+        """conv -> BN -> ReLU, conv -> BN -> +identity -> ReLU as fused BN epilogues (fused.py).
+        x_idt: the identity / downsample input — x's values as the producer's other forked view, so
+        that both gradients reach the producer's backward (fused._fork); nout: forked outputs."""
+        x_idt = x if x_idt is None else x_idt
+        idt = x_idt if self.downsample is None else bn_act(self.downsample[0](x_idt), self.downsample[1], relu=False)
         out = bn_act(self.conv1(x), self.bn1, relu=True)
-        return bn_act(self.conv2(out), self.bn2, relu=True, residual=idt)
+        return bn_act(self.conv2(out), self.bn2, relu=True, residual=idt, nout=nout)
 
 
 class Bottleneck(nn.Module):
@@ -54,11 +57,12 @@ class Bottleneck(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
-    def forward(self, x):
-        idt = x if self.downsample is None else bn_act(self.downsample[0](x), self.downsample[1], relu=False)
+    def forward(self, x, x_idt=None, nout=1):
+        x_idt = x if x_idt is None else x_idt
+        idt = x_idt if self.downsample is None else bn_act(self.downsample[0](x_idt), self.downsample[1], relu=False)
         out = bn_act(self.conv1(x), self.bn1, relu=True)
         out = bn_act(self.conv2(out), self.bn2, relu=True)
-        return bn_act(self.conv3(out), self.bn3, relu=True, residual=idt)
+        return bn_act(self.conv3(out), self.bn3, relu=True, residual=idt, nout=nout)
 
 
 RESNET_SPECS = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]),
@@ -116,12 +120,28 @@ class ResnetEncoder(nn.Module):
             self.num_ch_enc[1:] *= 4
 
     def forward(self, input_image):
+        """[relu(bn1(conv1)), layer1..4] as the reference (resnet_encoder.py:89-98).  Every tensor with
+        several consumers is produced forked (fused._fork): the stem output (maxpool, decoder skip), a
+        block output inside a layer (next block's conv1 and identity) and a layer output (next layer's
+        conv1 and downsample, decoder skip) — their gradients are summed by the producer's backward
+        kernel, not by autograd's bf16 add kernels.  (The maxpool output feeding layer1's first block
+        twice is ATen's and keeps autograd's add.)"""
         e = self.encoder
-        x = bn_act(e.conv1((input_image - 0.45) / 0.225), e.bn1, relu=True)
-        feats = [x]
-        feats.append(e.layer1(e.maxpool(x)))
-        for layer in (e.layer2, e.layer3, e.layer4):
-            feats.append(layer(feats[-1]))
+        x, skip = bn_act(e.conv1((input_image - 0.45) / 0.225), e.bn1, relu=True, nout=2)
+        feats = [skip]
+        h = e.maxpool(x)
+        h = (h, h)
+        layers = (e.layer1, e.layer2, e.layer3, e.layer4)
+        for li, layer in enumerate(layers):
+            blocks = list(layer)
+            for bi, blk in enumerate(blocks):
+                last = bi == len(blocks) - 1
+                nout = (3 if li < len(layers) - 1 else 1) if last else 2
+                outs = blk(h[0], h[1], nout=nout)
+                outs = outs if isinstance(outs, tuple) else (outs,)
+                h = outs[:2] if len(outs) > 1 else None
+                if last:
+                    feats.append(outs[-1])
         # not kept on the module (the reference stores self.features): a reference held between
         # steps keeps the previous step's encoder graph alive, and with it the AccumulateGrad nodes
         # of every encoder parameter — the next step (or HIP-graph capture) on another stream then

@@ -620,3 +620,48 @@ def test_backward_captured_for_a_forward_on_another_stream_raises(dev):
                          timeout=300)
     assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-3000:])
     assert "REFUSED: True" in out.stdout, out.stdout
+
+
+@gpu
+@pytest.mark.parametrize("kind", ["add_relu", "relu", "bn_resident", "bias_relu"])
+def test_forked_outputs_sum_their_gradients_like_autograd(dev, kind):
+    """fused._fork: an op asked for nout outputs returns views of one result; its backward sums the
+    views' gradients in the kernel's load.  Two consumers: bitwise what autograd computes when the
+    plain output is read twice (its bf16 add = fp32 sum, one rounding); three consumers: within one
+    bf16 rounding of it (autograd may accumulate in another order)."""
+    g = torch.Generator(device="cpu").manual_seed(12)
+    shape = (4, 256, 12, 40)
+    a = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    b = _cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16)
+    bias = torch.randn(shape[1], generator=g).to(dev, torch.bfloat16)
+    dys = [_cl(torch.randn(shape, generator=g)).to(dev, torch.bfloat16) for _ in range(3)]
+    bn = nn.BatchNorm2d(shape[1]).to(dev).train()
+    bn.num_batches_tracked = None
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+
+    def run(nout, ncons):
+        bn.running_mean.copy_(rm)
+        bn.running_var.copy_(rv)
+        ai, bi, wi = a.clone().requires_grad_(True), b.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+        if kind == "add_relu":
+            out = FU.add_relu(ai, bi, nout=nout)
+        elif kind == "relu":
+            out = FU.add_relu(ai, None, nout=nout)
+        elif kind == "bn_resident":
+            out = FU.bn_act(ai, bn, relu=True, residual=bi, nout=nout)
+        else:
+            out = FU.bias_act(ai, wi, FU.ACT_RELU, nout=nout)
+        outs = out if isinstance(out, tuple) else (out,) * ncons
+        sum((o.float() * d.float()).sum() for o, d in zip(outs, dys[:ncons])).backward()
+        return [t for t in (ai.grad, bi.grad if kind in ("add_relu", "bn_resident") else None,
+                            wi.grad if kind == "bias_relu" else None) if t is not None]
+
+    for ncons in (2, 3):
+        if kind == "bias_relu" and ncons == 3:
+            continue
+        fork, plain = run(ncons, ncons), run(1, ncons)
+        for f, p in zip(fork, plain):
+            if ncons == 2:
+                assert torch.equal(f, p), (kind, ncons, float((f.float() - p.float()).abs().max()))
+            else:
+                _close(f, p, 1e-2)
