@@ -20,7 +20,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   # counters on this library's kernels only (PMC_ALL=1: every kernel): MIOpen's find and the
   # convolutions run uninstrumented, so a PackNet pass fits its time limit
-  filt="--kernel-include-regex (k12_fwd_grad|k0_unwarped|k_sig_sum|k_finalize|k_grad_finish|k_pose_reduce|k_p3d_|k_gn_|k_bias_act|k_adam|k_upcat|k_cols_finish)"
+  filt="--kernel-include-regex (k12_fwd_grad|k0_unwarped|k_sig_sum|k_finalize|k_grad_finish|k_pose_reduce|k_p3d_|k_gn_|k_gnp_|k_gnr_|k_bnr_|k_pc_|k_bias_act|k_adam|k_upcat|k_cols_finish)"
   [ "${PMC_ALL:-0}" = 1 ] && filt=""
   (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $grp $filt --output-format csv -d "$OUT/p$i" -o run \
      -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 --no-cpu-baseline --no-kernel-timing ${PMC_EXTRA:-} "$@") > "$OUT/p$i.log" 2>&1; rc=$?

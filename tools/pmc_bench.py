@@ -27,7 +27,10 @@ NAMES = {"k12_fwd_grad": "K12_photometric_fwd_grad", "k0_unwarped": "K0_unwarped
          "k_p3d_reduce_w": "p3d_reduce_w", "k_p3d_fwd": "p3d_fwd", "k_p3d_bwd_x": "p3d_bwd_x", "k_p3d_bwd_w": "p3d_bwd_w", "k_adam": "adam",
          "k_gn_fwd_stats": "gn_fwd_stats", "k_gn_fwd_apply": "gn_fwd_apply", "k_gn_bwd_stats": "gn_bwd_stats",
          "k_gn_bwd_apply": "gn_bwd_apply", "k_bias_act_fwd": "bias_act_fwd", "k_bias_act_bwd": "bias_act_bwd",
-         "k_cols_finish": "cols_finish", "k_upcat_fwd": "upcat_fwd", "k_upcat_bwd": "upcat_bwd"}
+         "k_cols_finish": "cols_finish", "k_upcat_fwd": "upcat_fwd", "k_upcat_bwd": "upcat_bwd",
+         "k_gnp_fwd_stats": "gnp_fwd_stats", "k_gnp_fwd_apply": "gnp_fwd_apply", "k_gnp_bwd_stats": "gnp_bwd_stats",
+         "k_gnp_bwd_apply": "gnp_bwd_apply", "k_gnr_fwd": "gnr_fwd", "k_gnr_bwd": "gnr_bwd", "k_gnr_params": "gnr_params",
+         "k_bnr_fwd": "bnr_fwd", "k_bnr_bwd": "bnr_bwd", "k_pc_conv": "pc_conv", "k_pc_wgrad": "pc_wgrad"}
 
 
 def label(kernel):
