@@ -62,8 +62,9 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
                           void* dbias, int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
- * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there), else three
- * (statistics rows, per-channel finish, apply),
+ * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there); other shapes return
+ * -3 (the three-pass kernels — statistics rows, per-channel finish, apply — lost to MIOpen and are
+ * built into A/B variant libraries only, -DPSFM_AB_VARIANTS),
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
  * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,

@@ -368,6 +368,12 @@ inline hipError_t launch_finish(const ColJob* jobs, int njobs, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 // BatchNorm (training) + residual + ReLU
 // ------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t bn_coef_off(int nblk, int C) { return align4((size_t)nblk * 2 * C); }
+#ifdef PSFM_AB_VARIANTS
+// The three-pass fused BatchNorm (statistics rows -> per-channel finish -> apply, each way) lost to
+// MIOpen's BatchNorm + ATen in every A/B on these nets (profiles/r02/netops_ab, r03): it is built
+// into A/B variant libraries only (tools/build_variants.sh "-DPSFM_AB_VARIANTS"); the product runs
+// the resident one-launch kernels below where they hold the layer and MIOpen elsewhere.
 struct BNArgs {
     const uint16_t* x;
     const uint16_t* res;
@@ -388,7 +394,6 @@ struct BNArgs {
     int M, C, relu, G, TR, rpb, nblk;
 };
 
-__host__ __device__ inline size_t bn_coef_off(int nblk, int C) { return align4((size_t)nblk * 2 * C); }
 __device__ __forceinline__ float* bn_coef(const BNArgs& a) { return a.ws + bn_coef_off(a.nblk, a.C); }
 
 // Column totals for the finish kernels: thread = (column c = 4 * blockIdx.x + t % 4, lane t / 4 of
@@ -630,9 +635,13 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
     ROW_LOOP_END
 }
 
+#endif  // PSFM_AB_VARIANTS
+
 // ------------------------------------------------------------------------------------------
-// Resident BatchNorm: ONE launch each way for the small encoder layers (ResNet layer2-4 at
-// 192x640: M = N*H*W <= 7680 rows).  A workgroup owns 8 channels and ALL M rows of them: thread t
+// Resident BatchNorm: ONE launch each way for the small encoder layers (M = N*H*W rows up to the
+// BN_RES_MAXM knob, 2048 by default = ResNet18 layer3 / layer4 at B = 4, 192x640; the kernels hold up
+// to 8192, but at layer2's 7680 rows the 16-byte per-lane row loads of 16 workgroups lose to MIOpen,
+// psfm_knobs.hip).  A workgroup owns 8 channels and ALL M rows of them: thread t
 // holds rows t, t + NTH, ... (RPT 16-byte row vectors, <= 8 per tensor) in registers, so the batch
 // statistics (two passes over the registers: mean, then sum (x - mean)^2 — no E[x^2] - mean^2
 // cancellation), the running-stat update and the apply need no other workgroup, and the backward's
@@ -2400,6 +2409,11 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
+#ifndef PSFM_AB_VARIANTS
+    (void)ws;
+    return fail(-3, "bn_act_fwd: shape outside the resident kernels (psfm_bn_act_resident); the three-pass "
+                    "kernels are built into A/B variant libraries only");
+#else
     if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
     const int vec = pick_vec(C);
     const Geo g = geometry(M, C, vec);
@@ -2425,6 +2439,7 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     }
     NETOPS_LAUNCH_CHECK();
     return 0;
+#endif
 }
 
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
@@ -2458,6 +2473,11 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
+#ifndef PSFM_AB_VARIANTS
+    (void)ws;
+    return fail(-3, "bn_act_bwd: shape outside the resident kernels (psfm_bn_act_resident); the three-pass "
+                    "kernels are built into A/B variant libraries only");
+#else
     if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
     if (dy1 || dy2) return fail(-1, "bn_act_bwd: extra gradients (dy1 / dy2) need the resident shapes");
     const int vec = pick_vec(C);
@@ -2485,6 +2505,7 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
     }
     NETOPS_LAUNCH_CHECK();
     return 0;
+#endif
 }
 
 // the resident path is the default; the GN_PATH knob = 1 forces the two-pass kernels (A/B, tests)

@@ -25,9 +25,9 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
 # Which layer kinds run fused, from the A/B of the ResNetSAN01 + PoseNet step on MI355X
 # (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
 # chain (972 -> 1025 img/s together).  BatchNorm: "resident" = the one-launch kernels where a
-# workgroup holds the layer (psfm_bn_act_resident: ResNet layer2-4), MIOpen's BatchNorm elsewhere
-# (the three-pass kernels lose to it on the large layers, profiles/r02/netops_ab); True = the fused
-# kernels on every shape; False = MIOpen everywhere.  bench.py --fused-nets overrides.
+# workgroup holds the layer (psfm_bn_act_resident: ResNet18 layer3 / layer4), MIOpen's BatchNorm
+# elsewhere (the three-pass fused kernels lost to it and exist in A/B variant builds only,
+# profiles/r02/netops_ab, profiles/r05/bn); False = MIOpen everywhere.  bench.py --fused-nets overrides.
 FUSE = {"bias": True, "gn": True, "bn": "resident"}
 
 
@@ -227,9 +227,8 @@ def add_relu(a, b, nout=1):
 
 
 def _bn_fused_shape(x):
-    """FUSE["bn"] == "resident": only the shapes the one-launch kernels hold (psfm_bn_act_resident)."""
-    if FUSE["bn"] != "resident":
-        return True
+    """Only the shapes the one-launch kernels hold (psfm_bn_act_resident); the product library has no
+    other fused BatchNorm."""
     N, C, H, W = x.shape
     return bool(_hip.lib().psfm_bn_act_resident(N * H * W, C))
 

@@ -193,16 +193,17 @@ def test_knobs_are_read_once_and_set_explicitly(hip):
     assert set(k) == {"K12_PRIO", "K12_PARTS", "P3D_FWD", "P3D_DX", "P3D_DW", "GN_PATH", "BN_PATH", "BN_RES_MAXM",
                       "GN_RES_RPT"}
     assert hip.nondefault_knobs() == {}
-    prev = hip.set_knob("BN_PATH", 1)
+    prev = hip.set_knob("GN_PATH", 1)
     try:
-        assert hip.knobs()["BN_PATH"] == (1, 0) and hip.nondefault_knobs() == {"BN_PATH": 1}
+        assert hip.knobs()["GN_PATH"] == (1, 0) and hip.nondefault_knobs() == {"GN_PATH": 1}
     finally:
-        hip.set_knob("BN_PATH", prev)
+        hip.set_knob("GN_PATH", prev)
     assert hip.nondefault_knobs() == {}
     L = hip.lib()
-    assert L.psfm_knob_set(b"BN_PATH", 7) == -1 and L.psfm_knob_set(b"NO_SUCH", 0) == -1
-    with pytest.raises(ValueError):
-        hip.set_knob("P3D_DX", 3)   # the grouped-staging dx form exists in A/B variant builds only
+    assert L.psfm_knob_set(b"GN_PATH", 7) == -1 and L.psfm_knob_set(b"NO_SUCH", 0) == -1
+    for name, value in (("P3D_DX", 3), ("BN_PATH", 1)):   # forms that exist in A/B variant builds only
+        with pytest.raises(ValueError):
+            hip.set_knob(name, value)
 
 
 def test_knob_environment_is_parsed_at_load():
@@ -212,7 +213,7 @@ def test_knob_environment_is_parsed_at_load():
     import sys
     code = ("import sys; sys.path.insert(0, %r); import torch, packnet_sfm_amd; "
             "from packnet_sfm_amd import _hip; print(sorted(_hip.nondefault_knobs().items()))" % ROOT)
-    env = dict(os.environ, PSFM_P3D_FWD="valu", PSFM_K12_PRIO="0", PSFM_GN_PATH="bogus", PSFM_BN_PATH="9")
+    env = dict(os.environ, PSFM_P3D_FWD="valu", PSFM_K12_PRIO="0", PSFM_GN_PATH="bogus", PSFM_BN_PATH="threepass")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip().splitlines()[-1] == "[('K12_PRIO', 0), ('P3D_FWD', 2)]"

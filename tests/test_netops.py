@@ -50,7 +50,7 @@ def dev():
 def fused_on():
     """Every fused kind on (the product enables the measured winners, fused.FUSE)."""
     prev = dict(FU.FUSE)
-    FU.FUSE.update(bias=True, gn=True, bn=True)
+    FU.FUSE.update(bias=True, gn=True, bn="resident")
     yield
     FU.FUSE.update(prev)
 
@@ -92,13 +92,12 @@ def test_bias_act_matches_torch(dev, shape, act, bias_bf16):
     assert b.grad.dtype == b.dtype
 
 
-@pytest.fixture(params=["resident", "threepass"])
+@pytest.fixture(params=["resident8192", "resident2048"])
 def bn_path(request, knob):
-    """Both fused BatchNorm implementations: the one-launch resident kernels (where a workgroup holds
-    the layer: M = N*H*W <= 8192, C % 8 == 0) and the three-pass kernels (knob BN_PATH = 1; the
-    only fused form of the larger layers)."""
-    knob("BN_PATH", 1 if request.param == "threepass" else 0)
-    knob("BN_RES_MAXM", 8192)   # every geometry the resident kernels have (the product takes <= 2048 rows)
+    """bn_act with the resident kernels taking every geometry they have (BN_RES_MAXM 8192: M = N*H*W <=
+    8192 rows, C % 8 == 0) and with the product limit (2048); larger layers run MIOpen's BatchNorm +
+    the fused (add +) ReLU passes — the product library has no other fused BatchNorm."""
+    knob("BN_RES_MAXM", 8192 if request.param == "resident8192" else 2048)
     return request.param
 
 
@@ -200,27 +199,6 @@ def test_gn_act_matches_torch(dev, shape, gn_path):
 
 
 @gpu
-def test_fused_reductions_are_deterministic_and_rearm(dev):
-    """Repeated fused BatchNorm launches (statistics rows -> per-channel finish -> apply): results
-    stay bit-identical run to run (fixed-order reductions, no atomics)."""
-    g = torch.Generator(device="cpu").manual_seed(4)
-    bn = nn.BatchNorm2d(64).to(dev).train()
-    x = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
-    dy = _cl(torch.randn(4, 64, 48, 160, generator=g)).to(dev, torch.bfloat16)
-    outs = []
-    for _ in range(3):
-        xi = x.clone().requires_grad_(True)
-        bn.weight.grad = None
-        y = FU.bn_act(xi, bn, relu=True)
-        y.backward(dy)
-        torch.cuda.synchronize()
-        outs.append((y.detach().clone(), xi.grad.clone(), bn.weight.grad.clone()))
-    for o in outs[1:]:
-        for a, b in zip(o, outs[0]):
-            assert torch.equal(a, b)
-
-
-@gpu
 @pytest.mark.parametrize("shape,residual", [((4, 256, 12, 40), True), ((4, 512, 6, 20), False)])
 def test_resident_bn_is_bitwise_deterministic_and_captures(dev, shape, residual):
     """The resident BatchNorm (one launch each way, fixed-order reductions, no atomics): eager calls
@@ -294,7 +272,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
     x = _cl(torch.rand(2, 3, 96, 320)).to(dev)
 
     def run(enabled, amp):
-        FU.FUSE.update(bias=enabled, gn=enabled, bn=enabled)
+        FU.FUSE.update(bias=enabled, gn=enabled, bn="resident" if enabled else False)
         try:
             net.zero_grad(set_to_none=True)
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -306,7 +284,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
                      net.encoder.encoder.conv1.weight.grad.detach().float().clone(),
                      net.encoder.encoder.layer4[1].bn2.weight.grad.detach().float().clone()])
         finally:
-            FU.FUSE.update(bias=True, gn=True, bn=True)
+            FU.FUSE.update(bias=True, gn=True, bn="resident")
 
     ref = run(False, False)
     fused, plain = run(True, True), run(False, True)
