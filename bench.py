@@ -127,7 +127,8 @@ def parse(argv=None):
     ap.add_argument("--fused-nets", default="bias,gn,bn",
                     help="net epilogues as fused HIP kernels (psfm_netops): none | all | a comma list of "
                          "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU [+ identity]: the one-launch "
-                         "resident kernels where they hold the layer, MIOpen elsewhere), gn (GroupNorm + ReLU); "
+                         "resident kernels where they hold the layer, the two-launch ticket kernels elsewhere), "
+                         "bnres (the resident kernels only, MIOpen's BatchNorm elsewhere), gn (GroupNorm + ReLU); "
                          "default: the measured winners (networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
@@ -607,7 +608,8 @@ def main():
 
     from packnet_sfm_amd.networks.layers import fused
     kinds = {"none": set(), "all": {"bias", "bn", "gn"}}.get(args.fused_nets, set(args.fused_nets.split(",")))
-    fused.FUSE.update(bias="bias" in kinds, bn="resident" if "bn" in kinds else False, gn="gn" in kinds)
+    fused.FUSE.update(bias="bias" in kinds, bn="all" if "bn" in kinds else ("resident" if "bnres" in kinds else False),
+                      gn="gn" in kinds)
     fused.UPCAT = not args.no_upcat
     fused.ADD_RELU = not args.no_add_relu
     fused.FORK = not args.no_fork
@@ -712,8 +714,7 @@ def main():
                           "weights_dtype": "bf16 model + fp32 master" if (args.amp == "bf16" and not args.eager)
                           else "fp32",
                           "net_epilogues": (f"fused HIP (psfm_netops: {args.fused_nets}), the rest the reference "
-                                            f"op chain (MIOpen BN on the layers the resident BN does not hold)"
-                                            if args.fused_nets != "none" else "reference op chain"),
+                                            f"op chain" if args.fused_nets != "none" else "reference op chain"),
                           "decoder_upcat": "torch op chain" if args.no_upcat else "HIP (psfm_upcat)",
                           "weights": "random init (no network / checkpoints)", "config_key": config_key(args)}}
         out["library"] = __graft_entry__.library_hash()

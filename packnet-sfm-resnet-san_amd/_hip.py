@@ -140,6 +140,7 @@ def lib():
         "psfm_bn_act_fwd": ([V, V, V, V, V, V, c_float, c_float, c_int, c_int, c_int, V, V, V, V, V], c_int),
         "psfm_bn_act_bwd": ([V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
         "psfm_bn_act_resident": ([c_int, c_int], c_int),
+        "psfm_bn_act_fused": ([c_int, c_int], c_int),
         "psfm_bn_act_bwd_sum": ([V, V, V, V, V, V, V, V, c_int, c_int, c_int, V, V, V, V, V, V], c_int),
         "psfm_gn_act_fwd": ([V, V, V, c_int, V, V, c_float, c_int, c_int, c_int, c_int, c_int, V, V, V, V, V],
                             c_int),
@@ -203,7 +204,7 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_tiles_per_image", "psfm_last_error", "psfm_version", "psfm_k12_stamps",
             "psfm_optim_plan_chunks", "psfm_grad_pack", "psfm_adam_step", "psfm_optim_last_error",
             "psfm_netops_ws_floats", "psfm_gn_ws_floats", "psfm_bias_act_fwd", "psfm_bias_act_bwd",
-            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_bn_act_resident", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
+            "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_bn_act_resident", "psfm_bn_act_fused", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
             "psfm_add_relu_fwd", "psfm_relu_mask_bwd", "psfm_relu_mask_bwd_sum", "psfm_bias_act_bwd_sum",
             "psfm_bn_act_bwd_sum",
             "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",

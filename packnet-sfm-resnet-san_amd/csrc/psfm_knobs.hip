@@ -29,9 +29,9 @@ struct KnobDef {
 };
 
 #ifdef PSFM_AB_VARIANTS
-constexpr int P3D_DX_HI = 3, BN_PATH_HI = 1;
+constexpr int P3D_DX_HI = 3, BN_PATH_HI = 2;
 #else
-constexpr int P3D_DX_HI = 2, BN_PATH_HI = 0;   // the three-pass BatchNorm: A/B builds only
+constexpr int P3D_DX_HI = 2, BN_PATH_HI = 1;   // BN_PATH 2, the three-pass BatchNorm: A/B builds only
 #endif
 
 KnobDef g_knobs[psfm::KNOB_COUNT] = {
@@ -41,7 +41,7 @@ KnobDef g_knobs[psfm::KNOB_COUNT] = {
     {"P3D_DX", 0, 0, P3D_DX_HI, "auto,mfma,cl,mfmag", 0},
     {"P3D_DW", 0, 0, 1, "auto,generic", 0},
     {"GN_PATH", 0, 0, 1, "resident,twopass", 0},
-    {"BN_PATH", 0, 0, BN_PATH_HI, "resident,threepass", 0},
+    {"BN_PATH", 0, 0, BN_PATH_HI, "resident,ticket,threepass", 0},
     {"BN_RES_MAXM", PSFM_BN_RES_MAXM_DEFAULT, 0, 8192, "", PSFM_BN_RES_MAXM_DEFAULT},
     // resident GroupNorm up to 4 row vectors per thread: RPT 8 (PackNetSAN01's 24x80 layers) ran
     // 18 / 29 us a launch and lost the interleaved A/B (profiles/r05/gn: kitti-packnet-san 373.3 vs

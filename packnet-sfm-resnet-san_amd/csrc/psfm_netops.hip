@@ -916,7 +916,7 @@ struct BNRGeo {
     int rpt, nth;
 };
 inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
-    if (C % 8 || M < 1 || M > std::min(BNR_MAXM, knob(KNOB_BN_RES_MAXM))) return false;
+    if (C % 8 || C > 512 || M < 1 || M > std::min(BNR_MAXM, knob(KNOB_BN_RES_MAXM))) return false;
     for (int r = 1; r <= (bwd ? 16 : 8); r *= 2) {
         const int maxt = bwd ? bnr_bwd_maxt(r) : BNR_MAXT;
         if ((long long)r * maxt >= M) {
@@ -935,6 +935,317 @@ inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
         break
 #define BNR_BWD_CASE(R)                                                                                  \
     case R: hipLaunchKernelGGL((k_bnr_bwd<R>), dim3(a.nb), dim3(g.nth), 0, st, a); break
+
+// ------------------------------------------------------------------------------------------
+// Two-launch BatchNorm for the layers too large to be resident (the ResNet stem, layer1, layer2):
+// coalesced over all CUs, the cross-workgroup reduction finished inside the statistics launch.
+//   pass 1 (statistics): workgroups take row slices of all C channels (16-byte vectors, a wave
+//     covers whole 128-byte row lines) and publish a partial row of per-channel sums — sc1
+//     (write-through) stores, drained by every storing wave — then one lane takes a ticket (relaxed
+//     agent-scope atomic).  The workgroup holding the LAST ticket acquires (agent scope) and sums
+//     every partial row in a fixed order (fp64): batch statistics, running stats, and the apply
+//     coefficients, then re-arms its ticket word.  (MI355X_MICROARCH.md / cdna_hip_programming.md
+//     §6 Guideline 16: the fan-in form — payload sc1 + drained, counter by atomic, one acquire.)
+//   pass 2 (apply): y = act(x*scale + shift [+ res]) / dx = kg*g + kx*x + k0 over all rows.
+// Forward statistics are shifted sums (x - K, K = the channel's first value) as in the resident
+// kernels; the backward statistics are sum g and sum g (x - mean) of the ReLU-masked gradient (the
+// forked gradients summed in the load).  Deterministic: partial rows summed in workgroup order
+// whichever workgroup finishes last.  Ticket words: a zero-initialised device array, one word per
+// launch site taken round-robin on the host (a graph replays its launches' words; every launch
+// leaves its word at 0).
+// ------------------------------------------------------------------------------------------
+constexpr int BNT_SLOTS = 1024;
+__device__ unsigned int g_bnt_ticket[BNT_SLOTS];
+
+struct BNTArgs {
+    const uint16_t* x;
+    const uint16_t* res;
+    const uint16_t* dy;
+    const uint16_t* dy1;
+    const uint16_t* dy2;
+    const uint16_t* y;
+    const float* gamma;
+    const float* beta;
+    float* run_mean;
+    float* run_var;
+    float* save_mean;
+    float* save_invstd;
+    uint16_t* out;
+    uint16_t* dres;
+    float* dgamma;
+    float* dbeta;
+    float* part;      // [nblk][2C] partial rows
+    float* coef;      // [3][C]: apply coefficients
+    unsigned* ticket;
+    float momentum, eps;
+    int M, C, relu, G, TR, rpb, nblk;
+};
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {   // write-through (sc1) 4-byte store
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// publish this workgroup's partial row (lanes of row lane 0 hold the block sums) and take the ticket;
+// true in every thread of the workgroup that took the last one, after its acquire
+__device__ __forceinline__ bool bnt_publish(const BNTArgs& a, const float (&acc)[2][8], int c0, int r) {
+    __shared__ unsigned s_last;
+    if (r == 0 && c0 < a.C) {
+        float* row = a.part + (size_t)blockIdx.x * 2 * a.C;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            st_sc1(row + c0 + i, acc[0][i]);
+            st_sc1(row + a.C + c0 + i, acc[1][i]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (unsigned)(a.nblk - 1);
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    return s_last;
+}
+
+// the last workgroup: per-channel totals of the nblk partial rows (fixed order, fp64) -> tot[2][C]
+// in LDS.  Channels in chunks of w <= NT; thread (channel c, part q < P = NT / w) sums rows q, q + P,
+// ... (4 loads in flight), then the P parts are added in order.
+__device__ __forceinline__ void bnt_totals(const BNTArgs& a, double* tot, double* scratch) {
+    const int t = threadIdx.x;
+    for (int cb = 0; cb < a.C; cb += NT) {
+        const int w = min(a.C - cb, NT), P = NT / w, c = cb + t % w, q = t / w;
+        if (q < P) {
+            double s1 = 0.0, s2 = 0.0;
+            for (int b = q; b < a.nblk; b += 4 * P) {
+                float v1[4], v2[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int bb = b + u * P;
+                    v1[u] = bb < a.nblk ? a.part[(size_t)bb * 2 * a.C + c] : 0.0f;
+                    v2[u] = bb < a.nblk ? a.part[(size_t)bb * 2 * a.C + a.C + c] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    s1 += (double)v1[u];
+                    s2 += (double)v2[u];
+                }
+            }
+            scratch[2 * t] = s1;
+            scratch[2 * t + 1] = s2;
+        }
+        __syncthreads();
+        if (t < w) {
+            double t1 = 0.0, t2 = 0.0;
+            for (int k = 0; k < P; ++k) {
+                t1 += scratch[2 * (k * w + t)];
+                t2 += scratch[2 * (k * w + t) + 1];
+            }
+            tot[c] = t1;
+            tot[a.C + c] = t2;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_bnt_fwd_stats(BNTArgs a) {
+    __shared__ float red[2 * NT * 8];
+    __shared__ double tot[2 * 512];
+    __shared__ double scratch[2 * NT];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    float kk[8];
+    {
+        const Vec<8> k8 = ld_bf<8>(a.x + (r < a.TR ? c0 : 0));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kk[i] = k8.v[i];
+    }
+    float acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
+    if (r < a.TR) {
+        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        Vec<8> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = base_ + u * a.TR;
+            v[u] = ld_bf<8>(a.x + (size_t)min(row, row1 - 1) * a.C + c0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base_ + u * a.TR >= row1) break;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float d = v[u].v[i] - kk[i];
+                acc[0][i] += d;
+                acc[1][i] += d * d;
+            }
+        }
+        ROW_LOOP_END
+    }
+    block_colsum<8, 2>(acc, red, a.G, a.TR);
+    if (!bnt_publish(a, acc, r < a.TR ? c0 : a.C, r)) return;
+    bnt_totals(a, tot, scratch);
+    const double inv_m = 1.0 / (double)a.M;
+    for (int c = t; c < a.C; c += blockDim.x) {
+        const double m1 = tot[c] * inv_m;
+        const double mean = (double)bf2f(a.x[c]) + m1;
+        const double var = fmax(tot[a.C + c] * inv_m - m1 * m1, 0.0);
+        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+        a.save_mean[c] = (float)mean;
+        a.save_invstd[c] = invstd;
+        if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
+            const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
+            a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
+            a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
+        }
+        const float scale = a.gamma[c] * invstd;
+        a.coef[c] = scale;
+        a.coef[a.C + c] = a.beta[c] - (float)mean * scale;
+    }
+    if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+}
+
+__global__ __launch_bounds__(NT) void k_bnt_fwd_apply(BNTArgs a) {
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    if (r >= a.TR) return;
+    const int c0 = cg * 8;
+    const Vec<8> sc = ld_f<8>(a.coef + c0), sh = ld_f<8>(a.coef + a.C + c0);
+    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    Vec<8> v[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
+        v[u] = ld_bf<8>(a.x + o);
+        if (a.res) rv[u] = ld_bf<8>(a.res + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float w = v[u].v[i] * sc.v[i] + sh.v[i];
+            if (a.res) w = bfround(w) + rv[u].v[i];   // autocast: bn(x) is a bf16 tensor before the add
+            if (a.relu) w = w <= 0.0f ? 0.0f : w;     // ATen relu (NaN propagates)
+            v[u].v[i] = w;
+        }
+        st_bf<8>(a.out + (size_t)row * a.C + c0, v[u]);
+    }
+    ROW_LOOP_END
+}
+
+// the ReLU-masked gradient of one row vector (forked gradients summed first, bf16 rounding each)
+__device__ __forceinline__ uint4 bnt_grad(const BNTArgs& a, size_t o) {
+    uint4 g = *reinterpret_cast<const uint4*>(a.dy + o);
+    if (a.dy1) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy1 + o));
+    if (a.dy2) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy2 + o));
+    if (a.relu) g = relu_mask4(g, *reinterpret_cast<const uint4*>(a.y + o));
+    return g;
+}
+
+__global__ __launch_bounds__(NT) void k_bnt_bwd_stats(BNTArgs a) {
+    __shared__ float red[2 * NT * 8];
+    __shared__ double tot[2 * 512];
+    __shared__ double scratch[2 * NT];
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    const int c0 = cg * 8;
+    float acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
+    if (r < a.TR) {
+        float mu[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mu[i] = a.save_mean[c0 + i];
+        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
+        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+        uint4 gq[U], xq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
+            gq[u] = bnt_grad(a, o);
+            xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base_ + u * a.TR >= row1) break;
+            float g[8], v[8];
+            unpack8f(gq[u], g);
+            unpack8f(xq[u], v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                acc[0][i] += g[i];
+                acc[1][i] += g[i] * (v[i] - mu[i]);
+            }
+        }
+        ROW_LOOP_END
+    }
+    block_colsum<8, 2>(acc, red, a.G, a.TR);
+    if (!bnt_publish(a, acc, r < a.TR ? c0 : a.C, r)) return;
+    bnt_totals(a, tot, scratch);
+    const double inv_m = 1.0 / (double)a.M;
+    for (int c = t; c < a.C; c += blockDim.x) {
+        const double isd = a.save_invstd[c], k1 = (double)(a.gamma[c] * a.save_invstd[c]);
+        const double k2 = tot[c] * inv_m, k3 = tot[a.C + c] * isd * isd * inv_m;
+        a.dbeta[c] = (float)tot[c];
+        a.dgamma[c] = (float)(tot[a.C + c] * isd);
+        a.coef[c] = (float)k1;                                            // kg
+        a.coef[a.C + c] = (float)(-k1 * k3);                              // kx
+        a.coef[2 * a.C + c] = (float)(k1 * (k3 * (double)a.save_mean[c] - k2));   // k0
+    }
+    if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+}
+
+__global__ __launch_bounds__(NT) void k_bnt_bwd_apply(BNTArgs a) {
+    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
+    if (r >= a.TR) return;
+    const int c0 = cg * 8;
+    const Vec<8> kg = ld_f<8>(a.coef + c0), kx = ld_f<8>(a.coef + a.C + c0), k0 = ld_f<8>(a.coef + 2 * a.C + c0);
+    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
+    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
+    uint4 gq[U], xq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
+        gq[u] = bnt_grad(a, o);
+        xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int row = base_ + u * a.TR;
+        if (row >= row1) break;
+        const size_t o = (size_t)row * a.C + c0;
+        float g[8], v[8];
+        unpack8f(gq[u], g);
+        unpack8f(xq[u], v);
+        Vec<8> d;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d.v[i] = fmaf(kg.v[i], g[i], fmaf(kx.v[i], v[i], k0.v[i]));
+        st_bf<8>(a.out + o, d);
+        if (a.dres) *reinterpret_cast<uint4*>(a.dres + o) = gq[u];
+    }
+    ROW_LOOP_END
+}
+
+// ticket-form geometry: rows per workgroup >= 2 row steps (the last workgroup's fixed-order sum
+// reads nblk partial rows), <= 256 workgroups
+inline Geo bnt_geometry(int M, int C) { return geometry(M, C, 8, 256); }
+
+unsigned* bnt_ticket_slot() {
+    static unsigned* base = nullptr;
+    static unsigned next = 0;
+    if (!base) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bnt_ticket)) != hipSuccess) return nullptr;
+        base = static_cast<unsigned*>(p);
+    }
+    return base + (next++ % BNT_SLOTS);
+}
 
 // ------------------------------------------------------------------------------------------
 // GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW),
@@ -2379,12 +2690,33 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
     return 0;
 }
 
-// the resident path where it fits is the default; the BN_PATH knob = 1 forces the three-pass kernels
+// BatchNorm forms by the BN_PATH knob: 0 (default) the resident kernels up to BN_RES_MAXM rows and the
+// two-launch ticket kernels above; 1 the ticket kernels everywhere; 2 the three-pass kernels (A/B
+// builds only).  Returns 0 resident, 1 ticket, 2 three-pass, -1 none.
+static int bn_form(int M, int C, BNRGeo& rg, bool bwd) {
+    const int path = knob(KNOB_BN_PATH);
+    if (path == 0 && bnr_geometry(M, C, rg, bwd)) return 0;
+    if (path == 2) return 2;
+    if (C % 8 == 0 && C <= 512 && M >= 1) return 1;
+    return -1;
+}
 static bool bnr_path() { return knob(KNOB_BN_PATH) == 0; }
 
 int psfm_bn_act_resident(int M, int C) {
     BNRGeo g;
     return bnr_path() && bnr_geometry(M, C, g) ? 1 : 0;
+}
+
+int psfm_bn_act_fused(int M, int C) {
+    BNRGeo g;
+    const int f = bn_form(M, C, g, false);
+    return f == 0 || f == 1 ? 1 : 0;
+}
+
+static void bnt_common(BNTArgs& a, const Geo& g, int M, int C, float* ws) {
+    a.M = M, a.C = C, a.G = g.G, a.TR = g.TR, a.rpb = g.rpb, a.nblk = g.nblk;
+    a.part = ws;
+    a.coef = ws + align4((size_t)g.nblk * 2 * C);
 }
 
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
@@ -2395,7 +2727,27 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     if ((run_mean == nullptr) != (run_var == nullptr)) return fail(-1, "bn_act_fwd: running stats must pair");
     if (int e = check_vec(C, "bn_act_fwd")) return e;
     BNRGeo rgeo;
-    if (bnr_path() && bnr_geometry(M, C, rgeo)) {  // one launch (resident)
+    const int form = bn_form(M, C, rgeo, false);
+    if (form == 1) {  // two launches (ticket)
+        if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
+        unsigned* tk = bnt_ticket_slot();
+        if (!tk) return fail(-4, "bn_act_fwd: ticket words unavailable");
+        const Geo g = bnt_geometry(M, C);
+        BNTArgs a{};
+        bnt_common(a, g, M, C, ws);
+        a.x = static_cast<const uint16_t*>(x);
+        a.res = static_cast<const uint16_t*>(res);
+        a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
+        a.save_mean = save_mean, a.save_invstd = save_invstd;
+        a.out = static_cast<uint16_t*>(y);
+        a.ticket = tk, a.momentum = momentum, a.eps = eps, a.relu = relu;
+        hipStream_t st = (hipStream_t)stream;
+        hipLaunchKernelGGL(k_bnt_fwd_stats, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bnt_fwd_apply, dim3(g.nblk), dim3(NT), 0, st, a);
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
+    if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.x = static_cast<const uint16_t*>(x);
         a.res = static_cast<const uint16_t*>(res);
@@ -2411,8 +2763,8 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     }
 #ifndef PSFM_AB_VARIANTS
     (void)ws;
-    return fail(-3, "bn_act_fwd: shape outside the resident kernels (psfm_bn_act_resident); the three-pass "
-                    "kernels are built into A/B variant libraries only");
+    return fail(-3, "bn_act_fwd: no fused BatchNorm for this shape (psfm_bn_act_fused: C % 8 == 0, C <= 512; the "
+                    "three-pass kernels are built into A/B variant libraries only)");
 #else
     if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
     const int vec = pick_vec(C);
@@ -2457,7 +2809,29 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
         return fail(-1, "bn_act_bwd: bad arguments");
     if (int e = check_vec(C, "bn_act_bwd")) return e;
     BNRGeo rgeo;
-    if (bnr_path() && bnr_geometry(M, C, rgeo, true)) {  // one launch (resident)
+    const int form = bn_form(M, C, rgeo, true);
+    if (form == 1) {  // two launches (ticket)
+        if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
+        unsigned* tk = bnt_ticket_slot();
+        if (!tk) return fail(-4, "bn_act_bwd: ticket words unavailable");
+        const Geo g = bnt_geometry(M, C);
+        BNTArgs a{};
+        bnt_common(a, g, M, C, ws);
+        a.dy = static_cast<const uint16_t*>(dy);
+        a.dy1 = static_cast<const uint16_t*>(dy1), a.dy2 = static_cast<const uint16_t*>(dy2);
+        a.y = static_cast<const uint16_t*>(y);
+        a.x = static_cast<const uint16_t*>(x);
+        a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
+        a.out = static_cast<uint16_t*>(dx);
+        a.dres = static_cast<uint16_t*>(dres);
+        a.dgamma = dgamma, a.dbeta = dbeta, a.ticket = tk, a.relu = relu;
+        hipStream_t st = (hipStream_t)stream;
+        hipLaunchKernelGGL(k_bnt_bwd_stats, dim3(g.nblk), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL(k_bnt_bwd_apply, dim3(g.nblk), dim3(NT), 0, st, a);
+        NETOPS_LAUNCH_CHECK();
+        return 0;
+    }
+    if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.dy = static_cast<const uint16_t*>(dy);
         a.y = static_cast<const uint16_t*>(y);
@@ -2475,8 +2849,8 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
     }
 #ifndef PSFM_AB_VARIANTS
     (void)ws;
-    return fail(-3, "bn_act_bwd: shape outside the resident kernels (psfm_bn_act_resident); the three-pass "
-                    "kernels are built into A/B variant libraries only");
+    return fail(-3, "bn_act_bwd: no fused BatchNorm for this shape (psfm_bn_act_fused: C % 8 == 0, C <= 512; the "
+                    "three-pass kernels are built into A/B variant libraries only)");
 #else
     if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
     if (dy1 || dy2) return fail(-1, "bn_act_bwd: extra gradients (dy1 / dy2) need the resident shapes");

@@ -24,11 +24,12 @@ from ... import _hip
 ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
 # Which layer kinds run fused, from the A/B of the ResNetSAN01 + PoseNet step on MI355X
 # (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
-# chain (972 -> 1025 img/s together).  BatchNorm: "resident" = the one-launch kernels where a
-# workgroup holds the layer (psfm_bn_act_resident: ResNet18 layer3 / layer4), MIOpen's BatchNorm
-# elsewhere (the three-pass fused kernels lost to it and exist in A/B variant builds only,
-# profiles/r02/netops_ab, profiles/r05/bn); False = MIOpen everywhere.  bench.py --fused-nets overrides.
-FUSE = {"bias": True, "gn": True, "bn": "resident"}
+# chain (972 -> 1025 img/s together).  BatchNorm: "all" = every shape the fused kernels take
+# (psfm_bn_act_fused: the one-launch resident kernels where a workgroup holds the layer — ResNet18
+# layer3 / layer4 — and the two-launch ticket kernels above); "resident" = the resident shapes only,
+# MIOpen's BatchNorm elsewhere; False = MIOpen everywhere (profiles/r05/bn).  bench.py --fused-nets
+# overrides.
+FUSE = {"bias": True, "gn": True, "bn": "all"}
 
 
 def _fusable(x, kind):
@@ -159,9 +160,8 @@ class _BNAct(torch.autograd.Function):
         dev = x.device
         L = _hip.lib()
         resident = bool(L.psfm_bn_act_resident(M, C))
-        if not resident or len(gs) > 3:   # the three-pass kernels take one gradient: autograd's sum
-            while len(gs) > (3 if resident else 1):
-                gs = [gs[0] + gs[1]] + gs[2:]
+        while len(gs) > 3:   # the kernels sum up to three gradients in their loads
+            gs = [gs[0] + gs[1]] + gs[2:]
         dy = gs[0]
         dy1, dy2 = (gs + [None, None])[1:3]
         dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -227,10 +227,11 @@ def add_relu(a, b, nout=1):
 
 
 def _bn_fused_shape(x):
-    """Only the shapes the one-launch kernels hold (psfm_bn_act_resident); the product library has no
-    other fused BatchNorm."""
+    """FUSE["bn"] == "resident": the shapes the one-launch kernels hold (psfm_bn_act_resident); else
+    every shape the library's fused BatchNorm takes (psfm_bn_act_fused)."""
     N, C, H, W = x.shape
-    return bool(_hip.lib().psfm_bn_act_resident(N * H * W, C))
+    L = _hip.lib()
+    return bool(L.psfm_bn_act_resident(N * H * W, C) if FUSE["bn"] == "resident" else L.psfm_bn_act_fused(N * H * W, C))
 
 
 def bn_act(x, bn, relu=True, residual=None, nout=1):
