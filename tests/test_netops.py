@@ -111,7 +111,7 @@ def bn_path(request, knob):
                                                   ((2, 64, 24, 80), True, True),
                                                   ((4, 512, 6, 20), True, True),
                                                   ((2, 128, 12, 40), False, False),
-                                                  ((2, 12, 10, 30), True, True),
+                                                  ((2, 24, 10, 30), True, True),   # 3 channel blocks
                                                   # ResNet18 layer2-4 at B = 4, 192x640 (resident: forward
                                                   # RPT 8 x 960 threads, backward RPT 16 x 512; RPT 2 / 1)
                                                   ((4, 128, 24, 80), True, False),
