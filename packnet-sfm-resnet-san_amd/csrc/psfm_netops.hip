@@ -1012,49 +1012,46 @@ __device__ __forceinline__ bool bnt_publish(const BNTArgs& a, const float (&acc)
 }
 
 // the last workgroup: per-channel totals of the nblk partial rows (fixed order, fp64) -> tot[2][C]
-// in LDS.  Channels in chunks of w <= NT; thread (channel c, part q < P = NT / w) sums rows q, q + P,
-// ... (4 loads in flight), then the P parts are added in order.
+// in LDS.  A partial row is F = 2C / 4 float4 columns; thread (column f, row lane q < R = NT / F) sums
+// rows q, q + R, ... with every load of a chunk of 16 rows issued before the first add (the rows sit
+// in the memory-side cache after the sc1 stores: one round trip per chunk, not per row), then the R
+// row lanes are added in order.
 __device__ __forceinline__ void bnt_totals(const BNTArgs& a, double* tot, double* scratch) {
-    const int t = threadIdx.x;
-    for (int cb = 0; cb < a.C; cb += NT) {
-        const int w = min(a.C - cb, NT), P = NT / w, c = cb + t % w, q = t / w;
-        if (q < P) {
-            double s1 = 0.0, s2 = 0.0;
-            for (int b = q; b < a.nblk; b += 4 * P) {
-                float v1[4], v2[4];
+    const int t = threadIdx.x, F = a.C / 2, R = NT / F, f = t % F, q = t / F;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    if (q < R) {
+        const float4* part = reinterpret_cast<const float4*>(a.part);
+        for (int b0 = q; b0 < a.nblk; b0 += 16 * R) {
+            float4 v[16];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int bb = b + u * P;
-                    v1[u] = bb < a.nblk ? a.part[(size_t)bb * 2 * a.C + c] : 0.0f;
-                    v2[u] = bb < a.nblk ? a.part[(size_t)bb * 2 * a.C + a.C + c] : 0.0f;
-                }
+            for (int u = 0; u < 16; ++u) {
+                const int b = b0 + u * R;
+                v[u] = b < a.nblk ? part[(size_t)b * F + f] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    s1 += (double)v1[u];
-                    s2 += (double)v2[u];
-                }
+            for (int u = 0; u < 16; ++u) {
+                s[0] += (double)v[u].x;
+                s[1] += (double)v[u].y;
+                s[2] += (double)v[u].z;
+                s[3] += (double)v[u].w;
             }
-            scratch[2 * t] = s1;
-            scratch[2 * t + 1] = s2;
         }
-        __syncthreads();
-        if (t < w) {
-            double t1 = 0.0, t2 = 0.0;
-            for (int k = 0; k < P; ++k) {
-                t1 += scratch[2 * (k * w + t)];
-                t2 += scratch[2 * (k * w + t) + 1];
-            }
-            tot[c] = t1;
-            tot[a.C + c] = t2;
-        }
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) scratch[(size_t)q * 2 * a.C + 4 * f + k] = s[k];
     }
+    __syncthreads();
+    for (int c = t; c < 2 * a.C; c += NT) {   // c < C: sums, C <= c < 2C: second sums (the row layout)
+        double v = 0.0;
+        for (int k = 0; k < R; ++k) v += scratch[(size_t)k * 2 * a.C + c];
+        tot[c] = v;
+    }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(NT) void k_bnt_fwd_stats(BNTArgs a) {
     __shared__ float red[2 * NT * 8];
     __shared__ double tot[2 * 512];
-    __shared__ double scratch[2 * NT];
+    __shared__ double scratch[4 * NT];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * 8;
     float kk[8];
@@ -1152,7 +1149,7 @@ __device__ __forceinline__ uint4 bnt_grad(const BNTArgs& a, size_t o) {
 __global__ __launch_bounds__(NT) void k_bnt_bwd_stats(BNTArgs a) {
     __shared__ float red[2 * NT * 8];
     __shared__ double tot[2 * 512];
-    __shared__ double scratch[2 * NT];
+    __shared__ double scratch[4 * NT];
     const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
     const int c0 = cg * 8;
     float acc[2][8];
