@@ -127,9 +127,9 @@ def parse(argv=None):
     ap.add_argument("--fused-nets", default="bias,gn,bn",
                     help="net epilogues as fused HIP kernels (psfm_netops): none | all | a comma list of "
                          "bias (conv bias + ReLU/sigmoid), bn (BatchNorm + ReLU [+ identity]: the one-launch "
-                         "resident kernels where they hold the layer, the two-launch ticket kernels elsewhere), "
-                         "bnres (the resident kernels only, MIOpen's BatchNorm elsewhere), gn (GroupNorm + ReLU); "
-                         "default: the measured winners (networks/layers/fused.py FUSE)")
+                         "resident kernels where they hold the layer, MIOpen's BatchNorm elsewhere), bnall (every "
+                         "shape the library's fused BatchNorm takes: A/B builds add the two-launch form), "
+                         "gn (GroupNorm + ReLU); default: the measured winners (networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
     ap.add_argument("--no-fork", action="store_true",
@@ -608,7 +608,7 @@ def main():
 
     from packnet_sfm_amd.networks.layers import fused
     kinds = {"none": set(), "all": {"bias", "bn", "gn"}}.get(args.fused_nets, set(args.fused_nets.split(",")))
-    fused.FUSE.update(bias="bias" in kinds, bn="all" if "bn" in kinds else ("resident" if "bnres" in kinds else False),
+    fused.FUSE.update(bias="bias" in kinds, bn="all" if "bnall" in kinds else ("resident" if "bn" in kinds else False),
                       gn="gn" in kinds)
     fused.UPCAT = not args.no_upcat
     fused.ADD_RELU = not args.no_add_relu

@@ -14,8 +14,8 @@
  *   P3D_DX     pack3d input gradient: 0 policy, 1 matrix cores, 2 VALU       psfm_pack3d.hip
  *   P3D_DW     pack3d weight gradient: 0 policy, 1 VALU (generic)            psfm_pack3d.hip
  *   GN_PATH    GroupNorm: 0 resident where it fits, 1 two-pass everywhere   psfm_netops.hip
- *   BN_PATH    BatchNorm: 0 resident up to BN_RES_MAXM rows, two-launch ticket
- *              kernels above; 1 ticket everywhere; (2 three-pass: A/B builds)   psfm_netops.hip
+ *   BN_PATH    BatchNorm: 0 resident up to BN_RES_MAXM rows (A/B builds: two-launch
+ *              ticket kernels above; 1 ticket everywhere; 2 three-pass)          psfm_netops.hip
  *   BN_RES_MAXM  the largest M = N*H*W the resident BatchNorm takes (<= 8192) psfm_netops.hip
  *   GN_RES_RPT   most row vectors per thread of the resident GroupNorm (default 4) psfm_netops.hip
  * The environment accepts the integer or the value's name (e.g. PSFM_P3D_FWD=mfma).

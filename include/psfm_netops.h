@@ -62,10 +62,10 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
                           void* dbias, int bias_bf16, float* ws, void* stream);
 
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
- * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there), else (C % 8 == 0,
- * C <= 512) TWO: a statistics pass over all CUs whose last workgroup (a ticket) finishes the batch
- * statistics, then the apply pass (ws: psfm_netops_ws_floats floats); other shapes return -3 (the
- * round-2 three-pass kernels are built into A/B variant libraries only, -DPSFM_AB_VARIANTS),
+ * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there); other shapes return
+ * -3 — the two-launch "ticket" kernels (a statistics pass whose last workgroup finishes the batch
+ * statistics) and the round-2 three-pass kernels both lost to MIOpen's BatchNorm and are built into
+ * A/B variant libraries only (-DPSFM_AB_VARIANTS, psfm_bn_act_fused there),
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
  * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
@@ -77,7 +77,8 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
  * layer3-4 at B = 4, 192x640; at most 8192), else 0.  Callers keep MIOpen's BatchNorm for the other
  * shapes (the three-pass kernels lose to it, and so does the resident form at larger M: DESIGN.md). */
 int psfm_bn_act_resident(int M, int C);
-/* 1 when psfm_bn_act_fwd / _bwd(_sum) take an [M, C] BatchNorm at all (resident or two-launch), else 0. */
+/* 1 when psfm_bn_act_fwd / _bwd(_sum) take an [M, C] BatchNorm at all (the product: the resident
+ * shapes; A/B builds: also the two-launch ticket form), else 0. */
 int psfm_bn_act_fused(int M, int C);
 
 /* Backward of psfm_bn_act_fwd: dx (bf16), dres (bf16, = ReLU-masked dy; may be NULL),

@@ -31,7 +31,7 @@ struct KnobDef {
 #ifdef PSFM_AB_VARIANTS
 constexpr int P3D_DX_HI = 3, BN_PATH_HI = 2;
 #else
-constexpr int P3D_DX_HI = 2, BN_PATH_HI = 1;   // BN_PATH 2, the three-pass BatchNorm: A/B builds only
+constexpr int P3D_DX_HI = 2, BN_PATH_HI = 0;   // BN_PATH 1 / 2 (ticket / three-pass BatchNorm): A/B builds only
 #endif
 
 KnobDef g_knobs[psfm::KNOB_COUNT] = {

@@ -936,9 +936,13 @@ inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
 #define BNR_BWD_CASE(R)                                                                                  \
     case R: hipLaunchKernelGGL((k_bnr_bwd<R>), dim3(a.nb), dim3(g.nth), 0, st, a); break
 
+#ifdef PSFM_AB_VARIANTS
 // ------------------------------------------------------------------------------------------
 // Two-launch BatchNorm for the layers too large to be resident (the ResNet stem, layer1, layer2):
 // coalesced over all CUs, the cross-workgroup reduction finished inside the statistics launch.
+// A/B builds only (-DPSFM_AB_VARIANTS): the statistics launch costs 18-19 us whatever the layer size
+// (the hand-off's drains, ticket and acquire round trips), against 12 us for MIOpen's two statistics
+// kernels, and the step lost 1094-1097 vs 1140-1145 img/s to resident + MIOpen (profiles/r05/bn).
 //   pass 1 (statistics): workgroups take row slices of all C channels (16-byte vectors, a wave
 //     covers whole 128-byte row lines) and publish a partial row of per-channel sums — sc1
 //     (write-through) stores, drained by every storing wave — then one lane takes a ticket (relaxed
@@ -1243,6 +1247,7 @@ unsigned* bnt_ticket_slot() {
     }
     return base + (next++ % BNT_SLOTS);
 }
+#endif  // PSFM_AB_VARIANTS
 
 // ------------------------------------------------------------------------------------------
 // GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW),
@@ -2693,8 +2698,10 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
 static int bn_form(int M, int C, BNRGeo& rg, bool bwd) {
     const int path = knob(KNOB_BN_PATH);
     if (path == 0 && bnr_geometry(M, C, rg, bwd)) return 0;
+#ifdef PSFM_AB_VARIANTS
     if (path == 2) return 2;
     if (C % 8 == 0 && C <= 512 && M >= 1) return 1;
+#endif
     return -1;
 }
 static bool bnr_path() { return knob(KNOB_BN_PATH) == 0; }
@@ -2710,11 +2717,13 @@ int psfm_bn_act_fused(int M, int C) {
     return f == 0 || f == 1 ? 1 : 0;
 }
 
+#ifdef PSFM_AB_VARIANTS
 static void bnt_common(BNTArgs& a, const Geo& g, int M, int C, float* ws) {
     a.M = M, a.C = C, a.G = g.G, a.TR = g.TR, a.rpb = g.rpb, a.nblk = g.nblk;
     a.part = ws;
     a.coef = ws + align4((size_t)g.nblk * 2 * C);
 }
+#endif
 
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
@@ -2725,6 +2734,7 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     if (int e = check_vec(C, "bn_act_fwd")) return e;
     BNRGeo rgeo;
     const int form = bn_form(M, C, rgeo, false);
+#ifdef PSFM_AB_VARIANTS
     if (form == 1) {  // two launches (ticket)
         if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
         unsigned* tk = bnt_ticket_slot();
@@ -2744,6 +2754,7 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
+#endif
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.x = static_cast<const uint16_t*>(x);
@@ -2807,6 +2818,7 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
     if (int e = check_vec(C, "bn_act_bwd")) return e;
     BNRGeo rgeo;
     const int form = bn_form(M, C, rgeo, true);
+#ifdef PSFM_AB_VARIANTS
     if (form == 1) {  // two launches (ticket)
         if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
         unsigned* tk = bnt_ticket_slot();
@@ -2828,6 +2840,7 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
+#endif
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.dy = static_cast<const uint16_t*>(dy);

@@ -24,12 +24,12 @@ from ... import _hip
 ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
 # Which layer kinds run fused, from the A/B of the ResNetSAN01 + PoseNet step on MI355X
 # (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
-# chain (972 -> 1025 img/s together).  BatchNorm: "all" = every shape the fused kernels take
-# (psfm_bn_act_fused: the one-launch resident kernels where a workgroup holds the layer — ResNet18
-# layer3 / layer4 — and the two-launch ticket kernels above); "resident" = the resident shapes only,
-# MIOpen's BatchNorm elsewhere; False = MIOpen everywhere (profiles/r05/bn).  bench.py --fused-nets
-# overrides.
-FUSE = {"bias": True, "gn": True, "bn": "all"}
+# chain (972 -> 1025 img/s together).  BatchNorm: "resident" = the one-launch resident kernels where
+# a workgroup holds the layer (psfm_bn_act_resident: ResNet18 layer3 / layer4), MIOpen's BatchNorm
+# elsewhere; "all" = every shape the library's fused BatchNorm takes (psfm_bn_act_fused: the same on
+# the product library; A/B builds add the two-launch ticket kernels, which lost: profiles/r05/bn);
+# False = MIOpen everywhere.  bench.py --fused-nets overrides.
+FUSE = {"bias": True, "gn": True, "bn": "resident"}
 
 
 def _fusable(x, kind):

@@ -177,9 +177,10 @@ def test_bn_resident_shapes(hip):
         assert L.psfm_bn_act_resident(M, C) == 1, (M, C)
     for M, C in ((7680, 128), (2049, 8), (30720, 64), (122880, 64), (480, 12), (0, 64)):
         assert L.psfm_bn_act_resident(M, C) == 0, (M, C)
-    for M, C in ((122880, 64), (30720, 64), (7680, 128), (480, 512)):   # the two-launch form takes the rest
+    for M, C in ((1920, 256), (480, 512)):   # the product library's fused BatchNorm = the resident shapes
         assert L.psfm_bn_act_fused(M, C) == 1, (M, C)
-    assert L.psfm_bn_act_fused(480, 12) == 0 and L.psfm_bn_act_fused(64, 1024) == 0
+    for M, C in ((122880, 64), (30720, 64), (7680, 128), (480, 12), (64, 1024)):
+        assert L.psfm_bn_act_fused(M, C) == 0, (M, C)
     prev = hip.set_knob("BN_RES_MAXM", 8192)   # the kernels themselves hold up to 8192 rows
     try:
         assert L.psfm_bn_act_resident(7680, 128) == 1 and L.psfm_bn_act_resident(8192, 8) == 1
@@ -204,7 +205,7 @@ def test_knobs_are_read_once_and_set_explicitly(hip):
     assert hip.nondefault_knobs() == {}
     L = hip.lib()
     assert L.psfm_knob_set(b"GN_PATH", 7) == -1 and L.psfm_knob_set(b"NO_SUCH", 0) == -1
-    for name, value in (("P3D_DX", 3), ("BN_PATH", 2)):   # forms that exist in A/B variant builds only
+    for name, value in (("P3D_DX", 3), ("BN_PATH", 1), ("BN_PATH", 2)):   # forms in A/B variant builds only
         with pytest.raises(ValueError):
             hip.set_knob(name, value)
 

@@ -50,7 +50,7 @@ def dev():
 def fused_on():
     """Every fused kind on (the product enables the measured winners, fused.FUSE)."""
     prev = dict(FU.FUSE)
-    FU.FUSE.update(bias=True, gn=True, bn="all")
+    FU.FUSE.update(bias=True, gn=True, bn="resident")
     yield
     FU.FUSE.update(prev)
 
@@ -92,16 +92,12 @@ def test_bias_act_matches_torch(dev, shape, act, bias_bf16):
     assert b.grad.dtype == b.dtype
 
 
-@pytest.fixture(params=["resident8192", "resident2048", "ticket"])
+@pytest.fixture(params=["resident8192", "resident2048"])
 def bn_path(request, knob):
-    """The fused BatchNorm forms: the resident kernels taking every geometry they have (BN_RES_MAXM 8192:
-    M = N*H*W <= 8192 rows, C % 8 == 0) or the product limit (2048), the two-launch ticket kernels
-    above; and the ticket kernels on every shape (BN_PATH 1).  C % 8 != 0 runs MIOpen's BatchNorm + the
-    fused (add +) ReLU pass."""
-    if request.param == "ticket":
-        knob("BN_PATH", 1)
-    else:
-        knob("BN_RES_MAXM", 8192 if request.param == "resident8192" else 2048)
+    """bn_act with the resident kernels taking every geometry they have (BN_RES_MAXM 8192: M = N*H*W <=
+    8192 rows, C % 8 == 0) and with the product limit (2048); larger layers run MIOpen's BatchNorm + the
+    fused (add +) ReLU pass (the library's other fused BatchNorm forms lost and exist in A/B builds only)."""
+    knob("BN_RES_MAXM", 8192 if request.param == "resident8192" else 2048)
     return request.param
 
 
@@ -203,16 +199,14 @@ def test_gn_act_matches_torch(dev, shape, gn_path):
 
 
 @gpu
-@pytest.mark.parametrize("shape,residual,resident", [((4, 256, 12, 40), True, 1), ((4, 512, 6, 20), False, 1),
-                                                      ((4, 128, 24, 80), True, 0), ((4, 64, 96, 320), False, 0)])
-def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual, resident):
-    """The fused BatchNorm — resident (one launch each way) and two-launch ticket forms (the last
-    workgroup sums the partial rows in workgroup order, whichever finishes last, and re-arms its
-    ticket word): eager calls repeat bit for bit, and a HIP-graph capture of forward + backward
-    replays the eager results bit for bit, twice (running statistics included)."""
+@pytest.mark.parametrize("shape,residual", [((4, 256, 12, 40), True), ((4, 512, 6, 20), False)])
+def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual):
+    """The resident BatchNorm (one launch each way, fixed-order reductions, no atomics): eager calls
+    repeat bit for bit, and a HIP-graph capture of forward + backward replays the eager results bit for
+    bit, twice (running statistics included)."""
     from packnet_sfm_amd import _hip
     N, C, H, W = shape
-    assert _hip.lib().psfm_bn_act_resident(N * H * W, C) == resident
+    assert _hip.lib().psfm_bn_act_resident(N * H * W, C) == 1
     assert _hip.lib().psfm_bn_act_fused(N * H * W, C) == 1
     g = torch.Generator(device="cpu").manual_seed(11)
     x = _cl(torch.randn(shape, generator=g) + 0.2).to(dev, torch.bfloat16)
@@ -257,20 +251,20 @@ def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual, re
 
 @gpu
 def test_bn_policies_route_the_shapes(dev, monkeypatch):
-    """FUSE["bn"] == "resident": only the layers the resident kernels take (M <= 2048 rows: ResNet18
-    layer3 / layer4) run fused, the larger ones MIOpen's BatchNorm; "all" (the product default): every
-    shape with C % 8 == 0 (resident or two-launch ticket kernels), C % 8 != 0 MIOpen."""
+    """FUSE["bn"] == "resident" (the product default): only the layers the resident kernels take (M <=
+    2048 rows: ResNet18 layer3 / layer4) run fused, the larger ones and C % 8 != 0 MIOpen's BatchNorm;
+    "all" routes the same shapes on the product library (A/B builds add the two-launch form)."""
     calls = []
     orig = FU._BNAct.apply
     monkeypatch.setattr(FU._BNAct, "apply", lambda *a: calls.append(tuple(a[0].shape)) or orig(*a))
     shapes = ((4, 256, 12, 40), (4, 128, 24, 80), (4, 64, 48, 160), (2, 12, 10, 30))
-    for policy in ("resident", "all"):
+    for policy in ("resident", "all"):   # the same on the product library (no other fused form)
         FU.FUSE["bn"] = policy
         for shape in shapes:
             bn = nn.BatchNorm2d(shape[1]).to(dev).train()
             x = _cl(torch.randn(shape)).to(dev, torch.bfloat16)
             FU.bn_act(x, bn, relu=True)
-    assert calls == [(4, 256, 12, 40)] + [s for s in shapes if s[1] % 8 == 0]
+    assert calls == [(4, 256, 12, 40)] * 2
 
 
 @gpu
@@ -283,7 +277,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
     x = _cl(torch.rand(2, 3, 96, 320)).to(dev)
 
     def run(enabled, amp):
-        FU.FUSE.update(bias=enabled, gn=enabled, bn="all" if enabled else False)
+        FU.FUSE.update(bias=enabled, gn=enabled, bn="resident" if enabled else False)
         try:
             net.zero_grad(set_to_none=True)
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -295,7 +289,7 @@ def test_resnet_encoder_fused_matches_unfused(dev):
                      net.encoder.encoder.conv1.weight.grad.detach().float().clone(),
                      net.encoder.encoder.layer4[1].bn2.weight.grad.detach().float().clone()])
         finally:
-            FU.FUSE.update(bias=True, gn=True, bn="all")
+            FU.FUSE.update(bias=True, gn=True, bn="resident")
 
     ref = run(False, False)
     fused, plain = run(True, True), run(False, True)
