@@ -132,6 +132,8 @@ def parse(argv=None):
                          "gn (GroupNorm + ReLU); default: the measured winners (networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
+    ap.add_argument("--no-stem-pool", action="store_true",
+                    help="stem relu + max-pool as psfm_add_relu + ATen's max-pool instead of psfm_relu_maxpool")
     ap.add_argument("--no-fork", action="store_true",
                     help="tensors with several consumers as the plain op output (autograd sums their gradients "
                          "with add kernels) instead of forked views summed by the producer's backward kernel")
@@ -613,6 +615,7 @@ def main():
     fused.UPCAT = not args.no_upcat
     fused.ADD_RELU = not args.no_add_relu
     fused.FORK = not args.no_fork
+    fused.STEM_POOL = not args.no_stem_pool
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     torch.backends.cudnn.deterministic = args.deterministic != "none"

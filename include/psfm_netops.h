@@ -136,6 +136,19 @@ int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, voi
 int psfm_relu_mask_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, long long n, void* dz,
                            void* stream);
 
+/* The ResNet stem's ReLU + MaxPool2d(kernel 3, stride 2, padding 1) (torchvision ResNet through
+ * resnet_encoder.py: relu(bn1(conv1(x))) feeds the max-pool and the decoder's first skip) in ONE pass:
+ * x = the BatchNorm output, bf16 NHWC [N, H, W, C] (H, W even, C % 8 == 0); writes relu_out (same
+ * shape: the skip), pool_out [N, H/2, W/2, C] and argmax (uint8 per output element: the window
+ * position kh * 3 + kw of the maximum, ATen's first-maximum / NaN-propagating choice). */
+int psfm_relu_maxpool_fwd(const void* x, int N, int H, int W, int C, void* relu_out, void* pool_out, void* argmax,
+                          void* stream);
+/* Its backward in one pass: dx = relu'(relu_out) * bf16(bf16(max-pool backward of bf16(dpool + dpool1))
+ * + dskip) — ATen's max_pool2d backward (windows in (oh, ow) order, fp32, one rounding), autograd's adds
+ * of the pooled output's second consumer (dpool1, may be NULL) and of the skip (dskip, may be NULL). */
+int psfm_relu_maxpool_bwd(const void* dpool, const void* dpool1, const void* dskip, const void* relu_out,
+                          const void* argmax, int N, int H, int W, int C, void* dx, void* stream);
+
 const char* psfm_netops_last_error(void);
 
 /* Decoder up-stage input: out = cat([nearest_up2(x), skip], channels)  (the reference's

@@ -2514,9 +2514,183 @@ __global__ __launch_bounds__(256) void k_upcat_bwd(UpcatArgs a) {
     a.dskip[j] = a.dout[(size_t)pix * Vt + a.V1 + v];
 }
 
+// ------------------------------------------------------------------------------------------
+// The ResNet stem's ReLU + MaxPool2d(3, stride 2, pad 1) (torchvision ResNet via resnet_encoder.py:
+// relu(bn1(conv1(x))) feeds maxpool and the decoder's first skip): ONE pass each way on bf16
+// channels_last, H and W even.  A thread owns one output pixel's 8-channel vector and the 2 x 2
+// input block it tiles (stride 2): it loads the 3 x 3 window once, writes the ReLU output of its own
+// block (the decoder skip), the pooled value and the window position of the maximum (uint8 per
+// channel: kh * 3 + kw).  ATen semantics: max with NaN propagation (`v > m || isnan(v)`, first
+// maximum kept on ties).  Backward: per input pixel, the pooled gradients of the <= 4 windows whose
+// maximum it is, in (oh, ow) order in fp32, one bf16 rounding (max_pool_backward_nhwc), plus the
+// skip gradient (autograd's bf16 add), then the ReLU mask of the output — and the pooled output's
+// two consumers' gradients summed first (fused._fork): one kernel for max-pool backward, two adds and
+// the ReLU backward.
+// ------------------------------------------------------------------------------------------
+struct PoolArgs {
+    const uint16_t* x;     // fwd: the BatchNorm output [N, H, W, C]
+    uint16_t* relu;        // [N, H, W, C] relu(x)
+    uint16_t* pool;        // [N, H/2, W/2, C]
+    uint8_t* arg;          // [N, H/2, W/2, C] window position of the maximum
+    const uint16_t* dpool;   // bwd
+    const uint16_t* dpool1;  // may be null
+    const uint16_t* dskip;   // may be null
+    uint16_t* dx;
+    int N, H, W, C, Ho, Wo, CV;   // CV = C / 8
+    long long n;                  // N * Ho * Wo * CV threads
+};
+
+__global__ __launch_bounds__(256) void k_relu_maxpool_fwd(PoolArgs a) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int cv = (int)(i % a.CV);
+    const long long opix = i / a.CV;
+    const int ow = (int)(opix % a.Wo), oh = (int)((opix / a.Wo) % a.Ho), nb = (int)(opix / ((long long)a.Wo * a.Ho));
+    const int c0 = cv * 8;
+    float m[8];
+    uint32_t idx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = -INFINITY, idx[k] = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+        const int ih = 2 * oh - 1 + kh;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int iw = 2 * ow - 1 + kw;
+            if (ih < 0 || ih >= a.H || iw < 0 || iw >= a.W) continue;
+            const size_t o = (((size_t)nb * a.H + ih) * a.W + iw) * a.C + c0;
+            const uint4 q = *reinterpret_cast<const uint4*>(a.x + o);
+            float v[8];
+            unpack8f(q, v);
+            Vec<8> rv;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float r = v[k] <= 0.0f ? 0.0f : v[k];   // ATen relu (NaN propagates)
+                rv.v[k] = r;
+                if (r > m[k] || r != r) {   // max_pool_forward_nhwc's test (r >= 0 > -inf: the first sets it)
+                    m[k] = r;
+                    idx[k] = kh * 3 + kw;
+                }
+            }
+            if (kh >= 1 && kw >= 1) st_bf<8>(a.relu + o, rv);   // this thread's own 2 x 2 block
+        }
+    }
+    Vec<8> pv;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv.v[k] = m[k];
+    const size_t po = (size_t)opix * a.C + c0;
+    st_bf<8>(a.pool + po, pv);
+    uint2 packed;
+    packed.x = idx[0] | (idx[1] << 8) | (idx[2] << 16) | (idx[3] << 24);
+    packed.y = idx[4] | (idx[5] << 8) | (idx[6] << 16) | (idx[7] << 24);
+    *reinterpret_cast<uint2*>(a.arg + po) = packed;
+}
+
+__global__ __launch_bounds__(256) void k_relu_maxpool_bwd(PoolArgs a) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int cv = (int)(i % a.CV);
+    const long long opix = i / a.CV;
+    const int ow = (int)(opix % a.Wo), oh = (int)((opix / a.Wo) % a.Ho), nb = (int)(opix / ((long long)a.Wo * a.Ho));
+    const int c0 = cv * 8;
+    // the (up to) 4 windows touching this thread's 2 x 2 block: (oh + wy, ow + wx), wy, wx in {0, 1}
+    float g[2][2][8];
+    uint32_t ar[2][2][2];
+    bool ok[2][2];
+#pragma unroll
+    for (int wy = 0; wy < 2; ++wy)
+#pragma unroll
+        for (int wx = 0; wx < 2; ++wx) {
+            const int ph = oh + wy, pw = ow + wx;
+            ok[wy][wx] = ph < a.Ho && pw < a.Wo;
+            const size_t po = (((size_t)nb * a.Ho + min(ph, a.Ho - 1)) * a.Wo + min(pw, a.Wo - 1)) * a.C + c0;
+            uint4 d = *reinterpret_cast<const uint4*>(a.dpool + po);
+            if (a.dpool1) d = add_bf16x8(d, *reinterpret_cast<const uint4*>(a.dpool1 + po));
+            unpack8f(d, g[wy][wx]);
+            const uint2 q = *reinterpret_cast<const uint2*>(a.arg + po);
+            ar[wy][wx][0] = q.x;
+            ar[wy][wx][1] = q.y;
+        }
+#pragma unroll
+    for (int by = 0; by < 2; ++by)
+#pragma unroll
+        for (int bx = 0; bx < 2; ++bx) {
+            const int ih = 2 * oh + by, iw = 2 * ow + bx;
+            const size_t o = (((size_t)nb * a.H + ih) * a.W + iw) * a.C + c0;
+            float acc[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] = 0.0f;
+            // windows containing (ih, iw): row oh (+ oh + 1 when by == 1), column ow (+ ow + 1 when bx == 1),
+            // in (oh, ow) order; the pixel's position in window (oh + wy, ow + wx)
+#pragma unroll
+            for (int wy = 0; wy < 2; ++wy) {
+                if (wy > by) continue;
+#pragma unroll
+                for (int wx = 0; wx < 2; ++wx) {
+                    if (wx > bx || !ok[wy][wx]) continue;
+                    const uint32_t pos = (uint32_t)((1 + by - 2 * wy) * 3 + (1 + bx - 2 * wx));
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t am = (ar[wy][wx][k >> 2] >> (8 * (k & 3))) & 0xffu;
+                        if (am == pos) acc[k] += g[wy][wx][k];
+                    }
+                }
+            }
+            Vec<8> d;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d.v[k] = bfround(acc[k]);   // max_pool backward's bf16 gradient
+            if (a.dskip) {
+                const Vec<8> sk = ld_bf<8>(a.dskip + o);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) d.v[k] = bfround(d.v[k] + sk.v[k]);
+            }
+            const Vec<8> r = ld_bf<8>(a.relu + o);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d.v[k] = r.v[k] <= 0.0f ? 0.0f : d.v[k];   // threshold_backward
+            st_bf<8>(a.dx + o, d);
+        }
+}
+
 }  // namespace
 
 extern "C" {
+
+static int pool_setup(PoolArgs& a, int N, int H, int W, int C, const char* who) {
+    if (N < 1 || H < 2 || W < 2 || (H & 1) || (W & 1) || C < 8 || (C % 8)) return fail(-1, who);
+    a.N = N, a.H = H, a.W = W, a.C = C, a.Ho = H / 2, a.Wo = W / 2, a.CV = C / 8;
+    a.n = (long long)N * a.Ho * a.Wo * a.CV;
+    return 0;
+}
+
+int psfm_relu_maxpool_fwd(const void* x, int N, int H, int W, int C, void* relu_out, void* pool_out, void* argmax,
+                          void* stream) {
+    PoolArgs a{};
+    if (!x || !relu_out || !pool_out || !argmax) return fail(-1, "relu_maxpool_fwd: bad arguments");
+    if (int e = pool_setup(a, N, H, W, C, "relu_maxpool_fwd: H, W even, C % 8 == 0")) return e;
+    a.x = static_cast<const uint16_t*>(x);
+    a.relu = static_cast<uint16_t*>(relu_out);
+    a.pool = static_cast<uint16_t*>(pool_out);
+    a.arg = static_cast<uint8_t*>(argmax);
+    hipLaunchKernelGGL(k_relu_maxpool_fwd, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_relu_maxpool_bwd(const void* dpool, const void* dpool1, const void* dskip, const void* relu_out,
+                          const void* argmax, int N, int H, int W, int C, void* dx, void* stream) {
+    PoolArgs a{};
+    if (!dpool || !relu_out || !argmax || !dx) return fail(-1, "relu_maxpool_bwd: bad arguments");
+    if (int e = pool_setup(a, N, H, W, C, "relu_maxpool_bwd: H, W even, C % 8 == 0")) return e;
+    a.dpool = static_cast<const uint16_t*>(dpool);
+    a.dpool1 = static_cast<const uint16_t*>(dpool1);
+    a.dskip = static_cast<const uint16_t*>(dskip);
+    a.relu = const_cast<uint16_t*>(static_cast<const uint16_t*>(relu_out));
+    a.arg = const_cast<uint8_t*>(static_cast<const uint8_t*>(argmax));
+    a.dx = static_cast<uint16_t*>(dx);
+    hipLaunchKernelGGL(k_relu_maxpool_bwd, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
 
 static int upcat_check(int N, int h, int w, int C1, int C2, const char* who) {
     if (N < 1 || h < 1 || w < 1 || C1 < 8 || C2 < 0 || (C1 % 8) || (C2 % 8)) return fail(-1, who);

@@ -254,6 +254,77 @@ def bn_act(x, bn, relu=True, residual=None, nout=1):
     return fork_plain(torch.relu(y) if relu else y, nout)
 
 
+class _ReLUMaxPool(torch.autograd.Function):
+    """The ResNet stem's relu -> MaxPool2d(3, 2, 1) (include/psfm_netops.h psfm_relu_maxpool_fwd/bwd):
+    one pass each way for the ReLU, the pooling (uint8 window positions instead of ATen's int64
+    indices) and, backward, the pooled output's second consumer's add, the skip's add and the ReLU
+    mask.  Outputs: (relu(y) — the decoder skip, pooled [, its fork view])."""
+
+    @staticmethod
+    def forward(ctx, y, nout=2):
+        N, C, H, W = y.shape
+        r = torch.empty_like(y, memory_format=torch.channels_last)
+        p = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=y.dtype).contiguous(
+            memory_format=torch.channels_last)
+        am = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=torch.uint8).contiguous(
+            memory_format=torch.channels_last)
+        _hip.check(_hip.lib().psfm_relu_maxpool_fwd(_hip.ptr(y), N, H, W, C, _hip.ptr(r), _hip.ptr(p), _hip.ptr(am),
+                                                    _hip.stream(y.device)), "psfm_relu_maxpool_fwd")
+        ctx.save_for_backward(r, am)
+        ctx.mark_non_differentiable(am)
+        return (r,) + _fork(p, nout) if nout > 1 else (r, p)
+
+    @staticmethod
+    def backward(ctx, dskip, *dps):
+        _hip.capture_guard()
+        r, am = ctx.saved_tensors
+        N, C, H, W = r.shape
+        gs = [_rows(g.to(r.dtype)) for g in dps if g is not None]
+        if not gs:
+            gs = [torch.zeros((N, C, H // 2, W // 2), device=r.device, dtype=r.dtype).contiguous(
+                memory_format=torch.channels_last)]
+        while len(gs) > 2:
+            gs = [gs[0] + gs[1]] + gs[2:]
+        dskip = None if dskip is None else _rows(dskip.to(r.dtype))
+        dx = torch.empty_like(r, memory_format=torch.channels_last)
+        _hip.check(_hip.lib().psfm_relu_maxpool_bwd(_hip.ptr(gs[0]), _hip.ptr(gs[1] if len(gs) > 1 else None),
+                                                    _hip.ptr(dskip), _hip.ptr(r), _hip.ptr(am), N, H, W, C,
+                                                    _hip.ptr(dx), _hip.stream(r.device)), "psfm_relu_maxpool_bwd")
+        return dx, None
+
+
+STEM_POOL = True   # the stem's relu + max-pool on HIP (bench.py --no-stem-pool: add_relu + ATen's max-pool)
+
+
+def _stem_pool_ok(y, pool):
+    N, C, H, W = y.shape
+    k, s, p = (pool.kernel_size, pool.stride, pool.padding)
+    return (STEM_POOL and y.is_cuda and y.dtype == torch.bfloat16 and y.dim() == 4
+            and y.is_contiguous(memory_format=torch.channels_last) and H % 2 == 0 and W % 2 == 0 and C % 8 == 0
+            and k in (3, (3, 3)) and s in (2, (2, 2)) and p in (1, (1, 1)) and pool.dilation in (1, (1, 1))
+            and not pool.ceil_mode and not pool.return_indices)
+
+
+def bn_relu_maxpool(x, bn, pool, nout=2):
+    """The ResNet stem after conv1 (torchvision ResNet through resnet_encoder.py:89-92):
+    skip = relu(bn(x)), pooled = pool(skip).  Returns (skip, pooled) or, nout = 2, (skip, pooled,
+    pooled's fork view) for layer1's first block (conv1 and identity).  Where the fused BatchNorm
+    does not take the stem (MIOpen's BatchNorm runs it: M = N * H * W rows is beyond the resident
+    kernels) the ReLU and the pooling run as ONE HIP pass each way (_ReLUMaxPool)."""
+    if not (_fusable(x, "bn") and _bn_fused_shape(x)):
+        y = bn(x)
+        if _stem_pool_ok(y, pool):
+            if FORK or nout == 1:
+                return _ReLUMaxPool.apply(y, nout)
+            skip, h = _ReLUMaxPool.apply(y, 1)
+            return (skip,) + fork_plain(h, nout)
+        xr, skip = add_relu(y, None, 2)
+    else:
+        xr, skip = bn_act(x, bn, relu=True, nout=2)
+    h = pool(xr)
+    return (skip,) + fork_plain(h, nout) if nout > 1 else (skip, h)
+
+
 # ----------------------------------------------------------------------------------------------
 class _GNAct(torch.autograd.Function):
     @staticmethod

@@ -10,7 +10,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..fused import bn_act
+from ..fused import bn_act, bn_relu_maxpool
 
 
 def conv3x3(i, o, stride=1):
@@ -124,13 +124,11 @@ class ResnetEncoder(nn.Module):
         several consumers is produced forked (fused._fork): the stem output (maxpool, decoder skip), a
         block output inside a layer (next block's conv1 and identity) and a layer output (next layer's
         conv1 and downsample, decoder skip) — their gradients are summed by the producer's backward
-        kernel, not by autograd's bf16 add kernels.  (The maxpool output feeding layer1's first block
-        twice is ATen's and keeps autograd's add.)"""
+        kernel, not by autograd's bf16 add kernels.  The stem's ReLU + max-pool is one HIP pass each way
+        (fused.bn_relu_maxpool), its pooled output forked for layer1's first block (conv1, identity)."""
         e = self.encoder
-        x, skip = bn_act(e.conv1((input_image - 0.45) / 0.225), e.bn1, relu=True, nout=2)
+        skip, *h = bn_relu_maxpool(e.conv1((input_image - 0.45) / 0.225), e.bn1, e.maxpool, nout=2)
         feats = [skip]
-        h = e.maxpool(x)
-        h = (h, h)
         layers = (e.layer1, e.layer2, e.layer3, e.layer4)
         for li, layer in enumerate(layers):
             blocks = list(layer)

@@ -528,6 +528,64 @@ def test_add_relu_equals_the_op_chain_bitwise(dev, shape, cl):
 
 
 @gpu
+@pytest.mark.parametrize("shape,nout", [((4, 64, 96, 320), 2), ((2, 64, 96, 320), 1), ((3, 24, 10, 14), 2),
+                                        ((1, 8, 2, 2), 2)])
+def test_stem_relu_maxpool_equals_the_op_chain_bitwise(dev, shape, nout):
+    """The stem's relu -> MaxPool2d(3, 2, 1) (psfm_relu_maxpool_fwd/bwd via fused.bn_relu_maxpool's
+    HIP branch) equals ATen's relu + max_pool2d and autograd's backward (the pooled output read by
+    nout consumers, the skip by one) bit for bit: the pooled max and ties (relu zeros: first in window
+    order), NaN propagation, ATen's fp32 window sum in (oh, ow) order, the bf16 adds, the ReLU mask."""
+    g = torch.Generator(device="cpu").manual_seed(12)
+    y = torch.randn(shape, generator=g).permute(0, 2, 3, 1).contiguous()   # NHWC storage
+    y.view(-1)[:5] = torch.tensor([float("nan"), 0.0, -0.0, float("inf"), -float("inf")])
+    y.view(-1)[-3 * shape[1]:] = 0.0           # three pixels of ties at zero
+    y = y.permute(0, 3, 1, 2).to(dev, torch.bfloat16)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    pool = nn.MaxPool2d(3, 2, 1)
+    y1, y2 = y.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    calls = []
+    orig = FU._ReLUMaxPool.apply
+    FU._ReLUMaxPool.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        out1 = FU._ReLUMaxPool.apply(y1, nout) if FU._stem_pool_ok(y1, pool) else None
+    finally:
+        FU._ReLUMaxPool.apply = orig
+    assert calls and out1 is not None
+    r2 = torch.relu(y2)
+    p2 = pool(r2)
+    out2 = (r2,) + (p2,) * nout
+    assert len(out1) == len(out2)
+    for a, b in zip(out1, out2):
+        assert torch.equal(a.nan_to_num(), b.nan_to_num())
+        assert a.is_contiguous(memory_format=torch.channels_last) == b.is_contiguous(memory_format=torch.channels_last)
+    grads = [_cl(torch.randn(o.shape, generator=g)).to(dev, torch.bfloat16) for o in out2]
+    torch.autograd.backward(out1, grads)
+    torch.autograd.backward(out2, grads)
+    assert torch.equal(y1.grad, y2.grad)
+
+
+@gpu
+def test_stem_relu_maxpool_routes_the_resnet_stem(dev):
+    """bn_relu_maxpool: MIOpen's BatchNorm + the fused pass where the stem is beyond the resident
+    BatchNorm (B = 4, 192 x 640: M = 122880 rows); bench.py --no-stem-pool keeps add_relu + ATen."""
+    g = torch.Generator(device="cpu").manual_seed(13)
+    bn, pool = nn.BatchNorm2d(64).to(dev).train(), nn.MaxPool2d(3, 2, 1)
+    x = _cl(torch.randn((4, 64, 96, 320), generator=g)).to(dev, torch.bfloat16)
+    seen = []
+    orig = FU._ReLUMaxPool.apply
+    FU._ReLUMaxPool.apply = lambda *a: seen.append(1) or orig(*a)
+    try:
+        skip, h0, h1 = FU.bn_relu_maxpool(x, bn, pool, nout=2)
+        FU.STEM_POOL = False
+        s2, g0, g1 = FU.bn_relu_maxpool(x, bn, pool, nout=2)
+    finally:
+        FU._ReLUMaxPool.apply = orig
+        FU.STEM_POOL = True
+    assert seen == [1]
+    assert torch.equal(skip, s2) and torch.equal(h0, g0) and torch.equal(h1, g1)
+
+
+@gpu
 def test_gn_backward_captures_when_its_forward_ran_on_the_capture_stream(dev):
     """tools/gn_bench.py's round-3 capture segfault, resolved (profiles/r04/cap): 20 captured
     torch.autograd.grad calls through psfm_gn_act_bwd at [6, 64, 192, 640] replay bit-exactly when
