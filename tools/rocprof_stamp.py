@@ -20,7 +20,7 @@ def main():
     import bench
     args = bench.parse(["--config", a.config])
     txt = open(a.summary).read()
-    m = re.search(r"^\s*([\d.]+) us/step\s+n/step=\s*([\d.]+)\s+\S*k12_fwd_grad", txt, re.M)
+    m = re.search(r"^\s*([\d.]+) us/step\s+n/step=\s*([\d.]+)\s+[^\n]*?k12_fwd_grad", txt, re.M)
     if not m:
         raise SystemExit("no k12_fwd_grad row in " + a.summary)
     us, n = float(m.group(1)), float(m.group(2))
