@@ -936,274 +936,6 @@ inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
 #define BNR_BWD_CASE(R)                                                                                  \
     case R: hipLaunchKernelGGL((k_bnr_bwd<R>), dim3(a.nb), dim3(g.nth), 0, st, a); break
 
-// ------------------------------------------------------------------------------------------
-// Split BatchNorm: TWO launches each way for the layers too large to be resident (the ResNet stem,
-// layer1, layer2), with no cross-workgroup hand-off inside a launch (the ticket form below lost on
-// exactly that hand-off):
-//   statistics: at most BNS_MAXP workgroups of 1024 threads take row slices of all C channels
-//     (16-byte vectors, whole 128-byte row lines per wave, BNS_U loads in flight per thread) and
-//     write one partial row each — forward sum (x - K), sum (x - K)^2 (K = the channel's first
-//     value, as the resident kernels), backward sum g, sum g (x - mean) of the ReLU-masked,
-//     fork-summed gradient;
-//   apply: every workgroup first sums the P <= 64 partial rows in a fixed order (fp64; the same
-//     order in every workgroup, so all agree bit for bit) into its LDS coefficients, workgroup 0
-//     alone writes the batch / running statistics or dgamma / dbeta, then y = act(x*scale + shift
-//     [+ res]) / dx = kg*g + kx*x + k0 and dres = g over its rows.
-// Replaces MIOpen's 3 + 3 kernels and the add+ReLU / ReLU-mask passes around them.
-// ------------------------------------------------------------------------------------------
-constexpr int BNS_NT = 1024;   // statistics workgroup
-constexpr int BNS_U = 8;       // row loads in flight per statistics thread
-constexpr int BNS_MAXP = 64;   // partial rows
-
-struct BNSArgs {
-    const uint16_t* x;
-    const uint16_t* res;
-    const uint16_t* dy;
-    const uint16_t* dy1;
-    const uint16_t* dy2;
-    const uint16_t* y;
-    const float* gamma;
-    const float* beta;
-    float* run_mean;
-    float* run_var;
-    float* save_mean;
-    float* save_invstd;
-    uint16_t* out;
-    uint16_t* dres;
-    float* dgamma;
-    float* dbeta;
-    float* part;      // [P][2C] partial rows
-    float momentum, eps;
-    int M, C, relu, G;
-    int sTR, srpb, P;      // statistics geometry (BNS_NT threads)
-    int TR, rpb, nblk;     // apply geometry (NT threads)
-};
-
-// the ReLU-masked gradient of one row vector (forked gradients summed first, bf16 rounding each)
-__device__ __forceinline__ uint4 bns_grad(const BNSArgs& a, size_t o) {
-    uint4 g = *reinterpret_cast<const uint4*>(a.dy + o);
-    if (a.dy1) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy1 + o));
-    if (a.dy2) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy2 + o));
-    if (a.relu) g = relu_mask4(g, *reinterpret_cast<const uint4*>(a.y + o));
-    return g;
-}
-
-template <bool BWD>
-__global__ __launch_bounds__(BNS_NT) void k_bns_stats(BNSArgs a) {
-    __shared__ float red[2 * BNS_NT * 8];
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    const int c0 = cg * 8;
-    float acc[2][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
-    if (r < a.sTR) {
-        float kk[8];   // forward: the shift K; backward: the batch mean
-        if constexpr (BWD) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) kk[i] = a.save_mean[c0 + i];
-        } else {
-            unpack8f(*reinterpret_cast<const uint4*>(a.x + c0), kk);
-        }
-        const int row0 = blockIdx.x * a.srpb, row1 = min(a.M, row0 + a.srpb);
-        for (int base = row0 + r; base < row1; base += BNS_U * a.sTR) {
-            uint4 xq[BNS_U], gq[BWD ? BNS_U : 1];
-#pragma unroll
-            for (int u = 0; u < BNS_U; ++u) {   // every load issued before the first use (clamped rows)
-                const size_t o = (size_t)min(base + u * a.sTR, row1 - 1) * a.C + c0;
-                xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
-                if constexpr (BWD) gq[u] = bns_grad(a, o);
-            }
-#pragma unroll
-            for (int u = 0; u < BNS_U; ++u) {
-                if (base + u * a.sTR >= row1) break;
-                float v[8];
-                unpack8f(xq[u], v);
-                if constexpr (BWD) {
-                    float g[8];
-                    unpack8f(gq[u], g);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        acc[0][i] += g[i];
-                        acc[1][i] += g[i] * (v[i] - kk[i]);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const float d = v[i] - kk[i];
-                        acc[0][i] += d;
-                        acc[1][i] += d * d;
-                    }
-                }
-            }
-        }
-    }
-    block_colsum<8, 2>(acc, red, a.G, a.sTR);
-    if (r == 0 && r < a.sTR) {
-        float* row = a.part + (size_t)blockIdx.x * 2 * a.C;
-        *reinterpret_cast<float4*>(row + c0) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
-        *reinterpret_cast<float4*>(row + c0 + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
-        *reinterpret_cast<float4*>(row + a.C + c0) = make_float4(acc[1][0], acc[1][1], acc[1][2], acc[1][3]);
-        *reinterpret_cast<float4*>(row + a.C + c0 + 4) = make_float4(acc[1][4], acc[1][5], acc[1][6], acc[1][7]);
-    }
-}
-
-// per-channel totals of the P partial rows (fixed order, fp64) -> tot[2C] in LDS.  A partial row is
-// F = C / 2 float4 columns; thread (column f, row lane q < R = NT / F) sums rows q, q + R, ... (8
-// loads in flight; zero rows past P add exact zeros), then the R row lanes are added in order.
-__device__ __forceinline__ void bns_totals(const BNSArgs& a, double* tot, double* scratch) {
-    const int t = threadIdx.x, F = a.C / 2, R = NT / F, f = t % F, q = t / F;
-    if (q < R) {
-        const float4* part = reinterpret_cast<const float4*>(a.part);
-        double s[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int b0 = q; b0 < a.P; b0 += 8 * R) {   // 8 loads in flight per chunk
-            float4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int b = b0 + u * R;
-                v[u] = b < a.P ? part[(size_t)b * F + f] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                s[0] += (double)v[u].x;
-                s[1] += (double)v[u].y;
-                s[2] += (double)v[u].z;
-                s[3] += (double)v[u].w;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) scratch[(size_t)q * 2 * a.C + 4 * f + k] = s[k];
-    }
-    __syncthreads();
-    for (int c = t; c < 2 * a.C; c += NT) {   // c < C: first sums, C <= c < 2C: second sums
-        double v = 0.0;
-        for (int k = 0; k < R; ++k) v += scratch[(size_t)k * 2 * a.C + c];
-        tot[c] = v;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(NT) void k_bns_fwd_apply(BNSArgs a) {
-    __shared__ double tot[2 * 512];
-    __shared__ double scratch[2 * 1024];
-    __shared__ float coef[2 * 512];
-    bns_totals(a, tot, scratch);
-    const int t = threadIdx.x;
-    const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += NT) {
-        const double m1 = tot[c] * inv_m;
-        const double mean = (double)bf2f(a.x[c]) + m1;
-        const double var = fmax(tot[a.C + c] * inv_m - m1 * m1, 0.0);
-        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        const float scale = a.gamma[c] * invstd;
-        coef[c] = scale;
-        coef[a.C + c] = a.beta[c] - (float)mean * scale;
-        if (blockIdx.x == 0) {
-            a.save_mean[c] = (float)mean;
-            a.save_invstd[c] = invstd;
-            if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
-                const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-                a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
-                a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-            }
-        }
-    }
-    __syncthreads();
-    const int cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * 8;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sc[i] = coef[c0 + i], sh[i] = coef[a.C + c0 + i];
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    Vec<8> v[U], rv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
-        v[u] = ld_bf<8>(a.x + o);
-        if (a.res) rv[u] = ld_bf<8>(a.res + o);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float w = v[u].v[i] * sc[i] + sh[i];
-            if (a.res) w = bfround(w) + rv[u].v[i];   // autocast: bn(x) is a bf16 tensor before the add
-            if (a.relu) w = w <= 0.0f ? 0.0f : w;     // ATen relu (NaN propagates)
-            v[u].v[i] = w;
-        }
-        st_bf<8>(a.out + (size_t)row * a.C + c0, v[u]);
-    }
-    ROW_LOOP_END
-}
-
-__global__ __launch_bounds__(NT) void k_bns_bwd_apply(BNSArgs a) {
-    __shared__ double tot[2 * 512];
-    __shared__ double scratch[2 * 1024];
-    __shared__ float coef[3 * 512];
-    bns_totals(a, tot, scratch);
-    const int t = threadIdx.x;
-    const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += NT) {   // dx = k1 (g - k2 - (x - mu) k3), folded as in k_bnr_bwd
-        const double isd = a.save_invstd[c], k1 = (double)(a.gamma[c] * a.save_invstd[c]);
-        const double k2 = tot[c] * inv_m, k3 = tot[a.C + c] * isd * isd * inv_m;
-        coef[c] = (float)k1;                                                // kg
-        coef[a.C + c] = (float)(-k1 * k3);                                  // kx
-        coef[2 * a.C + c] = (float)(k1 * (k3 * (double)a.save_mean[c] - k2));   // k0
-        if (blockIdx.x == 0) {
-            a.dbeta[c] = (float)tot[c];
-            a.dgamma[c] = (float)(tot[a.C + c] * isd);
-        }
-    }
-    __syncthreads();
-    const int cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * 8;
-    float kg[8], kx[8], k0[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) kg[i] = coef[c0 + i], kx[i] = coef[a.C + c0 + i], k0[i] = coef[2 * a.C + c0 + i];
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    uint4 gq[U], xq[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
-        gq[u] = bns_grad(a, o);
-        xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-        const size_t o = (size_t)row * a.C + c0;
-        float g[8], v[8];
-        unpack8f(gq[u], g);
-        unpack8f(xq[u], v);
-        Vec<8> d;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d.v[i] = fmaf(kg[i], g[i], fmaf(kx[i], v[i], k0[i]));
-        st_bf<8>(a.out + o, d);
-        if (a.dres) *reinterpret_cast<uint4*>(a.dres + o) = gq[u];
-    }
-    ROW_LOOP_END
-}
-
-// split geometry: statistics rows per workgroup a multiple of BNS_U * sTR with P <= BNS_MAXP
-// workgroups; apply = the [M, C] pass geometry (NT threads, <= TARGET_BLOCKS workgroups).  P <= the
-// apply geometry's nblk, so psfm_netops_ws_floats(M, C) holds the partial rows.
-inline bool bns_geometry(int M, int C, BNSArgs& a) {
-    if (C % 8 || C > 512 || M < 1) return false;
-    const Geo g = geometry(M, C, 8);
-    a.G = g.G, a.TR = g.TR, a.rpb = g.rpb, a.nblk = g.nblk;
-    a.sTR = BNS_NT / g.G;
-    const int step = a.sTR * BNS_U, per = (M + BNS_MAXP - 1) / BNS_MAXP;
-    a.srpb = std::max(step, (per + step - 1) / step * step);
-    a.P = (M + a.srpb - 1) / a.srpb;
-    return a.P <= BNS_MAXP && a.P <= g.nblk;
-}
-
 #ifdef PSFM_AB_VARIANTS
 // ------------------------------------------------------------------------------------------
 // Two-launch BatchNorm for the layers too large to be resident (the ResNet stem, layer1, layer2):
@@ -3134,18 +2866,16 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
     return 0;
 }
 
-// BatchNorm forms by the BN_PATH knob: 0 (default) the resident kernels up to BN_RES_MAXM rows, the
-// split two-launch kernels above that; 1 the ticket kernels everywhere, 2 the three-pass kernels
-// (both A/B builds only).  Returns 0 resident, 1 ticket, 2 three-pass, 3 split, -1 none.
+// BatchNorm forms by the BN_PATH knob: 0 (default) the resident kernels up to BN_RES_MAXM rows and the
+// two-launch ticket kernels above; 1 the ticket kernels everywhere; 2 the three-pass kernels (A/B
+// builds only).  Returns 0 resident, 1 ticket, 2 three-pass, -1 none.
 static int bn_form(int M, int C, BNRGeo& rg, bool bwd) {
     const int path = knob(KNOB_BN_PATH);
     if (path == 0 && bnr_geometry(M, C, rg, bwd)) return 0;
 #ifdef PSFM_AB_VARIANTS
     if (path == 2) return 2;
-    if (path == 1 && C % 8 == 0 && C <= 512 && M >= 1) return 1;
+    if (C % 8 == 0 && C <= 512 && M >= 1) return 1;
 #endif
-    BNSArgs sa{};
-    if (path == 0 && bns_geometry(M, C, sa)) return 3;
     return -1;
 }
 static bool bnr_path() { return knob(KNOB_BN_PATH) == 0; }
@@ -3158,7 +2888,7 @@ int psfm_bn_act_resident(int M, int C) {
 int psfm_bn_act_fused(int M, int C) {
     BNRGeo g;
     const int f = bn_form(M, C, g, false);
-    return f == 0 || f == 1 || f == 3 ? 1 : 0;
+    return f == 0 || f == 1 ? 1 : 0;
 }
 
 #ifdef PSFM_AB_VARIANTS
@@ -3199,22 +2929,6 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
         return 0;
     }
 #endif
-    if (form == 3) {  // two launches (split)
-        if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
-        BNSArgs a{};
-        bns_geometry(M, C, a);
-        a.x = static_cast<const uint16_t*>(x);
-        a.res = static_cast<const uint16_t*>(res);
-        a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
-        a.save_mean = save_mean, a.save_invstd = save_invstd;
-        a.out = static_cast<uint16_t*>(y);
-        a.part = ws, a.momentum = momentum, a.eps = eps, a.M = M, a.C = C, a.relu = relu;
-        hipStream_t st = (hipStream_t)stream;
-        hipLaunchKernelGGL(k_bns_stats<false>, dim3(a.P), dim3(BNS_NT), 0, st, a);
-        hipLaunchKernelGGL(k_bns_fwd_apply, dim3(a.nblk), dim3(NT), 0, st, a);
-        NETOPS_LAUNCH_CHECK();
-        return 0;
-    }
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.x = static_cast<const uint16_t*>(x);
@@ -3301,24 +3015,6 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
         return 0;
     }
 #endif
-    if (form == 3) {  // two launches (split)
-        if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
-        BNSArgs a{};
-        bns_geometry(M, C, a);
-        a.dy = static_cast<const uint16_t*>(dy);
-        a.dy1 = static_cast<const uint16_t*>(dy1), a.dy2 = static_cast<const uint16_t*>(dy2);
-        a.y = static_cast<const uint16_t*>(y);
-        a.x = static_cast<const uint16_t*>(x);
-        a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
-        a.out = static_cast<uint16_t*>(dx);
-        a.dres = static_cast<uint16_t*>(dres);
-        a.dgamma = dgamma, a.dbeta = dbeta, a.part = ws, a.M = M, a.C = C, a.relu = relu;
-        hipStream_t st = (hipStream_t)stream;
-        hipLaunchKernelGGL(k_bns_stats<true>, dim3(a.P), dim3(BNS_NT), 0, st, a);
-        hipLaunchKernelGGL(k_bns_bwd_apply, dim3(a.nblk), dim3(NT), 0, st, a);
-        NETOPS_LAUNCH_CHECK();
-        return 0;
-    }
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.dy = static_cast<const uint16_t*>(dy);

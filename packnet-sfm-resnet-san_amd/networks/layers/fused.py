@@ -26,9 +26,9 @@ ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
 # (profiles/r02/netops_ab): conv bias + ReLU / sigmoid and bias + GroupNorm + ReLU beat the op
 # chain (972 -> 1025 img/s together).  BatchNorm: "resident" = the one-launch resident kernels where
 # a workgroup holds the layer (psfm_bn_act_resident: ResNet18 layer3 / layer4), MIOpen's BatchNorm
-# elsewhere; "all" = every shape the library's fused BatchNorm takes (psfm_bn_act_fused: resident, else
-# the split two-launch kernels; A/B builds add the ticket and three-pass forms, which lost:
-# profiles/r05/bn); False = MIOpen everywhere.  bench.py --fused-nets overrides.
+# elsewhere; "all" = every shape the library's fused BatchNorm takes (psfm_bn_act_fused: the same on
+# the product library; A/B builds add the two-launch ticket kernels, which lost: profiles/r05/bn);
+# False = MIOpen everywhere.  bench.py --fused-nets overrides.
 FUSE = {"bias": True, "gn": True, "bn": "resident"}
 
 
@@ -308,21 +308,19 @@ def _stem_pool_ok(y, pool):
 def bn_relu_maxpool(x, bn, pool, nout=2):
     """The ResNet stem after conv1 (torchvision ResNet through resnet_encoder.py:89-92):
     skip = relu(bn(x)), pooled = pool(skip).  Returns (skip, pooled) or, nout = 2, (skip, pooled,
-    pooled's fork view) for layer1's first block (conv1 and identity).  The BatchNorm runs as
-    bn_act routes it (MIOpen's, or the split fused kernels under FUSE["bn"] == "all"), then the ReLU
-    and the pooling run as ONE HIP pass each way (_ReLUMaxPool)."""
-    if _stem_pool_ok(x, pool):
-        y = bn_act(x, bn, relu=False)
+    pooled's fork view) for layer1's first block (conv1 and identity).  Where the fused BatchNorm
+    does not take the stem (MIOpen's BatchNorm runs it: M = N * H * W rows is beyond the resident
+    kernels) the ReLU and the pooling run as ONE HIP pass each way (_ReLUMaxPool)."""
+    if not (_fusable(x, "bn") and _bn_fused_shape(x)):
+        y = bn(x)
         if _stem_pool_ok(y, pool):
             if FORK or nout == 1:
                 return _ReLUMaxPool.apply(y, nout)
             skip, h = _ReLUMaxPool.apply(y, 1)
             return (skip,) + fork_plain(h, nout)
         xr, skip = add_relu(y, None, 2)
-    elif _fusable(x, "bn") and _bn_fused_shape(x):
-        xr, skip = bn_act(x, bn, relu=True, nout=2)
     else:
-        xr, skip = add_relu(bn(x), None, 2)
+        xr, skip = bn_act(x, bn, relu=True, nout=2)
     h = pool(xr)
     return (skip,) + fork_plain(h, nout) if nout > 1 else (skip, h)
 

@@ -92,17 +92,13 @@ def test_bias_act_matches_torch(dev, shape, act, bias_bf16):
     assert b.grad.dtype == b.dtype
 
 
-@pytest.fixture(params=["resident8192", "resident2048", "split"])
+@pytest.fixture(params=["resident8192", "resident2048"])
 def bn_path(request, knob):
     """bn_act with the resident kernels taking every geometry they have (BN_RES_MAXM 8192: M = N*H*W <=
-    8192 rows, C % 8 == 0) and with the product limit (2048) — larger layers then run MIOpen's BatchNorm
-    + the fused (add +) ReLU pass — and "split": FUSE["bn"] = "all", the larger layers on the split
-    two-launch kernels."""
+    8192 rows, C % 8 == 0) and with the product limit (2048); larger layers run MIOpen's BatchNorm + the
+    fused (add +) ReLU pass (the library's other fused BatchNorm forms lost and exist in A/B builds only)."""
     knob("BN_RES_MAXM", 8192 if request.param == "resident8192" else 2048)
-    prev = FU.FUSE["bn"]
-    FU.FUSE["bn"] = "all" if request.param == "split" else "resident"
-    yield request.param
-    FU.FUSE["bn"] = prev
+    return request.param
 
 
 @gpu
@@ -153,8 +149,7 @@ def test_bn_act_matches_torch(dev, shape, relu, residual, bn_path):
     # whose dgamma / dbeta sit up to ~5e-2 from the fp32 chain at these sizes; the fused kernels' fp32 /
     # fp64 reductions are held to 2e-2
     from packnet_sfm_amd import _hip
-    M = shape[0] * shape[2] * shape[3]
-    fused = bool(_hip.lib().psfm_bn_act_resident(M, C)) or (bn_path == "split" and bool(_hip.lib().psfm_bn_act_fused(M, C)))
+    fused = bool(_hip.lib().psfm_bn_act_resident(shape[0] * shape[2] * shape[3], C))
     ptol = 2e-2 if fused else 1e-1
     _close(bn.weight.grad, ref.weight.grad, ptol)
     _close(bn.bias.grad, ref.bias.grad, ptol)
@@ -210,16 +205,14 @@ def test_gn_act_matches_torch(dev, shape, gn_path):
 
 
 @gpu
-@pytest.mark.parametrize("shape,residual", [((4, 256, 12, 40), True), ((4, 512, 6, 20), False),
-                                            ((4, 64, 48, 160), True), ((4, 128, 24, 80), False)])
-def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual, monkeypatch):
-    """The fused BatchNorm — resident (one launch each way) and split (two: partial rows, then every
-    apply workgroup sums them in the same fixed order) — has fixed-order reductions and no atomics:
-    eager calls repeat bit for bit, and a HIP-graph capture of forward + backward replays the eager
-    results bit for bit, twice (running statistics included)."""
+@pytest.mark.parametrize("shape,residual", [((4, 256, 12, 40), True), ((4, 512, 6, 20), False)])
+def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual):
+    """The resident BatchNorm (one launch each way, fixed-order reductions, no atomics): eager calls
+    repeat bit for bit, and a HIP-graph capture of forward + backward replays the eager results bit for
+    bit, twice (running statistics included)."""
     from packnet_sfm_amd import _hip
     N, C, H, W = shape
-    monkeypatch.setitem(FU.FUSE, "bn", "all")
+    assert _hip.lib().psfm_bn_act_resident(N * H * W, C) == 1
     assert _hip.lib().psfm_bn_act_fused(N * H * W, C) == 1
     g = torch.Generator(device="cpu").manual_seed(11)
     x = _cl(torch.randn(shape, generator=g) + 0.2).to(dev, torch.bfloat16)
@@ -266,21 +259,18 @@ def test_fused_bn_is_bitwise_deterministic_and_captures(dev, shape, residual, mo
 def test_bn_policies_route_the_shapes(dev, monkeypatch):
     """FUSE["bn"] == "resident" (the product default): only the layers the resident kernels take (M <=
     2048 rows: ResNet18 layer3 / layer4) run fused, the larger ones and C % 8 != 0 MIOpen's BatchNorm;
-    "all" adds the larger layers (the split two-launch kernels); C % 8 != 0 stays on MIOpen."""
+    "all" routes the same shapes on the product library (A/B builds add the two-launch form)."""
     calls = []
     orig = FU._BNAct.apply
     monkeypatch.setattr(FU._BNAct, "apply", lambda *a: calls.append(tuple(a[0].shape)) or orig(*a))
     shapes = ((4, 256, 12, 40), (4, 128, 24, 80), (4, 64, 48, 160), (2, 12, 10, 30))
-    try:
-        for policy in ("resident", "all"):
-            FU.FUSE["bn"] = policy
-            for shape in shapes:
-                bn = nn.BatchNorm2d(shape[1]).to(dev).train()
-                x = _cl(torch.randn(shape)).to(dev, torch.bfloat16)
-                FU.bn_act(x, bn, relu=True)
-    finally:
-        FU.FUSE["bn"] = "resident"
-    assert calls == [(4, 256, 12, 40)] + [(4, 256, 12, 40), (4, 128, 24, 80), (4, 64, 48, 160)]
+    for policy in ("resident", "all"):   # the same on the product library (no other fused form)
+        FU.FUSE["bn"] = policy
+        for shape in shapes:
+            bn = nn.BatchNorm2d(shape[1]).to(dev).train()
+            x = _cl(torch.randn(shape)).to(dev, torch.bfloat16)
+            FU.bn_act(x, bn, relu=True)
+    assert calls == [(4, 256, 12, 40)] * 2
 
 
 @gpu
