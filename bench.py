@@ -132,6 +132,9 @@ def parse(argv=None):
                          "gn (GroupNorm + ReLU); default: the measured winners (networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
+    ap.add_argument("--no-net-inputs", action="store_true",
+                    help="the nets' input normalisation / concatenation + autocast casts as ATen ops instead of "
+                         "psfm_normalize_bf16 / psfm_cat_channels_bf16")
     ap.add_argument("--no-stem-pool", action="store_true",
                     help="stem relu + max-pool as psfm_add_relu + ATen's max-pool instead of psfm_relu_maxpool")
     ap.add_argument("--no-fork", action="store_true",
@@ -616,6 +619,7 @@ def main():
     fused.ADD_RELU = not args.no_add_relu
     fused.FORK = not args.no_fork
     fused.STEM_POOL = not args.no_stem_pool
+    fused.NET_INPUTS = not args.no_net_inputs
     torch.manual_seed(0)  # identical initial weights on every rank (the trainer also broadcasts them)
     torch.backends.cudnn.benchmark = not args.no_miopen_find
     torch.backends.cudnn.deterministic = args.deterministic != "none"

@@ -136,6 +136,17 @@ int psfm_relu_mask_bwd(const void* dy, const void* y, long long n, void* dz, voi
 int psfm_relu_mask_bwd_sum(const void* dy, const void* dy1, const void* dy2, const void* y, long long n, void* dz,
                            void* stream);
 
+/* The nets' fp32 input images as the bf16 first-convolution inputs, one pass each (ATen: sub, div,
+ * autocast cast / cat, cast).  psfm_normalize_bf16: y[i] = bf16((x[i] - sub) * mul) over n elements
+ * of any dense layout (y keeps x's), x 16-byte and y 8-byte aligned — the depth encoder's
+ * (x - 0.45) / 0.225 (resnet_encoder.py:89) with mul = 1.0f / 0.225f, which is how ATen divides by a
+ * scalar.  psfm_cat_channels_bf16: NHWC concatenation along channels of k <= 4 fp32 NHWC images of
+ * `pixels` pixels each (channels[q] per pixel, <= 32 in all) into bf16 y [pixels, sum channels] — PoseNet's
+ * torch.cat([image, *context], 1) (PoseNet.py) + its cast. */
+int psfm_normalize_bf16(const float* x, long long n, float sub, float mul, void* y, void* stream);
+int psfm_cat_channels_bf16(int k, const float* const* xs, const int* channels, long long pixels, void* y,
+                           void* stream);
+
 /* The ResNet stem's ReLU + MaxPool2d(kernel 3, stride 2, padding 1) (torchvision ResNet through
  * resnet_encoder.py: relu(bn1(conv1(x))) feeds the max-pool and the decoder's first skip) in ONE pass:
  * x = the BatchNorm output, bf16 NHWC [N, H, W, C] (H, W even, C % 8 == 0); writes relu_out (same

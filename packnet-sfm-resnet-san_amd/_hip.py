@@ -150,6 +150,8 @@ def lib():
         "psfm_add_relu_fwd": ([V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_relu_mask_bwd": ([V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_relu_mask_bwd_sum": ([V, V, V, V, ctypes.c_longlong, V, V], c_int),
+        "psfm_normalize_bf16": ([V, ctypes.c_longlong, c_float, c_float, V, V], c_int),
+        "psfm_cat_channels_bf16": ([c_int, V, V, ctypes.c_longlong, V, V], c_int),
         "psfm_relu_maxpool_fwd": ([V, c_int, c_int, c_int, c_int, V, V, V, V], c_int),
         "psfm_relu_maxpool_bwd": ([V, V, V, V, V, c_int, c_int, c_int, c_int, V, V], c_int),
         "psfm_upcat_fwd": ([V, V, c_int, c_int, c_int, c_int, c_int, V, V], c_int),
@@ -209,6 +211,7 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_bn_act_fwd", "psfm_bn_act_bwd", "psfm_bn_act_resident", "psfm_bn_act_fused", "psfm_gn_act_fwd", "psfm_gn_act_bwd", "psfm_netops_last_error",
             "psfm_add_relu_fwd", "psfm_relu_mask_bwd", "psfm_relu_mask_bwd_sum", "psfm_bias_act_bwd_sum",
             "psfm_bn_act_bwd_sum", "psfm_relu_maxpool_fwd", "psfm_relu_maxpool_bwd",
+            "psfm_normalize_bf16", "psfm_cat_channels_bf16",
             "psfm_upcat_fwd", "psfm_upcat_bwd", "psfm_upcat_bias_relu_fwd", "psfm_upcat_bias_relu_bwd",
             "psfm_upcat_ws_floats",
             "psfm_depth_metrics", "psfm_metrics_last_error",

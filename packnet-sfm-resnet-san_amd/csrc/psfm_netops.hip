@@ -2651,6 +2651,64 @@ __global__ __launch_bounds__(256) void k_relu_maxpool_bwd(PoolArgs a) {
         }
 }
 
+// ------------------------------------------------------------------------------------------
+// The nets' input images in bf16, in one pass each: the depth encoder's (x - 0.45) / 0.225
+// (resnet_encoder.py:89) and PoseNet's channel concatenation of target + contexts (PoseNet.py:
+// torch.cat([image, *context], 1)), each followed by autocast's bf16 cast for the first convolution
+// — ATen runs sub, div, cast / cat, cast as separate passes over the fp32 images.  Same arithmetic:
+// ATen's sub with a scalar is x + (-1 * a) = x - a in fp32, and its true division by a CPU scalar
+// multiplies by the fp32 reciprocal (BinaryDivTrueKernel.cu), so y = bf16((x - a) * m) with m =
+// 1.0f / b computed by the caller; the cast rounds to nearest even.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_normalize_bf16(const float* __restrict__ x, long long n, float a, float m,
+                                                        uint16_t* __restrict__ y) {
+    const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i);
+        uint2 o;
+        o.x = (uint32_t)f2bf((v.x - a) * m) | ((uint32_t)f2bf((v.y - a) * m) << 16);
+        o.y = (uint32_t)f2bf((v.z - a) * m) | ((uint32_t)f2bf((v.w - a) * m) << 16);
+        *reinterpret_cast<uint2*>(y + i) = o;
+    } else {
+        for (long long j = i; j < n; ++j) y[j] = f2bf((x[j] - a) * m);
+    }
+}
+
+struct CatArgs {
+    const float* x[4];
+    int c[4];
+    int k, ctot, pixels;
+};
+
+// NHWC: a workgroup per CAT_PX pixels.  Each input's slice of them (CAT_PX * c[q] consecutive floats)
+// is read coalesced, converted and scattered into the block's output rows in LDS, then the block's
+// CAT_PX * ctot bf16 values leave as coalesced 4-byte words (32-bit indexing: the host checks
+// pixels * ctot < 2^31, ctot <= CAT_MAXC).
+constexpr int CAT_PX = 256, CAT_MAXC = 32;
+
+__global__ __launch_bounds__(256) void k_cat_channels_bf16(CatArgs a, uint16_t* __restrict__ y) {
+    __shared__ uint16_t tile[CAT_PX * CAT_MAXC];
+    const int t = threadIdx.x, p0 = blockIdx.x * CAT_PX, npx = min(CAT_PX, a.pixels - p0);
+    int off = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (q >= a.k) break;
+        const int cq = a.c[q], ne = npx * cq;
+        const float* xi = a.x[q] + (size_t)p0 * cq;
+        for (int e = t; e < ne; e += 256) {
+            const int pp = e / cq;
+            tile[pp * a.ctot + off + (e - pp * cq)] = f2bf(xi[e]);
+        }
+        off += cq;
+    }
+    __syncthreads();
+    const int nout = npx * a.ctot;
+    uint16_t* o = y + (size_t)p0 * a.ctot;
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
+    for (int w = t; w < nout / 2; w += 256) reinterpret_cast<uint32_t*>(o)[w] = t32[w];
+    if ((nout & 1) && t == 0) o[nout - 1] = tile[nout - 1];
+}
+
 }  // namespace
 
 extern "C" {
@@ -2659,6 +2717,37 @@ static int pool_setup(PoolArgs& a, int N, int H, int W, int C, const char* who) 
     if (N < 1 || H < 2 || W < 2 || (H & 1) || (W & 1) || C < 8 || (C % 8)) return fail(-1, who);
     a.N = N, a.H = H, a.W = W, a.C = C, a.Ho = H / 2, a.Wo = W / 2, a.CV = C / 8;
     a.n = (long long)N * a.Ho * a.Wo * a.CV;
+    return 0;
+}
+
+int psfm_normalize_bf16(const float* x, long long n, float sub, float mul, void* y, void* stream) {
+    if (!x || !y || n < 1 || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 7))
+        return fail(-1, "normalize_bf16: bad arguments (16-byte aligned x, 8-byte aligned y)");
+    const long long threads = (n + 3) / 4;
+    hipLaunchKernelGGL(k_normalize_bf16, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       x, n, sub, mul, static_cast<uint16_t*>(y));
+    NETOPS_LAUNCH_CHECK();
+    return 0;
+}
+
+int psfm_cat_channels_bf16(int k, const float* const* xs, const int* channels, long long pixels, void* y,
+                           void* stream) {
+    if (k < 1 || k > 4 || !xs || !channels || !y || pixels < 1) return fail(-1, "cat_channels_bf16: bad arguments");
+    CatArgs a{};
+    a.k = k;
+    long long ctot = 0;
+    for (int q = 0; q < k; ++q) {
+        if (!xs[q] || channels[q] < 1) return fail(-1, "cat_channels_bf16: bad input");
+        a.x[q] = xs[q], a.c[q] = channels[q];
+        ctot += channels[q];
+    }
+    if (pixels * ctot >= (1LL << 31) || ctot > CAT_MAXC || (reinterpret_cast<uintptr_t>(y) & 3))
+        return fail(-1, "cat_channels_bf16: too large (pixels * channels < 2^31, <= 32 channels) or y not 4-byte aligned");
+    a.ctot = (int)ctot;
+    a.pixels = (int)pixels;
+    hipLaunchKernelGGL(k_cat_channels_bf16, dim3((unsigned)((pixels + CAT_PX - 1) / CAT_PX)), dim3(256), 0,
+                       (hipStream_t)stream, a, static_cast<uint16_t*>(y));
+    NETOPS_LAUNCH_CHECK();
     return 0;
 }
 

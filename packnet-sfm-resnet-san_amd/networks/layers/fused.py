@@ -16,6 +16,7 @@ the photometric loss (losses/_hip_photometric.py) has no such path.
 """
 import ctypes
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -254,6 +255,50 @@ def bn_act(x, bn, relu=True, residual=None, nout=1):
     return fork_plain(torch.relu(y) if relu else y, nout)
 
 
+NET_INPUTS = True   # the nets' bf16 input images in one HIP pass (bench.py --no-net-inputs: ATen's chain)
+
+
+def _autocast_bf16():
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def normalize_input(x, sub=0.45, div=0.225):
+    """(x - sub) / div, the depth encoder's input normalisation (resnet_encoder.py:89).  Under bf16
+    autocast on a ROCm device (where the first convolution casts it to bf16 anyway) ONE HIP pass
+    (include/psfm_netops.h psfm_normalize_bf16) returns that bf16 tensor, bit for bit what ATen's sub,
+    div (x * fp32 reciprocal) and cast give, in x's layout; otherwise the op chain."""
+    if (NET_INPUTS and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and not x.requires_grad
+            and _autocast_bf16() and (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last))
+            and x.data_ptr() % 16 == 0):
+        y = torch.empty_like(x, dtype=torch.bfloat16)
+        if y.stride() == x.stride():
+            mul = float(np.float32(1.0) / np.float32(div))
+            _hip.check(_hip.lib().psfm_normalize_bf16(_hip.ptr(x), x.numel(), ctypes.c_float(sub), ctypes.c_float(mul),
+                                                      _hip.ptr(y), _hip.stream(x.device)), "psfm_normalize_bf16")
+            return y
+    return (x - sub) / div
+
+
+def cat_input(images):
+    """torch.cat(images, 1), PoseNet's input (target + contexts, PoseNet.py).  Under bf16 autocast on a
+    ROCm device with channels_last fp32 images: ONE HIP pass (psfm_cat_channels_bf16) into the bf16
+    channels_last tensor the first convolution would cast the concatenation to; otherwise torch.cat."""
+    x0 = images[0]
+    if (NET_INPUTS and 1 <= len(images) <= 4 and _autocast_bf16() and all(
+            t.is_cuda and t.dtype == torch.float32 and t.dim() == 4 and not t.requires_grad
+            and t.device == x0.device and t.shape[0] == x0.shape[0] and t.shape[2:] == x0.shape[2:]
+            and t.is_contiguous(memory_format=torch.channels_last) for t in images)):
+        N, _, H, W = x0.shape
+        cs = [int(t.shape[1]) for t in images]
+        y = torch.empty((N, sum(cs), H, W), device=x0.device, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        P, CI = ctypes.c_void_p * len(images), ctypes.c_int * len(images)
+        _hip.check(_hip.lib().psfm_cat_channels_bf16(len(images), P(*[t.data_ptr() for t in images]), CI(*cs),
+                                                     N * H * W, _hip.ptr(y), _hip.stream(x0.device)),
+                   "psfm_cat_channels_bf16")
+        return y
+    return torch.cat(images, 1)
+
+
 class _ReLUMaxPool(torch.autograd.Function):
     """The ResNet stem's relu -> MaxPool2d(3, 2, 1) (include/psfm_netops.h psfm_relu_maxpool_fwd/bwd):
     one pass each way for the ReLU, the pooling (uint8 window positions instead of ATen's int64
@@ -264,14 +309,12 @@ class _ReLUMaxPool(torch.autograd.Function):
     def forward(ctx, y, nout=2):
         N, C, H, W = y.shape
         r = torch.empty_like(y, memory_format=torch.channels_last)
-        p = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=y.dtype).contiguous(
-            memory_format=torch.channels_last)
-        am = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=torch.uint8).contiguous(
-            memory_format=torch.channels_last)
+        # allocated channels_last (empty(...).contiguous(channels_last) would launch a copy of garbage)
+        p = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=y.dtype, memory_format=torch.channels_last)
+        am = torch.empty((N, C, H // 2, W // 2), device=y.device, dtype=torch.uint8, memory_format=torch.channels_last)
         _hip.check(_hip.lib().psfm_relu_maxpool_fwd(_hip.ptr(y), N, H, W, C, _hip.ptr(r), _hip.ptr(p), _hip.ptr(am),
                                                     _hip.stream(y.device)), "psfm_relu_maxpool_fwd")
         ctx.save_for_backward(r, am)
-        ctx.mark_non_differentiable(am)
         return (r,) + _fork(p, nout) if nout > 1 else (r, p)
 
     @staticmethod
@@ -281,8 +324,7 @@ class _ReLUMaxPool(torch.autograd.Function):
         N, C, H, W = r.shape
         gs = [_rows(g.to(r.dtype)) for g in dps if g is not None]
         if not gs:
-            gs = [torch.zeros((N, C, H // 2, W // 2), device=r.device, dtype=r.dtype).contiguous(
-                memory_format=torch.channels_last)]
+            gs = [torch.zeros((N, C, H // 2, W // 2), device=r.device, dtype=r.dtype, memory_format=torch.channels_last)]
         while len(gs) > 2:
             gs = [gs[0] + gs[1]] + gs[2:]
         dskip = None if dskip is None else _rows(dskip.to(r.dtype))

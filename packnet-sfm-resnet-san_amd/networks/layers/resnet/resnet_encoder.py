@@ -10,7 +10,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from ..fused import bn_act, bn_relu_maxpool
+from ..fused import bn_act, bn_relu_maxpool, normalize_input
 
 
 def conv3x3(i, o, stride=1):
@@ -127,7 +127,7 @@ class ResnetEncoder(nn.Module):
         kernel, not by autograd's bf16 add kernels.  The stem's ReLU + max-pool is one HIP pass each way
         (fused.bn_relu_maxpool), its pooled output forked for layer1's first block (conv1, identity)."""
         e = self.encoder
-        skip, *h = bn_relu_maxpool(e.conv1((input_image - 0.45) / 0.225), e.bn1, e.maxpool, nout=2)
+        skip, *h = bn_relu_maxpool(e.conv1(normalize_input(input_image, 0.45, 0.225)), e.bn1, e.maxpool, nout=2)
         feats = [skip]
         layers = (e.layer1, e.layer2, e.layer3, e.layer4)
         for li, layer in enumerate(layers):

@@ -3,7 +3,7 @@ blocks over [target, contexts] stacked on channels, 1x1 head, spatial mean, x0.0
 import torch
 import torch.nn as nn
 
-from ..layers.fused import conv_nobias, gn_act
+from ..layers.fused import cat_input, conv_nobias, gn_act
 
 
 def conv_gn(in_planes, out_planes, kernel_size=3):
@@ -35,7 +35,7 @@ class PoseNet(nn.Module):
 
     def forward(self, image, context):
         assert len(context) == self.nb_ref_imgs
-        x = torch.cat([image, *context], 1)
+        x = cat_input([image, *context])   # under bf16 autocast: the bf16 concatenation in one pass
         for i in range(7):  # conv -> (bias + GroupNorm + ReLU) fused epilogue (fused.py)
             conv, gn, _ = getattr(self, f"conv{i + 1}")
             x = gn_act(conv_nobias(conv, x), conv.bias, gn, relu=True)

@@ -586,6 +586,63 @@ def test_stem_relu_maxpool_routes_the_resnet_stem(dev):
 
 
 @gpu
+@pytest.mark.parametrize("shape,cl", [((4, 3, 192, 640), True), ((4, 3, 192, 640), False), ((1, 3, 5, 7), True),
+                                      ((2, 3, 9, 11), False)])
+def test_net_input_normalisation_equals_the_op_chain_bitwise(dev, shape, cl):
+    """fused.normalize_input under bf16 autocast (psfm_normalize_bf16) = ATen's (x - 0.45) / 0.225 +
+    autocast's bf16 cast, bit for bit and in the same layout (odd sizes: the scalar tail)."""
+    g = torch.Generator(device="cpu").manual_seed(14)
+    x = torch.rand(shape, generator=g) * 1.2 - 0.1
+    x.view(-1)[:3] = torch.tensor([0.45, 0.0, 1.0])
+    x = (_cl(x) if cl else x).to(dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = FU.normalize_input(x, 0.45, 0.225)   # bf16 out = the HIP pass (the op chain returns fp32)
+        ref = ((x - 0.45) / 0.225).to(torch.bfloat16)
+    assert y.dtype == torch.bfloat16 and y.stride() == ref.stride() and y.stride() == x.stride()
+    assert torch.equal(y, ref)
+    FU.NET_INPUTS = False
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert FU.normalize_input(x, 0.45, 0.225).dtype == torch.float32   # the op chain
+    finally:
+        FU.NET_INPUTS = True
+
+
+@gpu
+@pytest.mark.parametrize("k,shape", [(3, (4, 3, 192, 640)), (3, (4, 3, 24, 40)), (2, (2, 3, 24, 40)),
+                                     (1, (2, 3, 24, 40)), (3, (1, 3, 5, 7))])   # 35 px: a partial block, odd size
+def test_pose_input_concatenation_equals_the_op_chain_bitwise(dev, k, shape):
+    """fused.cat_input under bf16 autocast (psfm_cat_channels_bf16) = torch.cat of the channels_last
+    fp32 images + the bf16 cast, bit for bit, channels_last."""
+    g = torch.Generator(device="cpu").manual_seed(15)
+    ims = [_cl(torch.rand(shape, generator=g)).to(dev) for _ in range(k)]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = FU.cat_input(ims)
+        ref = torch.cat(ims, 1).to(torch.bfloat16)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    assert ref.is_contiguous(memory_format=torch.channels_last) and torch.equal(y, ref)
+
+
+@gpu
+def test_posenet_forward_unchanged_by_the_fused_inputs(dev):
+    """PoseNet's forward under bf16 autocast is bit-identical with and without the fused input pass."""
+    from packnet_sfm_amd.networks.pose.PoseNet import PoseNet
+    torch.manual_seed(3)
+    net = PoseNet(nb_ref_imgs=2, rotation_mode="euler").to(dev).train().to(memory_format=torch.channels_last)
+    g = torch.Generator(device="cpu").manual_seed(16)
+    ims = [_cl(torch.rand((2, 3, 64, 96), generator=g)).to(dev) for _ in range(3)]
+    outs = []
+    for flag in (True, False):
+        FU.NET_INPUTS = flag
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                outs.append(net(ims[0], ims[1:]).detach().float())
+        finally:
+            FU.NET_INPUTS = True
+    assert torch.equal(outs[0], outs[1])
+
+
+@gpu
 def test_gn_backward_captures_when_its_forward_ran_on_the_capture_stream(dev):
     """tools/gn_bench.py's round-3 capture segfault, resolved (profiles/r04/cap): 20 captured
     torch.autograd.grad calls through psfm_gn_act_bwd at [6, 64, 192, 640] replay bit-exactly when
