@@ -337,6 +337,19 @@ def test_cpu_path_is_the_reference_op_chain():
     b = torch.randn(8)
     assert torch.equal(FU.gn_act(x, b, gn, True), torch.relu(gn(x + b.view(1, -1, 1, 1))))
     assert torch.equal(FU.bias_act(x, b, FU.ACT_SIGMOID, nn.Module()), torch.sigmoid(x + b.view(1, -1, 1, 1)))
+    # the stem: relu -> MaxPool2d(3, 2, 1), the skip and the pooled output forked for two consumers
+    pool = nn.MaxPool2d(3, 2, 1)
+    xs = torch.randn(2, 8, 6, 10)
+    bn2 = nn.BatchNorm2d(8).train()
+    ref2 = nn.BatchNorm2d(8).train()
+    ref2.load_state_dict(bn2.state_dict())
+    skip, h0, h1 = FU.bn_relu_maxpool(xs, bn2, pool, nout=2)
+    rs = torch.relu(ref2(xs))
+    assert torch.equal(skip, rs) and torch.equal(h0, pool(rs)) and torch.equal(h1, pool(rs))
+    # the nets' input images: the reference's normalisation and concatenation (fp32 on CPU)
+    ims = [torch.rand(2, 3, 4, 6) for _ in range(3)]
+    assert torch.equal(FU.normalize_input(ims[0], 0.45, 0.225), (ims[0] - 0.45) / 0.225)
+    assert torch.equal(FU.cat_input(ims), torch.cat(ims, 1))
 
 
 @gpu
