@@ -132,6 +132,8 @@ def parse(argv=None):
                          "gn (GroupNorm + ReLU); default: the measured winners (networks/layers/fused.py FUSE)")
     ap.add_argument("--no-add-relu", action="store_true",
                     help="BasicBlock tail relu(bn2 + identity) as the torch op chain instead of psfm_add_relu")
+    ap.add_argument("--pose-first", action="store_true",
+                    help="enqueue the pose net's branch before the depth net (A/B of the step graph's node order)")
     ap.add_argument("--no-net-inputs", action="store_true",
                     help="the nets' input normalisation / concatenation + autocast casts as ATen ops instead of "
                          "psfm_normalize_bf16 / psfm_cat_channels_bf16")
@@ -626,6 +628,7 @@ def main():
     if args.deterministic == "all":
         torch.use_deterministic_algorithms(True, warn_only=True)
     model = build_model(args, device)
+    model.pose_first = args.pose_first
     if not args.nchw:
         to_channels_last(model)
     opt = make_optimizer(model, 1e-4, 1e-4, capturable=not args.eager, fused=True)

@@ -30,6 +30,10 @@ class SfmModel(BaseModel):
         # the depth net's stored maps; models/model_utils.upsample_output)
         self.lazy_upsample = lazy_upsample
         self.overlap_pose_net = overlap_pose_net
+        # A/B (bench.py --pose-first): enqueue the pose branch before the depth net.  Measured equal
+        # (profiles/r05/posefirst: 1146-1157 vs 1150-1159 img/s): the graph launch enqueues the branches
+        # in node order, so the depth net then waits for the pose forward, and the pose backward runs last
+        self.pose_first = False
         self._side_streams = {}
         self.depth_net = depth_net
         self.pose_net = pose_net
@@ -75,9 +79,13 @@ class SfmModel(BaseModel):
             cur = torch.cuda.current_stream(batch["rgb"].device)
             side = self._side_stream(batch["rgb"].device)
             side.wait_stream(cur)
+            if self.pose_first:
+                with torch.cuda.stream(side):
+                    poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
             depth_output = self.compute_depth_net(batch, force_flip=force_flip, **kwargs)
-            with torch.cuda.stream(side):
-                poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
+            if not self.pose_first:
+                with torch.cuda.stream(side):
+                    poses = self.compute_pose_net(batch["rgb"], batch["rgb_context"])
             cur.wait_stream(side)
             for p in poses:  # allocated on the side stream, consumed on the current one
                 p.mat.record_stream(cur)
