@@ -64,7 +64,9 @@ def ResidualBlock(in_channels, out_channels, num_blocks, stride, dropout=None):
 
 
 class InvDepth(nn.Module):
-    """3x3 conv -> sigmoid / min_depth."""
+    """3x3 conv -> sigmoid / min_depth.  As in Conv2D, the zero padding is the convolution's own
+    (`padding=1` == ConstantPad2d(1) + unpadded conv, layers01.py:66-78) instead of a padded copy of
+    the input (and its slice backward): at the full-resolution head that copy is 47 MB each way."""
 
     def __init__(self, in_channels, out_channels=1, min_depth=0.5):
         super().__init__()
@@ -74,7 +76,8 @@ class InvDepth(nn.Module):
         self.activ = nn.Sigmoid()
 
     def forward(self, x):
-        return self.activ(self.conv1(self.pad(x))) / self.min_depth
+        c = self.conv1
+        return self.activ(F.conv2d(x, c.weight, c.bias, c.stride, 1)) / self.min_depth
 
 
 def _channels_last_view(t):
