@@ -96,6 +96,27 @@ def test_fused_path_argument_checks(hip):
     assert L.psfm_pinhole_cam_records(None, None, None, 12, 1, 1, 1, 1.0, None, None) == -1
 
 
+def test_round5_netops_argument_checks(hip):
+    """The round-5 netops entry points refuse bad shapes / pointers before any launch (host-only):
+    the stem pool needs even H, W and C % 8 == 0; the input passes need aligned pointers, 1-4 inputs
+    and <= 32 channels."""
+    L = hip.lib()
+    a = ctypes.c_void_p(4096)
+    assert L.psfm_relu_maxpool_fwd(a, 2, 96, 320, 64, None, a, a, None) == -1          # no relu_out
+    assert L.psfm_relu_maxpool_fwd(a, 2, 95, 320, 64, a, a, a, None) == -1            # odd H
+    assert L.psfm_relu_maxpool_fwd(a, 2, 96, 320, 12, a, a, a, None) == -1            # C % 8
+    assert b"relu_maxpool_fwd" in L.psfm_netops_last_error()
+    assert L.psfm_relu_maxpool_bwd(a, None, None, a, a, 2, 96, 321, 64, a, None) == -1  # odd W
+    assert L.psfm_normalize_bf16(ctypes.c_void_p(4100), 16, 0.45, 1.0, a, None) == -1   # x not 16-byte aligned
+    assert L.psfm_normalize_bf16(a, 0, 0.45, 1.0, a, None) == -1
+    P, CI = ctypes.c_void_p * 5, ctypes.c_int * 5
+    xs, cs = P(*[4096] * 5), CI(*[3] * 5)
+    assert L.psfm_cat_channels_bf16(5, xs, cs, 100, a, None) == -1                    # > 4 inputs
+    assert L.psfm_cat_channels_bf16(2, xs, CI(*[20] * 5), 100, a, None) == -1         # 40 > 32 channels
+    assert L.psfm_cat_channels_bf16(2, xs, cs, 100, ctypes.c_void_p(4098), None) == -1   # y not 4-byte aligned
+    assert b"cat_channels_bf16" in L.psfm_netops_last_error()
+
+
 @pytest.mark.parametrize("field,value,code", [("N", 0, -3), ("N", 5, -3), ("S", 0, -4), ("H", 1, -2),
                                               ("reduce_op", 7, -6)])
 def test_bad_arguments_are_rejected(hip, field, value, code):
