@@ -64,8 +64,8 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
 /* Training-mode BatchNorm2d (+ residual) (+ ReLU):  y = act(gamma (x-mu)/sqrt(var+eps) + beta [+ res]),
  * ONE launch each way where psfm_bn_act_resident(M, C) (ws may be NULL there); other shapes return
  * -3 — the two-launch "ticket" kernels (a statistics pass whose last workgroup finishes the batch
- * statistics) and the round-2 three-pass kernels both lost to MIOpen's BatchNorm and are built into
- * A/B variant libraries only (-DPSFM_AB_VARIANTS, psfm_bn_act_fused there),
+ * statistics) and the round-2 three-pass kernels both lost to MIOpen's BatchNorm and were removed
+ * from the library in round 6 (git 61b4f88 holds them);
  * batch statistics over the M rows, running stats updated as torch does (momentum, unbiased
  * var), save_mean / save_invstd [C] for the backward.  res may be NULL. */
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,

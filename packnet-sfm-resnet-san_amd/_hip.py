@@ -9,6 +9,7 @@ shared with PyTorch-ROCm).
 import ctypes
 import os
 import threading
+import weakref
 
 import torch
 
@@ -193,6 +194,7 @@ def lib():
         "psfm_knob_default": ([c_int], c_int),
         "psfm_knob_value": ([c_int], c_int),
         "psfm_knob_set": ([ctypes.c_char_p, c_int], c_int),
+        "psfm_knob_rejected": ([c_int], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -221,7 +223,8 @@ EXPORTED = ("psfm_workspace_floats", "psfm_photometric_clip_stats", "psfm_photom
             "psfm_augment_plan", "psfm_augment_ws_bytes", "psfm_train_augment", "psfm_gather_frames",
             "psfm_augment_last_error",
             "psfm_pose_from_vec_fwd", "psfm_pose_from_vec_bwd", "psfm_pinhole_cam_records", "psfm_pose_last_error",
-            "psfm_knob_count", "psfm_knob_name", "psfm_knob_default", "psfm_knob_value", "psfm_knob_set")
+            "psfm_knob_count", "psfm_knob_name", "psfm_knob_default", "psfm_knob_value", "psfm_knob_set",
+            "psfm_knob_rejected")
 
 
 def knobs():
@@ -233,8 +236,15 @@ def knobs():
 
 
 def nondefault_knobs():
-    """The knobs whose value differs from the default ({} on the product configuration)."""
-    return {k: v for k, (v, d) in knobs().items() if v != d}
+    """The knobs whose value differs from the default ({} on the product configuration), plus
+    'rejected:<string>' for every PSFM_<NAME> value the library refused at load."""
+    L = lib()
+    out = {k: v for k, (v, d) in knobs().items() if v != d}
+    for i in range(L.psfm_knob_count()):
+        r = L.psfm_knob_rejected(i)
+        if r is not None:
+            out[L.psfm_knob_name(i).decode()] = "rejected:" + r.decode(errors="replace")
+    return out
 
 
 def set_knob(name, value):
@@ -295,6 +305,7 @@ def _install_capture_hooks():
 
     def capture_begin(self, *a, **k):
         global _ACTIVE_CAPTURES
+        _refuse_stray_backward(torch.cuda.current_stream())
         r = begin(self, *a, **k)
         with _CAPTURE_LOCK:
             _ACTIVE_CAPTURES += 1
@@ -312,15 +323,52 @@ def _install_capture_hooks():
     G.capture_begin, G.capture_end, G._psfm_counted = capture_begin, capture_end, True
 
 
+# Autograd contexts of HIP ops whose forward ran outside any capture and whose backward has not run
+# yet (weak: a context leaves the set when its graph is freed).  A capture may not begin on another
+# stream while one of them is alive: PyTorch-ROCm runs a node's backward on its forward's stream, so
+# capturing that backward makes the capturing stream wait on a stream outside the capture, and HIP
+# then segfaults in capture_end — by the time the op's own backward runs, the autograd engine has
+# already recorded that wait, so the refusal has to come before the capture exists.
+_EAGER_CTX = weakref.WeakSet()
+
+
+def note_forward(ctx):
+    """Called first thing in every HIP op's forward: remember a forward that ran outside any
+    capture (with its stream) until its backward runs (capture_guard(ctx))."""
+    if not torch.cuda.is_initialized() or torch.cuda.is_current_stream_capturing():
+        return
+    ctx._psfm_stream = torch.cuda.current_stream().cuda_stream
+    with _CAPTURE_LOCK:
+        _EAGER_CTX.add(ctx)
+
+
+def _refuse_stray_backward(cap_stream):
+    with _CAPTURE_LOCK:
+        stray = [c for c in list(_EAGER_CTX) if getattr(c, "_psfm_stream", None) != cap_stream.cuda_stream]
+    if stray:
+        names = sorted({type(c).__name__ for c in stray})
+        raise RuntimeError(
+            f"psfm: refusing to begin a HIP-graph capture on stream {cap_stream.cuda_stream:#x}: {len(stray)} "
+            f"HIP op forward(s) ({', '.join(names)}) ran outside any capture on another stream and can still be "
+            "backpropagated; a backward captured for them would run on their forward's stream, outside the "
+            "capture (HIP segfaults in capture_end).  Run the backward (or free the graph) first, or run the "
+            "forward inside the same capture, as DDPTrainer.capture does")
+
+
 _install_capture_hooks()
 
 
-def capture_guard():
+def capture_guard(ctx=None):
     """Raise before anything is allocated or launched when this thread is not capturing while a
     HIP-graph capture is in progress — called first thing in every HIP backward: PyTorch-ROCm runs a
     node's backward on its forward's stream, so a backward captured for a forward that ran outside
     the capture would otherwise allocate and launch on a stream the capture does not own, and HIP
-    segfaults in capture_end."""
+    segfaults in capture_end.  `ctx` (the op's autograd context) leaves
+    the set of pending eager forwards (note_forward) here.  The capture_begin hook refuses such a
+    capture before it starts; this check is the last line for anything it cannot see."""
+    if ctx is not None:
+        with _CAPTURE_LOCK:
+            _EAGER_CTX.discard(ctx)
     if _ACTIVE_CAPTURES and not torch.cuda.is_current_stream_capturing():
         # Refuse — but first join this stream into the capture and straight back (an empty fork), so
         # the capture is still well formed when the error unwinds through torch.cuda.graph: the

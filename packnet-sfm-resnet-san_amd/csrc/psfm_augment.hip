@@ -665,17 +665,9 @@ int psfm_train_augment(const psfm_augment_params* p, const uint8_t* src, const i
     uint32_t* part = (uint32_t*)(base + wl.part);
     const int hw = p->out_h * p->out_w;
     int vec = p->out_w % 4 == 0 ? 4 : 1;  // 4-pixel groups never straddle a row
-#ifdef PSFM_AB_VARIANTS
-    if (const char* e = getenv("PSFM_AUGMENT_VEC"))  // A/B variant builds only (tools/augment_scan.sh)
-        if (atoi(e) == 1) vec = 1;
-#endif
     const int nblk = (hw / vec + NT - 1) / NT;
     const size_t lds = (size_t)((3 * g.seg_len + 3) & ~3);
     int nth = NT;
-#ifdef PSFM_AB_VARIANTS
-    if (const char* e = getenv("PSFM_AUGMENT_NTH"))  // A/B variant builds only (tools/augment_scan.sh)
-        nth = std::min(1024, std::max(64, atoi(e) / 64 * 64));
-#endif
     hipLaunchKernelGGL(k_resize_h, dim3(d.rows_tmp, p->n_img), dim3(nth), lds, st, g, src, plan, tmp);
     if (vec == 4) {
         hipLaunchKernelGGL(k_resize_v<4>, dim3(nblk, p->n_img), dim3(NT), 0, st, g, plan, (const uint8_t*)tmp, jitter,

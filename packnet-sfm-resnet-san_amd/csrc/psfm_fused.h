@@ -371,11 +371,16 @@ struct K12 {
         c.load(reinterpret_cast<cfloat*>(rp), B, H, W);
         return c;
     }
-    // the context-paired pinhole record is NOT laundered: the compiler may keep it in SGPRs across
-    // the phases (105.2 vs 107.5 us per K12 call, profiles/r03/k12ab/kbench_variants_1.log)
+    // the context-paired pinhole record, re-loaded (s_load_dwordx16 through the scalar cache) at each
+    // use: held across the phases it lived in SGPRs spilled to VGPR lanes, and every use cost a
+    // v_readlane per dword.  Round 3 measured this the other way (105.2 vs 107.5 us,
+    // profiles/r03/k12ab/kbench_variants_1.log); without SLP packing (build TU_FLAGS) the re-load wins:
+    // 90.9 -> 90.2-90.5 us (profiles/r06/k12/kab_noslp.log)
     __device__ __forceinline__ CamPair load_pair() const {
         CamPair c;
-        c.load(reinterpret_cast<cf2*>(reinterpret_cast<uint64_t>(campair)), H, W);
+        uint64_t rp = reinterpret_cast<uint64_t>(campair);
+        asm volatile("" : "+s"(rp));
+        c.load(reinterpret_cast<cf2*>(rp), H, W);
         return c;
     }
 

@@ -12,7 +12,7 @@ enum Knob {
     KNOB_P3D_DX,        // 0 policy, 1 matrix cores, 2 VALU (3 = grouped staging, A/B builds only)
     KNOB_P3D_DW,        // 0 policy, 1 VALU
     KNOB_GN_PATH,       // 0 resident where it fits, 1 two-pass
-    KNOB_BN_PATH,       // 0 resident up to BN_RES_MAXM rows (+ A/B builds: ticket above; 1 ticket, 2 three-pass)
+    KNOB_BN_PATH,       // 0 resident up to BN_RES_MAXM rows (the only form left; 1 / 2 removed in round 6)
     KNOB_BN_RES_MAXM,   // largest M = N*H*W the resident BatchNorm takes (<= 8192)
     KNOB_GN_RES_RPT,    // most row vectors per thread of the resident GroupNorm (1, 2, 4, 8)
     KNOB_COUNT

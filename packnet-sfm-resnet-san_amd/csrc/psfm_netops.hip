@@ -369,273 +369,6 @@ inline hipError_t launch_finish(const ColJob* jobs, int njobs, hipStream_t st) {
 // BatchNorm (training) + residual + ReLU
 // ------------------------------------------------------------------------------------------
 __host__ __device__ inline size_t bn_coef_off(int nblk, int C) { return align4((size_t)nblk * 2 * C); }
-#ifdef PSFM_AB_VARIANTS
-// The three-pass fused BatchNorm (statistics rows -> per-channel finish -> apply, each way) lost to
-// MIOpen's BatchNorm + ATen in every A/B on these nets (profiles/r02/netops_ab, r03): it is built
-// into A/B variant libraries only (tools/build_variants.sh "-DPSFM_AB_VARIANTS"); the product runs
-// the resident one-launch kernels below where they hold the layer and MIOpen elsewhere.
-struct BNArgs {
-    const uint16_t* x;
-    const uint16_t* res;
-    const uint16_t* dy;
-    const uint16_t* y;
-    const float* gamma;
-    const float* beta;
-    float* run_mean;
-    float* run_var;
-    float* save_mean;
-    float* save_invstd;
-    uint16_t* out;   // y (fwd) / dx (bwd)
-    uint16_t* dres;  // bwd
-    float* dgamma;
-    float* dbeta;
-    float* ws;       // partial rows [nblk][2C], then [3][C] coefficients
-    float momentum, eps;
-    int M, C, relu, G, TR, rpb, nblk;
-};
-
-__device__ __forceinline__ float* bn_coef(const BNArgs& a) { return a.ws + bn_coef_off(a.nblk, a.C); }
-
-// Column totals for the finish kernels: thread = (column c = 4 * blockIdx.x + t % 4, lane t / 4 of
-// 64); tot[k] = sum over rows of rows[r * stride + off[k] + c] (fp64: each lane its rows in order,
-// then a fixed tree over the lanes), valid in every thread of the column on return.
-template <int K>
-__device__ __forceinline__ void cols4_totals(const float* rows, int nrows, int stride, const int (&off)[K], int c,
-                                             bool valid, double (&tot)[K]) {
-    __shared__ double part[K][256];
-    const int t = threadIdx.x, cl = t & 3, lane = t >> 2;
-    double s[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) s[k] = 0.0;
-    if (valid) {
-        for (int r0 = lane; r0 < nrows; r0 += 4 * 64) {
-            float v[4][K];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int rr = r0 + u * 64;
-                    v[u][k] = rr < nrows ? rows[(size_t)rr * stride + off[k] + c] : 0.0f;
-                }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int k = 0; k < K; ++k) s[k] += (double)v[u][k];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) part[k][t] = s[k];
-    __syncthreads();
-    for (int h = 32; h >= 1; h >>= 1) {
-        if (lane < h)
-#pragma unroll
-            for (int k = 0; k < K; ++k) part[k][t] += part[k][t + 4 * h];
-        __syncthreads();
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) tot[k] = part[k][cl];
-}
-
-// pass 1: per-channel sum / sum of squares of this workgroup's rows -> its partial row
-template <int VEC>
-__global__ __launch_bounds__(NT) void k_bn_fwd_stats(BNArgs a) {
-    __shared__ float red[2 * NT * VEC];
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    const int c0 = cg * VEC;
-    float acc[2][VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
-    if (r < a.TR) {
-        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<VEC> v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int row = base_ + u * a.TR;
-            v[u] = row < row1 ? ld_bf<VEC>(a.x + (size_t)row * a.C + c0) : zero<VEC>();
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) {
-                acc[0][i] += v[u].v[i];
-                acc[1][i] += v[u].v[i] * v[u].v[i];
-            }
-        ROW_LOOP_END
-    }
-    block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {   // this workgroup's partial row; k_bn_fwd_finish reduces the rows (next launch)
-        float* row = a.ws + (size_t)blockIdx.x * 2 * a.C;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            row[c0 + i] = acc[0][i];
-            row[a.C + c0 + i] = acc[1][i];
-        }
-    }
-}
-
-// pass 1b: per channel (4 channels x 64 lanes per workgroup) the column totals of the partial rows
-// -> mean, invstd, running stats and the affine coefficients scale = gamma*invstd,
-// shift = beta - mean*scale
-__global__ __launch_bounds__(256) void k_bn_fwd_finish(BNArgs a) {
-    const int c = blockIdx.x * 4 + (threadIdx.x & 3);
-    const int off[2] = {0, a.C};
-    double fin[2];
-    cols4_totals<2>(a.ws, a.nblk, 2 * a.C, off, c, c < a.C, fin);
-    if (threadIdx.x >= 4 || c >= a.C) return;
-    float* coef = bn_coef(a);  // [2][C]: scale, shift
-    const double inv_m = 1.0 / (double)a.M;
-    const double mean = fin[0] * inv_m;
-    const double var = fmax(fin[1] * inv_m - mean * mean, 0.0);
-    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-    a.save_mean[c] = (float)mean;
-    a.save_invstd[c] = invstd;
-    if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
-        const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-        a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
-        a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-    }
-    const float scale = a.gamma[c] * invstd;
-    coef[c] = scale;
-    coef[a.C + c] = a.beta[c] - (float)mean * scale;
-}
-
-// pass 2: y = act(x*scale + shift [+ res])
-template <int VEC>
-__global__ __launch_bounds__(NT) void k_bn_fwd_apply(BNArgs a) {
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * VEC;
-    const float* coef = bn_coef(a);
-    const Vec<VEC> sc = ld_f<VEC>(coef + c0), sh = ld_f<VEC>(coef + a.C + c0);
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    Vec<VEC> v[U], rv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        const size_t o = (size_t)row * a.C + c0;
-        v[u] = row < row1 ? ld_bf<VEC>(a.x + o) : zero<VEC>();
-        if (a.res) rv[u] = row < row1 ? ld_bf<VEC>(a.res + o) : zero<VEC>();
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            float w = v[u].v[i] * sc.v[i] + sh.v[i];
-            // the reference rounds bn(x) to bf16 before the residual add (both operands bf16)
-            if (a.res) w = bfround(w) + rv[u].v[i];
-            if (a.relu) w = fmaxf(w, 0.0f);
-            v[u].v[i] = w;
-        }
-        st_bf<VEC>(a.out + (size_t)row * a.C + c0, v[u]);
-    }
-    ROW_LOOP_END
-}
-
-// backward pass 1: per channel sum(dyr), sum(dyr * (x - mean)) of this workgroup's rows
-template <int VEC>
-__global__ __launch_bounds__(NT) void k_bn_bwd_stats(BNArgs a) {
-    __shared__ float red[2 * NT * VEC];
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    const int c0 = cg * VEC;
-    float acc[2][VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[0][i] = acc[1][i] = 0.0f;
-    if (r < a.TR) {
-        const Vec<VEC> mu = ld_f<VEC>(a.save_mean + c0);
-        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<VEC> g[U], y[U], x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int row = base_ + u * a.TR;
-            const size_t o = (size_t)row * a.C + c0;
-            const bool in = row < row1;
-            g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-            if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
-            x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) {
-                const float gg = (a.relu && !(y[u].v[i] > 0.0f)) ? 0.0f : g[u].v[i];
-                acc[0][i] += gg;
-                acc[1][i] += gg * (x[u].v[i] - mu.v[i]);
-            }
-        ROW_LOOP_END
-    }
-    block_colsum<VEC, 2>(acc, red, a.G, a.TR);
-    if (r == 0) {
-        float* row = a.ws + (size_t)blockIdx.x * 2 * a.C;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            row[c0 + i] = acc[0][i];
-            row[a.C + c0 + i] = acc[1][i];
-        }
-    }
-}
-
-// backward pass 1b: column totals -> dgamma, dbeta and the dx coefficients k1 = gamma*invstd,
-// k2 = sum(dyr)/M, k3 = sum(dyr*xc)*invstd^2/M
-__global__ __launch_bounds__(256) void k_bn_bwd_finish(BNArgs a) {
-    const int c = blockIdx.x * 4 + (threadIdx.x & 3);
-    const int off[2] = {0, a.C};
-    double fin[2];
-    cols4_totals<2>(a.ws, a.nblk, 2 * a.C, off, c, c < a.C, fin);
-    if (threadIdx.x >= 4 || c >= a.C) return;
-    float* coef = bn_coef(a);  // [3][C]
-    const double inv_m = 1.0 / (double)a.M;
-    const double is = a.save_invstd[c];
-    a.dbeta[c] = (float)fin[0];
-    a.dgamma[c] = (float)(fin[1] * is);
-    coef[c] = a.gamma[c] * (float)is;
-    coef[a.C + c] = (float)(fin[0] * inv_m);
-    coef[2 * a.C + c] = (float)(fin[1] * is * is * inv_m);
-}
-
-// backward pass 2: dx = k1 * (dyr - k2 - (x - mean) * k3); dres = dyr
-template <int VEC>
-__global__ __launch_bounds__(NT) void k_bn_bwd_apply(BNArgs a) {
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * VEC;
-    const float* coef = bn_coef(a);
-    const Vec<VEC> k1 = ld_f<VEC>(coef + c0), k2 = ld_f<VEC>(coef + a.C + c0), k3 = ld_f<VEC>(coef + 2 * a.C + c0);
-    const Vec<VEC> mu = ld_f<VEC>(a.save_mean + c0);
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    Vec<VEC> g[U], y[U], x[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        const size_t o = (size_t)row * a.C + c0;
-        const bool in = row < row1;
-        g[u] = in ? ld_bf<VEC>(a.dy + o) : zero<VEC>();
-        if (a.relu) y[u] = in ? ld_bf<VEC>(a.y + o) : zero<VEC>();
-        x[u] = in ? ld_bf<VEC>(a.x + o) : zero<VEC>();
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-        const size_t o = (size_t)row * a.C + c0;
-        Vec<VEC> d;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            if (a.relu && !(y[u].v[i] > 0.0f)) g[u].v[i] = 0.0f;
-            d.v[i] = k1.v[i] * ((g[u].v[i] - k2.v[i]) - (x[u].v[i] - mu.v[i]) * k3.v[i]);
-        }
-        if (a.dres) st_bf<VEC>(a.dres + o, g[u]);
-        st_bf<VEC>(a.out + o, d);
-    }
-    ROW_LOOP_END
-}
-
-#endif  // PSFM_AB_VARIANTS
 
 // ------------------------------------------------------------------------------------------
 // Resident BatchNorm: ONE launch each way for the small encoder layers (M = N*H*W rows up to the
@@ -915,8 +648,10 @@ __global__ __launch_bounds__(bnr_bwd_maxt(RPT)) void k_bnr_bwd(BNRArgs a) {
 struct BNRGeo {
     int rpt, nth;
 };
+// The forward applies the BN_RES_MAXM policy; the backward takes whatever the kernels hold (up to
+// BNR_MAXM rows), so it follows the forward's decision even if the knob changed in between.
 inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
-    if (C % 8 || C > 512 || M < 1 || M > std::min(BNR_MAXM, knob(KNOB_BN_RES_MAXM))) return false;
+    if (C % 8 || C > 512 || M < 1 || M > (bwd ? BNR_MAXM : std::min(BNR_MAXM, knob(KNOB_BN_RES_MAXM)))) return false;
     for (int r = 1; r <= (bwd ? 16 : 8); r *= 2) {
         const int maxt = bwd ? bnr_bwd_maxt(r) : BNR_MAXT;
         if ((long long)r * maxt >= M) {
@@ -936,318 +671,6 @@ inline bool bnr_geometry(int M, int C, BNRGeo& g, bool bwd = false) {
 #define BNR_BWD_CASE(R)                                                                                  \
     case R: hipLaunchKernelGGL((k_bnr_bwd<R>), dim3(a.nb), dim3(g.nth), 0, st, a); break
 
-#ifdef PSFM_AB_VARIANTS
-// ------------------------------------------------------------------------------------------
-// Two-launch BatchNorm for the layers too large to be resident (the ResNet stem, layer1, layer2):
-// coalesced over all CUs, the cross-workgroup reduction finished inside the statistics launch.
-// A/B builds only (-DPSFM_AB_VARIANTS): the statistics launch costs 18-19 us whatever the layer size
-// (the hand-off's drains, ticket and acquire round trips), against 12 us for MIOpen's two statistics
-// kernels, and the step lost 1094-1097 vs 1140-1145 img/s to resident + MIOpen (profiles/r05/bn).
-//   pass 1 (statistics): workgroups take row slices of all C channels (16-byte vectors, a wave
-//     covers whole 128-byte row lines) and publish a partial row of per-channel sums — sc1
-//     (write-through) stores, drained by every storing wave — then one lane takes a ticket (relaxed
-//     agent-scope atomic).  The workgroup holding the LAST ticket acquires (agent scope) and sums
-//     every partial row in a fixed order (fp64): batch statistics, running stats, and the apply
-//     coefficients, then re-arms its ticket word.  (MI355X_MICROARCH.md / cdna_hip_programming.md
-//     §6 Guideline 16: the fan-in form — payload sc1 + drained, counter by atomic, one acquire.)
-//   pass 2 (apply): y = act(x*scale + shift [+ res]) / dx = kg*g + kx*x + k0 over all rows.
-// Forward statistics are shifted sums (x - K, K = the channel's first value) as in the resident
-// kernels; the backward statistics are sum g and sum g (x - mean) of the ReLU-masked gradient (the
-// forked gradients summed in the load).  Deterministic: partial rows summed in workgroup order
-// whichever workgroup finishes last.  Ticket words: a zero-initialised device array, one word per
-// launch site taken round-robin on the host (a graph replays its launches' words; every launch
-// leaves its word at 0).
-// ------------------------------------------------------------------------------------------
-constexpr int BNT_SLOTS = 1024;
-__device__ unsigned int g_bnt_ticket[BNT_SLOTS];
-
-struct BNTArgs {
-    const uint16_t* x;
-    const uint16_t* res;
-    const uint16_t* dy;
-    const uint16_t* dy1;
-    const uint16_t* dy2;
-    const uint16_t* y;
-    const float* gamma;
-    const float* beta;
-    float* run_mean;
-    float* run_var;
-    float* save_mean;
-    float* save_invstd;
-    uint16_t* out;
-    uint16_t* dres;
-    float* dgamma;
-    float* dbeta;
-    float* part;      // [nblk][2C] partial rows
-    float* coef;      // [3][C]: apply coefficients
-    unsigned* ticket;
-    float momentum, eps;
-    int M, C, relu, G, TR, rpb, nblk;
-};
-
-__device__ __forceinline__ void st_sc1(float* p, float v) {   // write-through (sc1) 4-byte store
-    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// publish this workgroup's partial row (lanes of row lane 0 hold the block sums) and take the ticket;
-// true in every thread of the workgroup that took the last one, after its acquire
-__device__ __forceinline__ bool bnt_publish(const BNTArgs& a, const float (&acc)[2][8], int c0, int r) {
-    __shared__ unsigned s_last;
-    if (r == 0 && c0 < a.C) {
-        float* row = a.part + (size_t)blockIdx.x * 2 * a.C;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            st_sc1(row + c0 + i, acc[0][i]);
-            st_sc1(row + a.C + c0 + i, acc[1][i]);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == (unsigned)(a.nblk - 1);
-        if (s_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    return s_last;
-}
-
-// the last workgroup: per-channel totals of the nblk partial rows (fixed order, fp64) -> tot[2][C]
-// in LDS.  A partial row is F = 2C / 4 float4 columns; thread (column f, row lane q < R = NT / F) sums
-// rows q, q + R, ... with every load of a chunk of 16 rows issued before the first add (the rows sit
-// in the memory-side cache after the sc1 stores: one round trip per chunk, not per row), then the R
-// row lanes are added in order.
-__device__ __forceinline__ void bnt_totals(const BNTArgs& a, double* tot, double* scratch) {
-    const int t = threadIdx.x, F = a.C / 2, R = NT / F, f = t % F, q = t / F;
-    double s[4] = {0.0, 0.0, 0.0, 0.0};
-    if (q < R) {
-        const float4* part = reinterpret_cast<const float4*>(a.part);
-        for (int b0 = q; b0 < a.nblk; b0 += 16 * R) {
-            float4 v[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int b = b0 + u * R;
-                v[u] = b < a.nblk ? part[(size_t)b * F + f] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                s[0] += (double)v[u].x;
-                s[1] += (double)v[u].y;
-                s[2] += (double)v[u].z;
-                s[3] += (double)v[u].w;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) scratch[(size_t)q * 2 * a.C + 4 * f + k] = s[k];
-    }
-    __syncthreads();
-    for (int c = t; c < 2 * a.C; c += NT) {   // c < C: sums, C <= c < 2C: second sums (the row layout)
-        double v = 0.0;
-        for (int k = 0; k < R; ++k) v += scratch[(size_t)k * 2 * a.C + c];
-        tot[c] = v;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(NT) void k_bnt_fwd_stats(BNTArgs a) {
-    __shared__ float red[2 * NT * 8];
-    __shared__ double tot[2 * 512];
-    __shared__ double scratch[4 * NT];
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    const int c0 = cg * 8;
-    float kk[8];
-    {
-        const Vec<8> k8 = ld_bf<8>(a.x + (r < a.TR ? c0 : 0));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) kk[i] = k8.v[i];
-    }
-    float acc[2][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
-    if (r < a.TR) {
-        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        Vec<8> v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int row = base_ + u * a.TR;
-            v[u] = ld_bf<8>(a.x + (size_t)min(row, row1 - 1) * a.C + c0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (base_ + u * a.TR >= row1) break;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float d = v[u].v[i] - kk[i];
-                acc[0][i] += d;
-                acc[1][i] += d * d;
-            }
-        }
-        ROW_LOOP_END
-    }
-    block_colsum<8, 2>(acc, red, a.G, a.TR);
-    if (!bnt_publish(a, acc, r < a.TR ? c0 : a.C, r)) return;
-    bnt_totals(a, tot, scratch);
-    const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += blockDim.x) {
-        const double m1 = tot[c] * inv_m;
-        const double mean = (double)bf2f(a.x[c]) + m1;
-        const double var = fmax(tot[a.C + c] * inv_m - m1 * m1, 0.0);
-        const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-        a.save_mean[c] = (float)mean;
-        a.save_invstd[c] = invstd;
-        if (a.run_mean) {  // torch: running = (1-m) running + m batch (unbiased var)
-            const double unb = a.M > 1 ? var * (double)a.M / (double)(a.M - 1) : var;
-            a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mean);
-            a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-        }
-        const float scale = a.gamma[c] * invstd;
-        a.coef[c] = scale;
-        a.coef[a.C + c] = a.beta[c] - (float)mean * scale;
-    }
-    if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
-}
-
-__global__ __launch_bounds__(NT) void k_bnt_fwd_apply(BNTArgs a) {
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * 8;
-    const Vec<8> sc = ld_f<8>(a.coef + c0), sh = ld_f<8>(a.coef + a.C + c0);
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    Vec<8> v[U], rv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
-        v[u] = ld_bf<8>(a.x + o);
-        if (a.res) rv[u] = ld_bf<8>(a.res + o);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float w = v[u].v[i] * sc.v[i] + sh.v[i];
-            if (a.res) w = bfround(w) + rv[u].v[i];   // autocast: bn(x) is a bf16 tensor before the add
-            if (a.relu) w = w <= 0.0f ? 0.0f : w;     // ATen relu (NaN propagates)
-            v[u].v[i] = w;
-        }
-        st_bf<8>(a.out + (size_t)row * a.C + c0, v[u]);
-    }
-    ROW_LOOP_END
-}
-
-// the ReLU-masked gradient of one row vector (forked gradients summed first, bf16 rounding each)
-__device__ __forceinline__ uint4 bnt_grad(const BNTArgs& a, size_t o) {
-    uint4 g = *reinterpret_cast<const uint4*>(a.dy + o);
-    if (a.dy1) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy1 + o));
-    if (a.dy2) g = add_bf16x8(g, *reinterpret_cast<const uint4*>(a.dy2 + o));
-    if (a.relu) g = relu_mask4(g, *reinterpret_cast<const uint4*>(a.y + o));
-    return g;
-}
-
-__global__ __launch_bounds__(NT) void k_bnt_bwd_stats(BNTArgs a) {
-    __shared__ float red[2 * NT * 8];
-    __shared__ double tot[2 * 512];
-    __shared__ double scratch[4 * NT];
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    const int c0 = cg * 8;
-    float acc[2][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[0][i] = acc[1][i] = 0.0f;
-    if (r < a.TR) {
-        float mu[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) mu[i] = a.save_mean[c0 + i];
-        const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-        ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-        uint4 gq[U], xq[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
-            gq[u] = bnt_grad(a, o);
-            xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (base_ + u * a.TR >= row1) break;
-            float g[8], v[8];
-            unpack8f(gq[u], g);
-            unpack8f(xq[u], v);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                acc[0][i] += g[i];
-                acc[1][i] += g[i] * (v[i] - mu[i]);
-            }
-        }
-        ROW_LOOP_END
-    }
-    block_colsum<8, 2>(acc, red, a.G, a.TR);
-    if (!bnt_publish(a, acc, r < a.TR ? c0 : a.C, r)) return;
-    bnt_totals(a, tot, scratch);
-    const double inv_m = 1.0 / (double)a.M;
-    for (int c = t; c < a.C; c += blockDim.x) {
-        const double isd = a.save_invstd[c], k1 = (double)(a.gamma[c] * a.save_invstd[c]);
-        const double k2 = tot[c] * inv_m, k3 = tot[a.C + c] * isd * isd * inv_m;
-        a.dbeta[c] = (float)tot[c];
-        a.dgamma[c] = (float)(tot[a.C + c] * isd);
-        a.coef[c] = (float)k1;                                            // kg
-        a.coef[a.C + c] = (float)(-k1 * k3);                              // kx
-        a.coef[2 * a.C + c] = (float)(k1 * (k3 * (double)a.save_mean[c] - k2));   // k0
-    }
-    if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
-}
-
-__global__ __launch_bounds__(NT) void k_bnt_bwd_apply(BNTArgs a) {
-    const int t = threadIdx.x, cg = t % a.G, r = t / a.G;
-    if (r >= a.TR) return;
-    const int c0 = cg * 8;
-    const Vec<8> kg = ld_f<8>(a.coef + c0), kx = ld_f<8>(a.coef + a.C + c0), k0 = ld_f<8>(a.coef + 2 * a.C + c0);
-    const int row0 = blockIdx.x * a.rpb, row1 = min(a.M, row0 + a.rpb);
-    ROW_LOOP_BEGIN(row0, row1, r, a.TR)
-    uint4 gq[U], xq[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const size_t o = (size_t)min(base_ + u * a.TR, row1 - 1) * a.C + c0;
-        gq[u] = bnt_grad(a, o);
-        xq[u] = *reinterpret_cast<const uint4*>(a.x + o);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int row = base_ + u * a.TR;
-        if (row >= row1) break;
-        const size_t o = (size_t)row * a.C + c0;
-        float g[8], v[8];
-        unpack8f(gq[u], g);
-        unpack8f(xq[u], v);
-        Vec<8> d;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d.v[i] = fmaf(kg.v[i], g[i], fmaf(kx.v[i], v[i], k0.v[i]));
-        st_bf<8>(a.out + o, d);
-        if (a.dres) *reinterpret_cast<uint4*>(a.dres + o) = gq[u];
-    }
-    ROW_LOOP_END
-}
-
-// ticket-form geometry: rows per workgroup >= 2 row steps (the last workgroup's fixed-order sum
-// reads nblk partial rows), <= 256 workgroups
-inline Geo bnt_geometry(int M, int C) { return geometry(M, C, 8, 256); }
-
-unsigned* bnt_ticket_slot() {
-    static unsigned* base = nullptr;
-    static unsigned next = 0;
-    if (!base) {
-        void* p = nullptr;
-        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bnt_ticket)) != hipSuccess) return nullptr;
-        base = static_cast<unsigned*>(p);
-    }
-    return base + (next++ % BNT_SLOTS);
-}
-#endif  // PSFM_AB_VARIANTS
 
 // ------------------------------------------------------------------------------------------
 // GroupNorm(NG) of (x [+ res] + bias) + ReLU / ELU, per sample n over rows [n*HW, (n+1)*HW),
@@ -2357,16 +1780,8 @@ __global__ __launch_bounds__(NT) void k_gnp_bwd_apply(GNArgs a) {
 }
 
 // the software-pipelined two-pass GroupNorm (k_gnp_*) is the product's form for VEC = 8; the
-// unpipelined k_gn_*<8> (bitwise the same results, 208 vs 211 img/s on PackNet01,
-// profiles/r04/gn) is built into A/B variant libraries only (tools/build_variants.sh)
-static bool gnp_enabled() {
-#ifdef PSFM_AB_VARIANTS
-    const char* e = getenv("PSFM_GN_PIPE");
-    return !(e && e[0] == '0');
-#else
-    return true;
-#endif
-}
+// unpipelined k_gn_*<VEC> kernels run only VEC = 1 (the unpipelined VEC = 8 form, bitwise the same
+// results, lost 208 vs 211 img/s on PackNet01, profiles/r04/gn, and was removed in round 6)
 
 template <typename A>
 void set_geo(A& a, const Geo& g) {
@@ -2955,23 +2370,15 @@ int psfm_bias_act_bwd_sum(const void* dy, const void* dy1, const void* y, int M,
     return 0;
 }
 
-// BatchNorm forms by the BN_PATH knob: 0 (default) the resident kernels up to BN_RES_MAXM rows and the
-// two-launch ticket kernels above; 1 the ticket kernels everywhere; 2 the three-pass kernels (A/B
-// builds only).  Returns 0 resident, 1 ticket, 2 three-pass, -1 none.
+// BatchNorm form: 0 the resident kernels (forward: up to BN_RES_MAXM rows; backward: any shape they
+// hold), -1 none (MIOpen's BatchNorm runs there).  The ticket / three-pass forms were removed in round 6.
 static int bn_form(int M, int C, BNRGeo& rg, bool bwd) {
-    const int path = knob(KNOB_BN_PATH);
-    if (path == 0 && bnr_geometry(M, C, rg, bwd)) return 0;
-#ifdef PSFM_AB_VARIANTS
-    if (path == 2) return 2;
-    if (C % 8 == 0 && C <= 512 && M >= 1) return 1;
-#endif
+    if (bnr_geometry(M, C, rg, bwd)) return 0;
     return -1;
 }
-static bool bnr_path() { return knob(KNOB_BN_PATH) == 0; }
-
 int psfm_bn_act_resident(int M, int C) {
     BNRGeo g;
-    return bnr_path() && bnr_geometry(M, C, g) ? 1 : 0;
+    return bnr_geometry(M, C, g) ? 1 : 0;
 }
 
 int psfm_bn_act_fused(int M, int C) {
@@ -2980,13 +2387,6 @@ int psfm_bn_act_fused(int M, int C) {
     return f == 0 || f == 1 ? 1 : 0;
 }
 
-#ifdef PSFM_AB_VARIANTS
-static void bnt_common(BNTArgs& a, const Geo& g, int M, int C, float* ws) {
-    a.M = M, a.C = C, a.G = g.G, a.TR = g.TR, a.rpb = g.rpb, a.nblk = g.nblk;
-    a.part = ws;
-    a.coef = ws + align4((size_t)g.nblk * 2 * C);
-}
-#endif
 
 int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const float* beta, float* run_mean,
                     float* run_var, float momentum, float eps, int M, int C, int relu, void* y, float* save_mean,
@@ -2997,27 +2397,6 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
     if (int e = check_vec(C, "bn_act_fwd")) return e;
     BNRGeo rgeo;
     const int form = bn_form(M, C, rgeo, false);
-#ifdef PSFM_AB_VARIANTS
-    if (form == 1) {  // two launches (ticket)
-        if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
-        unsigned* tk = bnt_ticket_slot();
-        if (!tk) return fail(-4, "bn_act_fwd: ticket words unavailable");
-        const Geo g = bnt_geometry(M, C);
-        BNTArgs a{};
-        bnt_common(a, g, M, C, ws);
-        a.x = static_cast<const uint16_t*>(x);
-        a.res = static_cast<const uint16_t*>(res);
-        a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
-        a.save_mean = save_mean, a.save_invstd = save_invstd;
-        a.out = static_cast<uint16_t*>(y);
-        a.ticket = tk, a.momentum = momentum, a.eps = eps, a.relu = relu;
-        hipStream_t st = (hipStream_t)stream;
-        hipLaunchKernelGGL(k_bnt_fwd_stats, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bnt_fwd_apply, dim3(g.nblk), dim3(NT), 0, st, a);
-        NETOPS_LAUNCH_CHECK();
-        return 0;
-    }
-#endif
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.x = static_cast<const uint16_t*>(x);
@@ -3032,37 +2411,9 @@ int psfm_bn_act_fwd(const void* x, const void* res, const float* gamma, const fl
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
-#ifndef PSFM_AB_VARIANTS
     (void)ws;
-    return fail(-3, "bn_act_fwd: no fused BatchNorm for this shape (psfm_bn_act_fused: C % 8 == 0, C <= 512; the "
-                    "three-pass kernels are built into A/B variant libraries only)");
-#else
-    if (!ws) return fail(-1, "bn_act_fwd: ws required outside the resident shapes");
-    const int vec = pick_vec(C);
-    const Geo g = geometry(M, C, vec);
-    BNArgs a{};
-    a.x = static_cast<const uint16_t*>(x);
-    a.res = static_cast<const uint16_t*>(res);
-    a.gamma = gamma, a.beta = beta, a.run_mean = run_mean, a.run_var = run_var;
-    a.save_mean = save_mean, a.save_invstd = save_invstd;
-    a.out = static_cast<uint16_t*>(y);
-    a.ws = ws, a.momentum = momentum, a.eps = eps;
-    a.M = M, a.C = C, a.relu = relu, a.nblk = g.nblk;
-    set_geo(a, g);
-    hipStream_t st = (hipStream_t)stream;
-    const dim3 fin((C + 3) / 4);
-    if (vec == 8) {
-        hipLaunchKernelGGL(k_bn_fwd_stats<8>, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_finish, fin, dim3(256), 0, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_apply<8>, dim3(g.nblk), dim3(NT), 0, st, a);
-    } else {
-        hipLaunchKernelGGL(k_bn_fwd_stats<1>, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_finish, fin, dim3(256), 0, st, a);
-        hipLaunchKernelGGL(k_bn_fwd_apply<1>, dim3(g.nblk), dim3(NT), 0, st, a);
-    }
-    NETOPS_LAUNCH_CHECK();
-    return 0;
-#endif
+    return fail(-3, "bn_act_fwd: no fused BatchNorm for this shape (psfm_bn_act_fused: C % 8 == 0, C <= 512, M <= "
+                    "BN_RES_MAXM)");
 }
 
 int psfm_bn_act_bwd(const void* dy, const void* y, const void* x, const float* gamma, const float* save_mean,
@@ -3081,29 +2432,6 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
     if (int e = check_vec(C, "bn_act_bwd")) return e;
     BNRGeo rgeo;
     const int form = bn_form(M, C, rgeo, true);
-#ifdef PSFM_AB_VARIANTS
-    if (form == 1) {  // two launches (ticket)
-        if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
-        unsigned* tk = bnt_ticket_slot();
-        if (!tk) return fail(-4, "bn_act_bwd: ticket words unavailable");
-        const Geo g = bnt_geometry(M, C);
-        BNTArgs a{};
-        bnt_common(a, g, M, C, ws);
-        a.dy = static_cast<const uint16_t*>(dy);
-        a.dy1 = static_cast<const uint16_t*>(dy1), a.dy2 = static_cast<const uint16_t*>(dy2);
-        a.y = static_cast<const uint16_t*>(y);
-        a.x = static_cast<const uint16_t*>(x);
-        a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
-        a.out = static_cast<uint16_t*>(dx);
-        a.dres = static_cast<uint16_t*>(dres);
-        a.dgamma = dgamma, a.dbeta = dbeta, a.ticket = tk, a.relu = relu;
-        hipStream_t st = (hipStream_t)stream;
-        hipLaunchKernelGGL(k_bnt_bwd_stats, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bnt_bwd_apply, dim3(g.nblk), dim3(NT), 0, st, a);
-        NETOPS_LAUNCH_CHECK();
-        return 0;
-    }
-#endif
     if (form == 0) {  // one launch (resident)
         BNRArgs a{};
         a.dy = static_cast<const uint16_t*>(dy);
@@ -3120,39 +2448,8 @@ int psfm_bn_act_bwd_sum(const void* dy, const void* dy1, const void* dy2, const 
         NETOPS_LAUNCH_CHECK();
         return 0;
     }
-#ifndef PSFM_AB_VARIANTS
     (void)ws;
-    return fail(-3, "bn_act_bwd: no fused BatchNorm for this shape (psfm_bn_act_fused: C % 8 == 0, C <= 512; the "
-                    "three-pass kernels are built into A/B variant libraries only)");
-#else
-    if (!ws) return fail(-1, "bn_act_bwd: ws required outside the resident shapes");
-    if (dy1 || dy2) return fail(-1, "bn_act_bwd: extra gradients (dy1 / dy2) need the resident shapes");
-    const int vec = pick_vec(C);
-    const Geo g = geometry(M, C, vec);
-    BNArgs a{};
-    a.dy = static_cast<const uint16_t*>(dy);
-    a.y = static_cast<const uint16_t*>(y);
-    a.x = static_cast<const uint16_t*>(x);
-    a.gamma = gamma, a.save_mean = const_cast<float*>(save_mean), a.save_invstd = const_cast<float*>(save_invstd);
-    a.out = static_cast<uint16_t*>(dx);
-    a.dres = static_cast<uint16_t*>(dres);
-    a.dgamma = dgamma, a.dbeta = dbeta, a.ws = ws;
-    a.M = M, a.C = C, a.relu = relu, a.nblk = g.nblk;
-    set_geo(a, g);
-    hipStream_t st = (hipStream_t)stream;
-    const dim3 fin((C + 3) / 4);
-    if (vec == 8) {
-        hipLaunchKernelGGL(k_bn_bwd_stats<8>, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bn_bwd_finish, fin, dim3(256), 0, st, a);
-        hipLaunchKernelGGL(k_bn_bwd_apply<8>, dim3(g.nblk), dim3(NT), 0, st, a);
-    } else {
-        hipLaunchKernelGGL(k_bn_bwd_stats<1>, dim3(g.nblk), dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_bn_bwd_finish, fin, dim3(256), 0, st, a);
-        hipLaunchKernelGGL(k_bn_bwd_apply<1>, dim3(g.nblk), dim3(NT), 0, st, a);
-    }
-    NETOPS_LAUNCH_CHECK();
-    return 0;
-#endif
+    return fail(-3, "bn_act_bwd: no fused BatchNorm for this shape (C % 8 == 0, C <= 512, M <= 8192)");
 }
 
 // the resident path is the default; the GN_PATH knob = 1 forces the two-pass kernels (A/B, tests)
@@ -3202,7 +2499,7 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
         return 0;
     }
     const dim3 grid(N * g.nblk);
-    if (vec == 8 && gnp_enabled()) {
+    if (vec == 8) {
         if (res) {
             hipLaunchKernelGGL(k_gnp_fwd_stats<true>, grid, dim3(NT), 0, st, a);
             hipLaunchKernelGGL(k_gnp_fwd_apply<true>, grid, dim3(NT), 0, st, a);
@@ -3210,9 +2507,6 @@ int psfm_gn_act_fwd(const void* x, const void* res, const void* bias, int bias_b
             hipLaunchKernelGGL(k_gnp_fwd_stats<false>, grid, dim3(NT), 0, st, a);
             hipLaunchKernelGGL(k_gnp_fwd_apply<false>, grid, dim3(NT), 0, st, a);
         }
-    } else if (vec == 8) {
-        hipLaunchKernelGGL(k_gn_fwd_stats<8>, grid, dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_gn_fwd_apply<8>, grid, dim3(NT), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_gn_fwd_stats<1>, grid, dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_gn_fwd_apply<1>, grid, dim3(NT), 0, st, a);
@@ -3254,7 +2548,7 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
         return 0;
     }
     const dim3 grid(N * g.nblk), grid_apply(N * g.nblk + (C + 3) / 4);
-    if (vec == 8 && gnp_enabled()) {
+    if (vec == 8) {
         if (res) {
             hipLaunchKernelGGL(k_gnp_bwd_stats<true>, grid, dim3(NT), 0, st, a);
             hipLaunchKernelGGL(k_gnp_bwd_apply<true>, grid_apply, dim3(NT), 0, st, a);
@@ -3262,9 +2556,6 @@ int psfm_gn_act_bwd(const void* dy, const void* x, const void* res, const void* 
             hipLaunchKernelGGL(k_gnp_bwd_stats<false>, grid, dim3(NT), 0, st, a);
             hipLaunchKernelGGL(k_gnp_bwd_apply<false>, grid_apply, dim3(NT), 0, st, a);
         }
-    } else if (vec == 8) {
-        hipLaunchKernelGGL(k_gn_bwd_stats<8>, grid, dim3(NT), 0, st, a);
-        hipLaunchKernelGGL(k_gn_bwd_apply<8>, grid_apply, dim3(NT), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_gn_bwd_stats<1>, grid, dim3(NT), 0, st, a);
         hipLaunchKernelGGL(k_gn_bwd_apply<1>, grid_apply, dim3(NT), 0, st, a);

@@ -1612,12 +1612,6 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
             // 8-k chunks per workgroup: 2 when that still leaves >= 1024 workgroups (unpack 96x320 / 48x160
             // layers: 128 vs 138 us), else 1 (the small layers want the workgroups)
             int cpw = a.K % 16 == 0 && (int64_t)gxn * gyn * a.B * (a.K / 16) >= 1024 ? 2 : 1;
-#ifdef PSFM_AB_VARIANTS
-            const bool grp = t->mode == PSFM_P3D_PACK && a.K % 32 == 0 && dknob == 3;
-            if (grp) cpw = 4;
-#else
-            constexpr bool grp = false;
-#endif
             const dim3 g1((unsigned)(gxn * gyn * a.B * (a.K / (8 * cpw))));
 #define P3D_DXM(ND, CPW)                                                                                              \
     do {                                                                                                              \
@@ -1626,12 +1620,7 @@ int psfm_p3d_bwd(const psfm_p3d_desc* t, const void* x, const float* w, const vo
         else                                                                                                          \
             hipLaunchKernelGGL((k_p3d_bwd_x_mfma<ND, CPW, PSFM_P3D_UNPACK>), g1, dim3(256), 0, st, a, gxn, gyn);      \
     } while (0)
-            if (grp) {
-#ifdef PSFM_AB_VARIANTS
-                if (t->d == 4) hipLaunchKernelGGL((k_p3d_bwd_x_mfma<4, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
-                else hipLaunchKernelGGL((k_p3d_bwd_x_mfma<8, 4, PSFM_P3D_PACK, true>), g1, dim3(256), 0, st, a, gxn, gyn);
-#endif
-            } else if (t->d == 4) {
+            if (t->d == 4) {
                 if (cpw == 2) P3D_DXM(4, 2);
                 else P3D_DXM(4, 1);
             } else {

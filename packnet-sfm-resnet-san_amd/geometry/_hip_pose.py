@@ -15,6 +15,7 @@ class PoseFromVecFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, vec):
+        _hip.note_forward(ctx)
         ctx.set_materialize_grads(False)   # an unused context's matrix gets no zero-filled grad
         B, N = vec.shape[0], vec.shape[1]
         mats = [torch.empty(B, 4, 4, device=vec.device, dtype=torch.float32) for _ in range(N)]
@@ -26,7 +27,7 @@ class PoseFromVecFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         vec, = ctx.saved_tensors
         B, N = vec.shape[0], vec.shape[1]
         gs = [None if g is None else g.float().contiguous() for g in grads]

@@ -168,6 +168,7 @@ class PhotometricLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, image, mask, K, ref_K, T, n_ctx, *rest):
+        _hip.note_forward(ctx)
         ctx.set_materialize_grads(False)   # no zero-filled grads for the metric outputs
         # detached: the per-call records (_Call) live on ctx, and an input with a grad_fn stored
         # there would form a ctx -> tensor -> graph -> ctx cycle that keeps every step's autograd
@@ -260,7 +261,7 @@ class PhotometricLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, g_photo, g_smooth):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         calls, cfg = ctx.calls, ctx.cfg
         dev = calls[0].image.device
         gout = (g_loss if g_loss is not None else torch.zeros(1, device=dev)).reshape(1).float().contiguous()
@@ -323,6 +324,7 @@ class ViewSynthesisFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ref_image, depth, rec, T, cam_model):
+        _hip.note_forward(ctx)
         ref_image, depth = ref_image.contiguous(), depth.contiguous()
         _hip.require_device(ref_image, depth)
         B, _, H, W = ref_image.shape
@@ -338,7 +340,7 @@ class ViewSynthesisFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         ref_image, depth, cam = ctx.saved_tensors
         B, _, H, W = ref_image.shape
         g = g.contiguous().float()

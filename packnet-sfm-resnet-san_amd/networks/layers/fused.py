@@ -76,6 +76,7 @@ def fork_plain(y, nout):
 class _BiasAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, act, nout=1):
+        _hip.note_forward(ctx)
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -90,7 +91,7 @@ class _BiasAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *dys):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         (y,) = ctx.saved_tensors
         gs = [_rows(g.to(y.dtype)) for g in _grads(dys, y)]
         while len(gs) > 2:   # (a decoder output has at most two consumers)
@@ -132,6 +133,7 @@ def conv_nobias(conv, x):
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, nout=1):
+        _hip.note_forward(ctx)
         x = _rows(x)
         N, C, H, W = x.shape
         M = N * H * W
@@ -141,26 +143,28 @@ class _BNAct(torch.autograd.Function):
         mean = torch.empty(C, device=dev, dtype=torch.float32)
         invstd = torch.empty(C, device=dev, dtype=torch.float32)
         L = _hip.lib()
-        ws = None if L.psfm_bn_act_resident(M, C) else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev,
-                                                                   dtype=torch.float32)
+        # the form is decided once, here; the backward reuses it (a knob changed in between must not
+        # send the backward down another path, or leave it without the workspace it needs)
+        resident = bool(L.psfm_bn_act_resident(M, C))
+        ws = None if resident else torch.empty(L.psfm_netops_ws_floats(M, C), device=dev, dtype=torch.float32)
         _hip.check(L.psfm_bn_act_fwd(_hip.ptr(x), _hip.ptr(res), _hip.ptr(weight), _hip.ptr(bias),
                                      _hip.ptr(running_mean), _hip.ptr(running_var), ctypes.c_float(momentum),
                                      ctypes.c_float(eps), M, C, int(relu), _hip.ptr(y), _hip.ptr(mean),
                                      _hip.ptr(invstd), _hip.ptr(ws), _hip.stream(dev)), "psfm_bn_act_fwd")
         ctx.save_for_backward(x, y, weight, mean, invstd)
-        ctx.relu, ctx.has_res = relu, residual is not None
+        ctx.relu, ctx.has_res, ctx.resident = relu, residual is not None, resident
         return _fork(y, nout)
 
     @staticmethod
     def backward(ctx, *dys):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         x, y, weight, mean, invstd = ctx.saved_tensors
         gs = [_rows(g.to(x.dtype)) for g in _grads(dys, y)]
         N, C, H, W = x.shape
         M = N * H * W
         dev = x.device
         L = _hip.lib()
-        resident = bool(L.psfm_bn_act_resident(M, C))
+        resident = ctx.resident
         while len(gs) > 3:   # the kernels sum up to three gradients in their loads
             gs = [gs[0] + gs[1]] + gs[2:]
         dy = gs[0]
@@ -185,6 +189,7 @@ class _AddReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, a, b, nout=1):
+        _hip.note_forward(ctx)
         y = torch.empty_like(a)
         _hip.check(_hip.lib().psfm_add_relu_fwd(_hip.ptr(a), _hip.ptr(b), a.numel(), _hip.ptr(y),
                                                 _hip.stream(a.device)), "psfm_add_relu_fwd")
@@ -194,7 +199,7 @@ class _AddReLU(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *dys):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         (y,) = ctx.saved_tensors
         gs = [g.contiguous(memory_format=_fmt(y)) for g in _grads(dys, y)]
         while len(gs) > 3:
@@ -307,6 +312,7 @@ class _ReLUMaxPool(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, nout=2):
+        _hip.note_forward(ctx)
         N, C, H, W = y.shape
         r = torch.empty_like(y, memory_format=torch.channels_last)
         # allocated channels_last (empty(...).contiguous(channels_last) would launch a copy of garbage)
@@ -319,7 +325,7 @@ class _ReLUMaxPool(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dskip, *dps):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         r, am = ctx.saved_tensors
         N, C, H, W = r.shape
         gs = [_rows(g.to(r.dtype)) for g in dps if g is not None]
@@ -371,6 +377,7 @@ def bn_relu_maxpool(x, bn, pool, nout=2):
 class _GNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, bias, weight, beta, G, eps, act):
+        _hip.note_forward(ctx)
         x = _rows(x)
         res = _rows(res.to(x.dtype)) if res is not None else None
         N, C, H, W = x.shape
@@ -391,7 +398,7 @@ class _GNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         x, res, bias, weight, beta, mean, invstd = ctx.saved_tensors
         dy = _rows(dy.to(x.dtype))
         N, C, H, W = x.shape
@@ -452,6 +459,7 @@ UPCAT = True  # decoder up-stage input on HIP
 class _UpCat(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, skip):
+        _hip.note_forward(ctx)
         N, C1, h, w = x.shape
         C2 = skip.shape[1] if skip is not None else 0
         out = torch.empty((N, C1 + C2, 2 * h, 2 * w), device=x.device, dtype=x.dtype,
@@ -463,7 +471,7 @@ class _UpCat(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         N, C1, C2, h, w = ctx.dims
         dout = _rows(dout)
         dx = torch.empty((N, C1, h, w), device=dout.device, dtype=dout.dtype, memory_format=torch.channels_last)
@@ -500,6 +508,7 @@ class _UpCatBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, bias, skip):
+        _hip.note_forward(ctx)
         N, C1, h, w = x.shape
         C2 = skip.shape[1] if skip is not None else 0
         out = torch.empty((N, C1 + C2, 2 * h, 2 * w), device=x.device, dtype=x.dtype,
@@ -514,7 +523,7 @@ class _UpCatBiasReLU(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         (out,) = ctx.saved_tensors
         N, C1, C2, h, w = ctx.dims
         dout = _rows(dout)

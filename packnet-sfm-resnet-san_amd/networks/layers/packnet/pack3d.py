@@ -47,6 +47,7 @@ def _out_shape(mode, x, r, d):
 class Pack3dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, mode, r):
+        _hip.note_forward(ctx)
         d = w.shape[0]
         y = torch.empty(_out_shape(mode, x, r, d), device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
         wf = w.detach().float().reshape(d, 27).contiguous()
@@ -60,7 +61,7 @@ class Pack3dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         x, wf = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last).to(x.dtype)
         d = wf.shape[0]

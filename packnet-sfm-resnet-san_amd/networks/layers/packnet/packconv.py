@@ -45,12 +45,29 @@ class PcWeights(ctypes.Structure):
                 ("corner", c_void_p), ("bt", c_void_p)]
 
 
+def _cl_strides(B, C, H, W):
+    return [H * W * C, 1, W * C, C]
+
+
 def supported(x, C, k, d):
+    """The library takes this layer (asked through psfm_pc_ws_floats, which applies every limit of
+    the kernels — including the corner kernels' LDS bound — and returns -1 outside them)."""
     B, _, H, W = x.shape
-    pk = k // 2
-    return (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and C % 32 == 0 and B <= 16 and B * 4 * C * 4 <= 65536
-            and H % 2 == 0 and W % 2 == 0
-            and H // 2 >= 2 * pk + 1 and W // 2 >= 2 * pk + 1)
+    if not (ENABLED and x.is_cuda and k in (3, 5) and d in (4, 8) and H % 2 == 0 and W % 2 == 0):
+        return False
+    t = PcDesc(B=B, C=C, H=H, W=W, k=k, d=d)
+    t.xs[:] = _cl_strides(B, C, H, W)
+    t.ys[:] = _cl_strides(B, C, H // 2, W // 2)
+    return int(_hip.lib().psfm_pc_ws_floats(ctypes.byref(t))) >= 0
+
+
+def _sizes(L, t):
+    """(workspace floats, weight-buffer bytes) of a descriptor; a negative answer is the library
+    refusing the shape, an error here (supported() said yes)."""
+    ws, wb = int(L.psfm_pc_ws_floats(ctypes.byref(t))), int(L.psfm_pc_wbuf_bytes(ctypes.byref(t)))
+    if ws < 0 or wb < 0:
+        raise RuntimeError("psfm_pc: shape refused: " + L.psfm_pc_last_error().decode(errors="replace"))
+    return ws, wb
 
 
 def beneficial(x, C):
@@ -87,6 +104,7 @@ class PackConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W2, w3, b3, k):
+        _hip.note_forward(ctx)
         B, C, H, W = x.shape
         d = w3.shape[0]
         ctx.dtypes = (W2.dtype, w3.dtype, b3.dtype if b3 is not None else None)
@@ -97,8 +115,9 @@ class PackConvFn(torch.autograd.Function):
                         memory_format=torch.channels_last)
         t = _desc(x, y, k, d)
         L = _hip.lib()
-        wbuf = torch.empty(int(L.psfm_pc_wbuf_bytes(ctypes.byref(t))), device=x.device, dtype=torch.uint8)
-        ws = torch.empty(max(int(L.psfm_pc_ws_floats(ctypes.byref(t))), 1), device=x.device, dtype=torch.float32)
+        nws, nwb = _sizes(L, t)
+        wbuf = torch.empty(nwb, device=x.device, dtype=torch.uint8)
+        ws = torch.empty(max(nws, 1), device=x.device, dtype=torch.float32)
         st = _hip.stream(x.device)
         _hip.check(L.psfm_pc_compose(ctypes.byref(t), _hip.ptr(W2), _hip.ptr(w3), _hip.ptr(b3), _hip.ptr(wbuf), st),
                    "psfm_pc_compose")
@@ -112,7 +131,7 @@ class PackConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        _hip.capture_guard()
+        _hip.capture_guard(ctx)
         x, W2, w3, b3, wbuf = ctx.saved_tensors
         k = ctx.k
         B, C, H, W = x.shape
@@ -127,7 +146,7 @@ class PackConvFn(torch.autograd.Function):
         st = _hip.stream(dev)
         w = PcWeights()
         _hip.check(L.psfm_pc_weights_of(ctypes.byref(t), _hip.ptr(wbuf), ctypes.byref(w)), "psfm_pc_weights_of")
-        ws = torch.empty(max(int(L.psfm_pc_ws_floats(ctypes.byref(t))), 1), **f32)
+        ws = torch.empty(max(_sizes(L, t)[0], 1), **f32)
         dx = torch.empty_like(x, memory_format=torch.channels_last) if need_x else None
         dwm = de = dc = dbt = None
         if need_w:

@@ -226,19 +226,27 @@ def test_knobs_are_read_once_and_set_explicitly(hip):
     assert hip.nondefault_knobs() == {}
     L = hip.lib()
     assert L.psfm_knob_set(b"GN_PATH", 7) == -1 and L.psfm_knob_set(b"NO_SUCH", 0) == -1
-    for name, value in (("P3D_DX", 3), ("BN_PATH", 1), ("BN_PATH", 2)):   # forms in A/B variant builds only
+    for name, value in (("P3D_DX", 3), ("BN_PATH", 1), ("BN_PATH", 2), ("K12_PRIO", 1)):   # removed forms
         with pytest.raises(ValueError):
             hip.set_knob(name, value)
 
 
 def test_knob_environment_is_parsed_at_load():
     """PSFM_<NAME> is read when the library loads (names or integers; invalid values keep the
-    default) — in a fresh process, since this one has loaded the library already."""
+    default, are reported on stderr and listed as rejected) — in a fresh process, since this one
+    has loaded the library already."""
     import subprocess
     import sys
     code = ("import sys; sys.path.insert(0, %r); import torch, packnet_sfm_amd; "
             "from packnet_sfm_amd import _hip; print(sorted(_hip.nondefault_knobs().items()))" % ROOT)
-    env = dict(os.environ, PSFM_P3D_FWD="valu", PSFM_K12_PRIO="0", PSFM_GN_PATH="bogus", PSFM_BN_PATH="threepass")
+    env = dict(os.environ, PSFM_P3D_FWD="valu", PSFM_K12_PRIO="0", PSFM_GN_PATH="bogus", PSFM_BN_PATH="threepass",
+               PSFM_GN_PIPE="0")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.strip().splitlines()[-1] == "[('K12_PRIO', 0), ('P3D_FWD', 2)]"
+    assert out.stdout.strip().splitlines()[-1] == ("[('BN_PATH', 'rejected:threepass'), ('GN_PATH', 'rejected:bogus'), "
+                                                   "('K12_PRIO', 0), ('P3D_FWD', 2)]")
+    assert "ignoring PSFM_GN_PATH=bogus" in out.stderr and "ignoring PSFM_BN_PATH=threepass" in out.stderr
+    assert "PSFM_GN_PIPE is set but that form was removed" in out.stderr
+    env = dict(os.environ, PSFM_K12_PRIO="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().splitlines()[-1] == "[('K12_PRIO', 'rejected:1')]", out

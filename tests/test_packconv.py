@@ -337,20 +337,40 @@ def test_hip_path_is_bitwise_deterministic_and_graph_capturable():
         assert torch.equal(t.grad, r.cuda())
 
 
+def _spy_pack_conv(monkeypatch, packconv):
+    """Count PackConvFn.apply calls (the composed layer's only entry) while the test runs."""
+    calls = []
+    orig = packconv.PackConvFn.apply
+
+    def spy(*a):
+        calls.append(tuple(a[0].shape))
+        return orig(*a)
+    monkeypatch.setattr(packconv.PackConvFn, "apply", staticmethod(spy))
+    return calls
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,d,k,H,W", [(64, 8, 5, 48, 160), (32, 4, 5, 64, 96), (128, 8, 3, 24, 40)])
-def test_pack_layer_composed_path_matches_the_round4_path(C, d, k, H, W):
-    """PackLayerConv3d under bf16 autocast: composed HIP path vs the pack3d + MIOpen Conv2d path
-    (both bf16, GN + ELU after): outputs and gradients within the bf16 noise of the two paths."""
+@pytest.mark.parametrize("C,d,k,B,H,W,force", [(64, 8, 5, 2, 192, 320, False), (32, 4, 5, 2, 64, 96, False),
+                                               (128, 8, 3, 6, 96, 320, True)])
+def test_pack_layer_composed_path_matches_the_round4_path(monkeypatch, C, d, k, B, H, W, force):
+    """PackLayerConv3d under bf16 autocast: the composed HIP path (asserted to run: PackConvFn.apply
+    is called exactly once per forward) vs the pack3d + MIOpen Conv2d path with composition off
+    (both bf16, the Conv2d bias, GroupNorm + ELU after): outputs and every gradient within the bf16
+    noise of the two paths.  Every case satisfies B (H/2) (W/2) >= 2 C^2 (packconv.beneficial);
+    `force` bypasses beneficial() where the round-5 policy keeps a C = 128 layer on the old path."""
     from packnet_sfm_amd.networks.layers.packnet import packconv
     from packnet_sfm_amd.networks.layers.packnet.layers01 import PackLayerConv3d
+    assert B * (H // 2) * (W // 2) >= 2 * C * C
+    if force:
+        monkeypatch.setattr(packconv, "beneficial", lambda x, C: True)
+    calls = _spy_pack_conv(monkeypatch, packconv)
     torch.manual_seed(0)
     m = PackLayerConv3d(C, k, d=d).cuda()
     with torch.no_grad():
         m.conv3d.bias.normal_(0, 0.3)
         m.conv.conv_base.bias.normal_(0, 0.1)
-    x = torch.randn(2, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(2, C, H // 2, W // 2, device="cuda")
+    x = torch.randn(B, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(B, C, H // 2, W // 2, device="cuda")
     outs = []
     for enabled in (True, False):
         packconv.ENABLED = enabled
@@ -358,11 +378,93 @@ def test_pack_layer_composed_path_matches_the_round4_path(C, d, k, H, W):
             xd = x.clone().requires_grad_(True)
             m.zero_grad()
             with torch.autocast("cuda", dtype=torch.bfloat16):
+                assert m._composed(xd) == enabled
                 y = m(xd)
             y.float().backward(gy)
             outs.append([y.detach().float(), xd.grad.float()] + [p.grad.float().clone() for p in m.parameters()])
         finally:
             packconv.ENABLED = True
-    for i, (a, b) in enumerate(zip(*outs)):
-        l2 = ((a - b).norm() / b.norm()).item()
-        assert l2 < 3e-2, (i, l2)
+        assert len(calls) == (1 if enabled else 0), calls
+        calls.clear()
+    errs = [((a - b).norm() / b.norm()).item() for a, b in zip(*outs)]
+    print("composed vs round-4 path, rel L2 (y, dx, dparams):", ["%.2e" % e for e in errs])
+    assert max(errs) < 2e-2, errs
+
+
+@pytest.mark.gpu
+def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monkeypatch):
+    """a whole PackNet01 depth net at B = 2, 192 x 640 — where pack1 and pack2
+    take the composed path (asserted: two PackConvFn calls per forward) — under bf16 autocast, against
+    the SAME weights in fp32 with composition off (MIOpen fp32 + the fp32 pack3d kernels: the chain
+    test_packnet_layer_gradients_match_reference_gpu_fp32 pins to the reference).  A fixed linear
+    loss on the four inverse-depth maps; compared: the maps, dL/drgb and the pack1 / pack2 parameter
+    gradients.  The composed network must be as close to fp32 as the round-4 bf16 network (composition
+    off) is: its relative L2 error at most 1.25x the round-4 path's + 2e-3, and the maps within 2e-2."""
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.networks.layers.packnet import packconv
+    torch.backends.cudnn.benchmark = False
+    calls = _spy_pack_conv(monkeypatch, packconv)
+    import golden_util as gu
+    from test_networks import _packnet_model
+    dev = torch.device("cuda:0")
+    depth, _ = _packnet_model()
+    depth = depth.to(dev).train()
+    g = torch.Generator().manual_seed(11)
+    B, H, W = 2, 192, 640
+    rgb = gu.smooth_texture(g, B, 3, H, W).to(dev)
+    gys = [torch.randn(B, 1, H >> i, W >> i, generator=g).to(dev) for i in range(4)]
+    watched = [depth.pack1.conv.conv_base.weight, depth.pack1.conv3d.weight, depth.pack1.conv3d.bias,
+               depth.pack2.conv.conv_base.weight, depth.pack2.conv3d.weight, depth.pack2.conv3d.bias]
+
+    def run(bf16, enabled):
+        packconv.ENABLED = enabled
+        try:
+            depth.zero_grad()
+            x = rgb.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+                inv = depth(x)["inv_depths"]
+            loss = sum((i.float() * gy).sum() for i, gy in zip(inv, gys))
+            loss.backward()
+            torch.cuda.synchronize()
+            return [i.detach().float() for i in inv] + [x.grad.float()] + [p.grad.float().clone() for p in watched]
+        finally:
+            packconv.ENABLED = True
+
+    ref = run(False, False)
+    assert not calls
+    comp = run(True, True)
+    assert len(calls) == 2 and calls[0][1:] == (64, 192, 640) and calls[1][1:] == (64, 96, 320), calls
+    calls.clear()
+    old = run(True, False)
+    assert not calls
+    names = ["inv0", "inv1", "inv2", "inv3", "drgb", "pack1.W2", "pack1.w3", "pack1.b3", "pack2.W2", "pack2.w3",
+             "pack2.b3"]
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    rows = [(n, rel(c, r), rel(o, r)) for n, c, o, r in zip(names, comp, old, ref)]
+    print("rel L2 vs fp32 (composed, round-4 bf16):", ["%s %.2e %.2e" % t for t in rows])
+    for n, ec, eo in rows:
+        assert ec <= 1.25 * eo + 2e-3, (n, ec, eo)
+        if n.startswith("inv"):
+            assert ec < 2e-2, (n, ec)
+
+
+def test_supported_asks_the_library_for_its_limits():
+    """packconv.supported() applies every limit of the kernels (it asks psfm_pc_ws_floats),
+    including the corner kernels' LDS bound (B pk^2 C + 4 B 64) * 4 <= 64 KB that the round-5 Python
+    check missed (k = 5, B = 16, C = 256 and B = 8, C = 512 were accepted there, then refused)."""
+    import __graft_entry__
+    __graft_entry__.build()
+    from packnet_sfm_amd.networks.layers.packnet import packconv
+
+    class X:   # stands in for a bf16 channels_last ROCm tensor (only .shape / .is_cuda are read)
+        is_cuda = True
+
+        def __init__(self, *shape):
+            self.shape = shape
+    assert not packconv.supported(X(16, 256, 64, 64), 256, 5, 8)
+    assert not packconv.supported(X(8, 512, 64, 64), 512, 5, 8)
+    assert packconv.supported(X(8, 512, 64, 64), 512, 3, 8)
+    assert packconv.supported(X(6, 64, 192, 640), 64, 5, 8)
+    assert not packconv.supported(X(6, 64, 191, 640), 64, 5, 8)
+    assert not packconv.supported(X(2, 48, 64, 64), 48, 5, 8)      # C % 32

@@ -25,6 +25,9 @@ VARIANTS = {
         else __builtin_amdgcn_s_setprio(2);""", """        __builtin_amdgcn_s_setprio(2);""")],
 }
 VARIANTS["launder_prio2"] = VARIANTS["launder"] + VARIANTS["prio2"]
+# ("FLAGS", extra hipcc flags) entries add compile flags instead of editing text
+VARIANTS["noslp"] = [("FLAGS", "-fno-slp-vectorize")]
+VARIANTS["noslp_launder"] = VARIANTS["noslp"] + VARIANTS["launder"]
 
 
 def build(name):
@@ -32,7 +35,8 @@ def build(name):
     try:
         src = os.path.join(d, "csrc")
         shutil.copytree(os.path.join(ROOT, "packnet-sfm-resnet-san_amd", "csrc"), src)
-        for fn, old, new in VARIANTS[name]:
+        extra = [f for fn, f, _ in [(e[0], e[1], None) for e in VARIANTS[name]] if fn == "FLAGS"]
+        for fn, old, new in [e for e in VARIANTS[name] if e[0] != "FLAGS"]:
             p = os.path.join(src, fn)
             s = open(p).read()
             assert old in s, (name, fn, old[:80])
@@ -46,7 +50,7 @@ def build(name):
         os.makedirs(os.path.dirname(out), exist_ok=True)
         import __graft_entry__ as G
         srcs = sorted(os.path.join(src, f) for f in os.listdir(src) if f.endswith(".hip"))
-        r = subprocess.run(["/opt/rocm/bin/hipcc", *G.FLAGS, "-I", os.path.join(ROOT, "include"),
+        r = subprocess.run(["/opt/rocm/bin/hipcc", *G.FLAGS, *extra, "-I", os.path.join(ROOT, "include"),
                             f'-DPSFM_SRC_HASH="variant-{name[:8]:8s}"', *srcs, "-o", out], capture_output=True, text=True)
         if r.returncode or os.path.getsize(out) < 1 << 20:
             raise RuntimeError(f"variant {name}: build failed rc={r.returncode}\n{r.stdout[-1500:]}\n{r.stderr[-2000:]}")
