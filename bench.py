@@ -20,11 +20,13 @@ and `cpu_baseline` (the CPU restatement — same nets on CPU in fp32 + the oracl
 this host's cores, rank 0 at N=1 only).
 """
 import argparse
+import datetime
 import json
 import os
 import socket
 import statistics
 import subprocess
+import tempfile
 import sys
 import time
 
@@ -101,6 +103,7 @@ def parse(argv=None):
                     help="seconds before a hung probe child is killed (-> split)")
     ap.add_argument("--probe-only", action="store_true",
                     help="run the --comm auto selection, print it as JSON on rank 0, exit (no training)")
+    ap.add_argument("--probe-report", default=None, help=argparse.SUPPRESS)   # probe child: rank 0's info as JSON
     ap.add_argument("--probe-backend", default=None, choices=["nccl", "gloo"],
                     help="backend of the probe children (default: --dist-backend; gloo = CPU, tests)")
     ap.add_argument("--force-comm", action="store_true",
@@ -183,7 +186,7 @@ def relaunch_distributed(args):
     return subprocess.call(cmd, env=env)
 
 
-def launch_comm_probe(args, rank, world, local_rank, port, backend):
+def launch_comm_probe(args, rank, world, local_rank, port, backend, report=None):
     """Start THIS rank's probe child (bench.py --comm-probe: trainers/comm_probe.py) in its own
     session and return its exit status (124 after a kill at --comm-probe-timeout).  The children
     form their own process group on `port`; nothing of theirs lives on in this process."""
@@ -191,8 +194,10 @@ def launch_comm_probe(args, rank, world, local_rank, port, backend):
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
     env.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local_rank), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-    cmd = [sys.executable, os.path.abspath(__file__), "--comm-probe", "--gpus", str(world),
-           "--dist-backend", backend]
+    # the child re-parses this run's own arguments (config, batch, --bucket-mb: the probe cuts the
+    # same buckets) with the probe flags last
+    cmd = [sys.executable, os.path.abspath(__file__), *sys.argv[1:], "--comm-probe", "--gpus", str(world),
+           "--dist-backend", backend] + (["--probe-report", report] if report else [])
     p = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=sys.stderr, stderr=sys.stderr)
     try:
         return p.wait(timeout=args.comm_probe_timeout)
@@ -219,6 +224,21 @@ def choose_comm(store, rank, world, run_child):
     return "split", f"auto: overlap probe failed (rank: exit status {bad}), split"
 
 
+def param_shapes(args):
+    """(depth-net, pose-net) shapes, in order, of this run's parameters that receive a gradient in its
+    step (the trainer buckets only those; ResNetSAN01's sparse-branch blend weights get none on the
+    RGB path): the model built and run forward + backward on the meta device (no memory, no kernels).
+    The probe's ShapeNet stands in for the model with them."""
+    with torch.device("meta"):
+        m = build_model(args, torch.device("meta"))
+        x = torch.empty(1, 3, args.height, args.width)
+        inv = m.depth_net(x)["inv_depths"]
+        vec = m.pose_net(x, [x] * N_CTX)
+        (sum(i.float().mean() for i in inv) + vec.float().mean()).backward()
+    used = lambda net: [tuple(p.shape) for p in net.parameters() if p.grad is not None]  # noqa: E731
+    return used(m.depth_net), used(m.pose_net)
+
+
 def comm_probe_main(args, world, rank, local_rank):
     """The probe child: its own process group, trainers/comm_probe.run_probe, exit status."""
     if os.environ.get("PSFM_TEST_PROBE_FAIL_RANK") == str(rank):   # tests/test_distributed.py: a failing child
@@ -235,9 +255,13 @@ def comm_probe_main(args, world, rank, local_rank):
     rc = 0
     try:
         import __graft_entry__
-        __graft_entry__.build()
+        __graft_entry__.build()   # a no-op: the training ranks built before starting the probe
         from packnet_sfm_amd.trainers.comm_probe import run_probe
-        info = run_probe(device)
+        info = run_probe(device, bucket_mb=args.bucket_mb, shapes=param_shapes(args))
+        if rank == 0 and args.probe_report:
+            with open(args.probe_report, "w") as f:
+                json.dump(info, f)
+        info.pop("cuts")
         print(f"[comm probe] rank {rank}: {json.dumps(info)}", file=sys.stderr, flush=True)
     except Exception as e:  # noqa: BLE001  (any failure means: do not use the overlap path)
         print(f"[comm probe] rank {rank}: FAILED {type(e).__name__}: {e}", file=sys.stderr, flush=True)
@@ -572,9 +596,28 @@ def main():
             if world > 1:   # torch.distributed.run's store (the training process group reuses it)
                 from torch.distributed.rendezvous import rendezvous
                 store, _, _ = next(rendezvous("env://", rank, world))
+            # the library is built ONCE, by rank 0, before any probe child starts (hipcc does not touch
+            # the GPU); the others wait for it, so a cold build never runs inside a probe's timeout
+            import __graft_entry__
+            if rank == 0:
+                __graft_entry__.build()
+                if store is not None:
+                    store.set("psfm_built", "1")
+            elif store is not None:
+                store.wait(["psfm_built"], datetime.timedelta(seconds=1800))
+            probe_file = os.path.join(tempfile.gettempdir(), f"psfm_probe_{os.getpid()}.json") if rank == 0 else None
             args.comm, comm_note = choose_comm(
                 store if store is not None else dist.HashStore(), rank, world,
-                lambda port: launch_comm_probe(args, rank, world, local_rank, port, probe_backend))
+                lambda port: launch_comm_probe(args, rank, world, local_rank, port, probe_backend, probe_file))
+            if rank == 0:
+                try:
+                    with open(probe_file) as f:
+                        probe_info = json.load(f)
+                    os.remove(probe_file)
+                    comm_note += (f"; probe: {probe_info['model']}, {probe_info['buckets']} buckets of "
+                                  f"{probe_info['bucket_mb']} MB")
+                except (OSError, ValueError, KeyError):
+                    pass
             if args.dist_backend == "gloo":   # a gloo run cannot capture its collectives
                 args.comm, comm_note = "split", comm_note + " (gloo run: split)"
         else:

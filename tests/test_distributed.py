@@ -536,3 +536,62 @@ def test_comm_auto_probe_failure_and_hang_select_split():
     res, err = _torchrun_probe({"PSFM_TEST_PROBE_FAIL_RANK": "1"}, "--comm-probe-timeout", "20")
     assert res["comm"] == "split" and "failed" in res["comm_note"], res
     assert "3" in res["comm_note"] and "124" in res["comm_note"], res
+
+
+class _NetsOnly(torch.nn.Module):
+    """The bench model's depth / pose nets with a loss that reaches every output (so the same
+    parameters get gradients as under the photometric loss), for the bucket-cut comparison."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.depth_net, self.pose_net = model.depth_net, model.pose_net
+
+    def forward(self, batch, progress=0.0):
+        inv = self.depth_net(batch["rgb"])["inv_depths"]
+        vec = self.pose_net(batch["rgb"], batch["rgb_context"])
+        return {"loss": (sum(i.float().mean() for i in inv) + vec.float().mean()).reshape(1)}
+
+
+def _cuts_worker(rank, world, init_file, config, out_dir):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    os.environ["WORLD_SIZE"] = str(world)
+    import json
+
+    import bench
+    from packnet_sfm_amd.trainers import comm_probe
+    from packnet_sfm_amd.trainers.ddp_trainer import DDPTrainer, make_optimizer
+    torch.set_num_threads(4)
+    args = bench.parse(["--config", config, "--bucket-mb", "16"])
+    probe = comm_probe.run_probe(torch.device("cpu"), steps=2, bucket_mb=args.bucket_mb, shapes=bench.param_shapes(args))
+    torch.manual_seed(0)
+    model = _NetsOnly(bench.build_model(args, torch.device("cpu")))
+    tr = DDPTrainer(model, make_optimizer(model), torch.device("cpu"), amp_dtype=None, graph=False, flat=True,
+                    comm="overlap", overlap_bucket_mb=args.bucket_mb, force_comm=True)
+    g = torch.Generator().manual_seed(rank)
+    batch = {"rgb": torch.rand(1, 3, 64, 192, generator=g), "rgb_context": [torch.rand(1, 3, 64, 192, generator=g)
+                                                                            for _ in range(2)]}
+    for _ in range(2):
+        tr.train_step(batch)
+    real = comm_probe.bucket_cuts(tr)
+    if rank == 0:
+        with open(os.path.join(out_dir, "cuts.json"), "w") as f:
+            json.dump({"probe": [list(r) for r in probe["cuts"]], "probe_mb": probe["bucket_mb"],
+                       "real": [list(r) for r in real[0]], "real_mb": real[1]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config", ["kitti-resnet-san", "kitti-packnet"])
+def test_comm_probe_cuts_the_same_buckets_as_the_training_step(config):
+    """the --comm auto probe's stand-in (trainers/comm_probe.ShapeNet: the bench
+    model's parameter shapes, built on the meta device) cuts exactly the gradient buckets the real
+    model's trainer cuts at the bench's 16 MB bucket size — the same number of RCCL calls with the same
+    message sizes — on 2 gloo ranks."""
+    import json
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_cuts_worker, args=(world, os.path.join(d, "init"), config, d), nprocs=world, join=True)
+        with open(os.path.join(d, "cuts.json")) as f:
+            res = json.load(f)
+    assert len(res["real"]) >= 2 and res["probe"] == res["real"], res
+    assert res["probe_mb"] == res["real_mb"]
