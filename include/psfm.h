@@ -96,8 +96,9 @@ typedef struct psfm_workspace {
                                                     UN-warped context (scale independent)  */
     float* sig_part;     /* [S][B][16]              chunk sums of each sigmoid map (the
                                                     smoothness normaliser, fwd_grad only)  */
-    float* cam_pairs;    /* [S][B][PSFM_CAMREC][2]  the camera records of contexts 0 and 1
-                                                    interleaved (written by the prepass): K12
+    float* cam_pairs;    /* [S][B][48][2]           the camera records of contexts 0 and 1
+                                                    interleaved (written by the prepass), with
+                                                    M = K_ref R and m = K_ref t appended: K12
                                                     projects both contexts with packed f32
                                                     pairs, one 8-byte scalar load per entry  */
 } psfm_workspace;

@@ -389,18 +389,25 @@ def sensitive_pixels(image, contexts, sigs, K, pose_mats, min_depth, max_depth, 
       2e-4 px coordinate difference on a steep texture moves the warped value that much) — the
       derivative of |est - tgt| flips sign there (the selected candidate's 3x3 SSIM window aside,
       only that pixel's gradient moves).
-    Computed in float64 from the same inputs.  Full-resolution scales only.  With `return_ties`
-    also the (undilated) near-tie maps, the `tie_flip` argument of photometric_loss.
+    Computed in float64 from the same inputs.  A scale whose map is smaller than the image is
+    evaluated as photometric_loss evaluates it (multi-resolution maps: the images resized to the
+    map, the intrinsics scaled, :274-300).  With `return_ties` also the (undilated) near-tie maps,
+    the `tie_flip` argument of photometric_loss.
     """
     out, ties = [], []
-    img = image.double()
-    ctx = [c.double() for c in contexts]
     fish = isinstance(K, dict)
-    Kd = {k: v.double() for k, v in K.items()} if fish else K.double()
+    Kf = {k: v.double() for k, v in K.items()} if fish else K.double()
     mats = [m.double() for m in pose_mats]
-    H, W = image.shape[-2:]
+    H0, W0 = image.shape[-2:]
     for s in sigs:
         s = s.double()
+        H, W = s.shape[-2:]
+        img = resize_like(image.double(), s.shape)
+        ctx = [resize_like(c.double(), s.shape) for c in contexts]
+        if (H, W) == (H0, W0):
+            Kd = Kf
+        else:
+            Kd = fisheye_scale(Kf, W / float(W0), H / float(H0)) if fish else scale_K(Kf, W / float(W0))
         depth = 1.0 / (1.0 / (sigmoid_to_depth(s, min_depth, max_depth) + 1e-8)).clamp(min=1e-6)
         X = fisheye_lift(depth, Kd) if fish else lift(depth, Kd)
         bad = torch.zeros_like(s, dtype=torch.bool)

@@ -25,11 +25,14 @@
 //           vertically into the three q-rows they touch (reflect weights at the image edge);
 //   q-eval  row v-3 (its three p-rows are now complete): horizontal 3-sum of the accumulated
 //           coefficients (DPP), adjoint through the bilinear sample (d warp / d(ix,iy) stashed
-//           in wave-private LDS at issue time) and the projection, dL/d[R|t] of both contexts,
-//           plus the per-pixel smoothness gradient -> dL/dsig written once (no LDS ring, no
-//           barrier, no atomics: deterministic);
-//   resolve the bilinear samples of row v (x and d x/d(ix,iy)) with validity-masked tap and
-//           derivative coefficients (grid_sample's zero padding: an out-of-bounds tap adds 0).
+//           in wave-private LDS at issue time) and the projection — pinhole: from the issue's
+//           stashed 1/z, warp depth and d warp / d sigmoid, p = M X + m (M = K_ref R) and
+//           dL/dX = M^T dL/dp, no second depth chain or projection — dL/dp (X, 1)^T of both
+//           contexts (taken through K_ref^T once per wave), plus the per-pixel smoothness
+//           gradient -> dL/dsig written once (no LDS ring, no barrier, no atomics: deterministic);
+//   resolve the bilinear samples of row v (x and d x/d(ix,iy)); the gathers are range-checked
+//           raw buffer loads, so an out-of-bounds tap arrives as 0 (grid_sample's zero padding)
+//           and needs neither a clamped address nor a mask.
 // Reference: losses/multiview_photometric_loss.py:15-54, :199-297, :301-327,
 // utils/depth.py:146-198, geometry/camera.py:111-190, geometry/camera_utils.py:27-59.
 #pragma once
@@ -69,13 +72,20 @@ constexpr int SIGCH = 16;        // chunks of the per-(scale, image) sigmoid sum
 constexpr int GTS = 28;          // per-lane dL/dT row: 12 entries x 2 contexts, padded to 28 dwords
                                  // (the 16 lanes of a b128 access start on distinct bank groups)
 
+constexpr int PAIR_REC = 48;     // entries (f2: both contexts) of the context-paired camera record
+                                 // ws.cam_pairs: Ki 0-8 | Kr 9-17 | T 18-29 | pad | M = Kr R 32-40 |
+                                 // m = Kr t 41-43 | pad (psfm_photometric.hip k_sig_sum builds it)
+
 __host__ __device__ inline int stripes(int W) { return (W + OW - 1) / OW; }
 __host__ __device__ inline int units(int H, int W, int rb) { return stripes(W) * ((H + rb - 1) / rb); }
 // wave-private LDS (each lane touches only its own column: no barriers):
-//   [3 row slots][6][64] f2  d warp / d(ix, iy) of both contexts | [64][GTS] dL/dT accumulators
+//   [3 row slots][6][64] f2  d warp / d(ix, iy) of both contexts | [64][GTS] dL/dT accumulators |
+//   [4 row slots][64] float4  the issue phase's projection terms the q-eval reuses (pinhole: 1/z of
+//   both contexts with the z-clamp pass in the sign, the warp depth, d warp / d sigmoid)
+// 20 KB: 8 waves per CU (two per SIMD) fill the 160 KB exactly
 __host__ __device__ inline size_t lds_bytes(int NC) {
     (void)NC;
-    return ((size_t)3 * 6 * 64 * 2 + (size_t)GTS * 64) * sizeof(float);
+    return ((size_t)3 * 6 * 64 * 2 + (size_t)GTS * 64 + (size_t)4 * 64 * 4) * sizeof(float);
 }
 
 // Optional per-wave timestamps (psfm_k12_stamps): when set, lane 0 of every wave writes the
@@ -117,41 +127,53 @@ __device__ __forceinline__ f2 mask01(bool a, bool b) { return f2{a ? 1.0f : 0.0f
 struct Pend {
     float q[3][4];
     float ax, bx, ay, by;
-    bool xw, xe, yn, ys;
 };
 
-__device__ __forceinline__ void gather(const float* __restrict__ img, uint32_t pb, float ix, float iy, int H,
-                                       int W, Pend& g) {
-    const TapAddr t = tap_addr(ix, iy, H, W);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        g.q[c][0] = ldg(img, c * pb + t.nw);
-        g.q[c][1] = ldg(img, c * pb + t.ne);
-        g.q[c][2] = ldg(img, c * pb + t.sw);
-        g.q[c][3] = ldg(img, c * pb + t.se);
-    }
-    g.ax = t.ax;
-    g.bx = t.bx;
-    g.ay = t.ay;
-    g.by = t.by;
-    g.xw = t.xw;
-    g.xe = t.xe;
-    g.yn = t.yn;
-    g.ys = t.ys;
+// The context image of (b) as a range-checked buffer: V# with the image's 3 planes as num_records,
+// stride 0 (raw), gfx9 dword3.  A raw buffer load whose offset lies past num_records returns 0, which
+// is grid_sample's zero padding of an out-of-bounds tap (padding_mode='zeros'): the 12 gathers need
+// no coordinate clamps and the resolve no per-channel tap masks.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t img_rsrc(const float* img, uint32_t pb) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0, (int)(3u * pb), 0x00020000);
 }
 
-// grid_sample value and d/d(ix), d/d(iy) of the two contexts of a pair (same arithmetic as
-// sweep::bilinear3_vd).  A tap is valid when its row and its column are: the taps are multiplied
-// by 0/1 masks (out-of-bounds taps read a clamped valid address), which is grid_sample's zero
-// padding (padding_mode='zeros') without per-channel selects — every channel is v_pk_* work for
-// both contexts.
-__device__ __forceinline__ void resolve1(const Pend& g, float v[3], float dix[3], float diy[3]) {
-    const float wnw = g.ax * g.ay, wne = g.bx * g.ay, wsw = g.ax * g.by, wse = g.bx * g.by;
-    const bool vnw = g.yn && g.xw, vne = g.yn && g.xe, vsw = g.ys && g.xw, vse = g.ys && g.xe;
+// one tap's byte offset when valid, else past the buffer (channel c adds c * pb as the SGPR offset:
+// the result stays past 3 * pb either way the hardware counts it)
+constexpr uint32_t TAP_OOB = 0x80000000u;
+
+__device__ __forceinline__ void gather(__amdgpu_buffer_rsrc_t rs, uint32_t pb, float ix, float iy, int H, int W,
+                                       Pend& g) {
+    // some tap may be in bounds iff ix in [-1, W) (and y alike); the wider open interval keeps the
+    // float -> int conversion defined (and rejects NaN): outside it every tap is out of bounds
+    const bool ok = (ix > -2.0f) && (ix < (float)W + 1.0f) && (iy > -2.0f) && (iy < (float)H + 1.0f);
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = ok ? (int)fx0 : -2, y0 = ok ? (int)fy0 : -2;
+    const bool xw = (unsigned)x0 < (unsigned)W, xe = (unsigned)(x0 + 1) < (unsigned)W;
+    const bool yn = (unsigned)y0 < (unsigned)H, ys = (unsigned)(y0 + 1) < (unsigned)H;
+    const uint32_t o = (uint32_t)(y0 * W + x0) * 4u, row = (uint32_t)W * 4u;
+    const uint32_t onw = (yn && xw) ? o : TAP_OOB, one = (yn && xe) ? o + 4u : TAP_OOB;
+    const uint32_t osw = (ys && xw) ? o + row : TAP_OOB, ose = (ys && xe) ? o + row + 4u : TAP_OOB;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const float nw = vnw ? g.q[c][0] : 0.0f, ne = vne ? g.q[c][1] : 0.0f;
-        const float sw = vsw ? g.q[c][2] : 0.0f, se = vse ? g.q[c][3] : 0.0f;
+        const int so = (int)(c * pb);
+        g.q[c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, onw, so, 0));
+        g.q[c][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, one, so, 0));
+        g.q[c][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, osw, so, 0));
+        g.q[c][3] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ose, so, 0));
+    }
+    g.ax = (fx0 + 1.0f) - ix;
+    g.bx = ix - fx0;
+    g.ay = (fy0 + 1.0f) - iy;
+    g.by = iy - fy0;
+}
+
+// grid_sample value and d/d(ix), d/d(iy) of one context (same arithmetic as sweep::bilinear3_vd;
+// out-of-bounds taps arrived as 0)
+__device__ __forceinline__ void resolve1(const Pend& g, float v[3], float dix[3], float diy[3]) {
+    const float wnw = g.ax * g.ay, wne = g.bx * g.ay, wsw = g.ax * g.by, wse = g.bx * g.by;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float nw = g.q[c][0], ne = g.q[c][1], sw = g.q[c][2], se = g.q[c][3];
         float acc = 0.0f;
         acc += nw * wnw;
         acc += ne * wne;
@@ -181,6 +203,23 @@ __device__ __forceinline__ void resolve_pair(const Pend& a, const Pend& b, f2 (&
 // context-paired record of (s, b): entry k = (context 0, context 1) floats 2k, 2k+1.
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(4))) const f2 cf2;
+
+// What the q-eval needs of the pinhole pair record: K^-1 of the target, M = K_ref R and m = K_ref t
+// of both contexts (p = M X + m: the projection's first two rows without the intermediate c = R X + t;
+// the adjoint dL/dX = M^T dL/dp).  dL/d[R|t] is accumulated as dL/dp (X, 1)^T and taken through
+// K_ref^T once per wave (bwd_pose_rows).
+struct CamPairBwd {
+    float Ki[9];
+    f2 M[9], m[3];
+    __device__ __forceinline__ void load(cf2* rec) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Ki[i] = rec[i].x;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) M[i] = rec[32 + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) m[i] = rec[41 + i];
+    }
+};
 
 struct PairProj {
     f2 p0, p1, p2;  // K_ref (R X + t)
@@ -283,12 +322,16 @@ __device__ __forceinline__ f2 photo_grad_pair(const f2 (&xa)[3], const f2 (&xb)[
         const f2 Nn = A1 * A2, D = B1 * B2;
         const f2 iD = pk_rcp(D);
         const f2 l = (1.0f - Nn * iD) * 0.5f;
-        ls += f2{__builtin_amdgcn_fmed3f(l.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(l.y, 0.0f, 1.0f)};
-        const f2 pass = pk_sel01(l);
-        const f2 iD2 = iD * iD;
-        cf[c] = pass * (2.0f * my * (A2 - A1) * iD - Nn * 2.0f * mx * (B2 - B1) * iD2);
-        cf[3 + c] = pass * (-Nn * B1 * iD2);
-        cf[6 + c] = pass * (2.0f * A1 * iD);
+        const f2 lc = f2{__builtin_amdgcn_fmed3f(l.x, 0.0f, 1.0f), __builtin_amdgcn_fmed3f(l.y, 0.0f, 1.0f)};
+        ls += lc;
+        // adjoint coefficients with the clamp pass (l inside [0, 1]: the clamped value is l; NaN fails)
+        // folded into the common factor u = pass / D:  dSSIM/dmx = 2 u (my (A2 - A1) - mx (Nn / D) (B2 - B1)),
+        // dSSIM/dE[x^2] = -(Nn / D) B1 u, dSSIM/dE[xy] = 2 A1 u
+        const f2 u = f2{lc.x == l.x ? iD.x : 0.0f, lc.y == l.y ? iD.y : 0.0f};
+        const f2 u2 = u + u, q = Nn * iD;
+        cf[c] = u2 * (my * (A2 - A1) - (mx * q) * (B2 - B1));
+        cf[3 + c] = -(q * B1) * u;
+        cf[6 + c] = A1 * u2;
         const f2 dd = xb[c] - yb[c];
         l1 += f2{fabsf(dd.x), fabsf(dd.y)};
         PSFM_CHAN();
@@ -337,7 +380,7 @@ struct K12 {
     uint32_t plane, pb;
     bool pcol, qcol, border_l, border_r;
     DepthChain dc;
-    float l1w, gscale, cx, cy, mc, wxl, wxr;
+    float l1w, gscale, cx, cy, mc, rmc, wxl, wxr;
     const float* tgt;
     const float* sig;
     const float* ctx[NC];
@@ -345,7 +388,9 @@ struct K12 {
     const float* mask;
     float* gsig;
     f2* di;      // wave-private LDS [3][6][64] f2
-    float* gt;   // this lane's dL/dT accumulators: gt[2 m + j] (entry m, context j), 16-B aligned
+    float* gt;   // this lane's dL/dT accumulators: gt[2 m + j] (entry m, context j), 16-B aligned;
+                 // pinhole: dL/dp (X, 1)^T (K_ref^T applied per wave at the end), fisheye: dL/d[R|t]
+    float4* stash;  // wave-private LDS [4][64]: the issue phase's projection terms for the q-eval
     const float* camrec;   // record of (s, context 0, b); context j is j*B records further
     const float* campair;  // context-paired record of (s, b) (ws.cam_pairs)
     bool young;            // the second wave dispatched to its SIMD (Args::young_from), wave-uniform
@@ -381,6 +426,13 @@ struct K12 {
         uint64_t rp = reinterpret_cast<uint64_t>(campair);
         asm volatile("" : "+s"(rp));
         c.load(reinterpret_cast<cf2*>(rp), H, W);
+        return c;
+    }
+    __device__ __forceinline__ CamPairBwd load_pair_bwd() const {
+        CamPairBwd c;
+        uint64_t rp = reinterpret_cast<uint64_t>(campair);
+        asm volatile("" : "+s"(rp));
+        c.load(reinterpret_cast<cf2*>(rp));
         return c;
     }
 
@@ -433,8 +485,9 @@ struct K12 {
         gsig = pick4(a.grad_sig, s) + (size_t)b * plane;
         di = reinterpret_cast<f2*>(lds);
         gt = lds + 3 * 6 * 64 * 2 + lane * GTS;
+        stash = reinterpret_cast<float4*>(lds + 3 * 6 * 64 * 2 + GTS * 64);
         camrec = a.in.cam + ((size_t)s * NC * B + b) * PSFM_CAMREC;
-        campair = a.ws.cam_pairs + ((size_t)s * B + b) * 2 * PSFM_CAMREC;
+        campair = a.ws.cam_pairs + ((size_t)s * B + b) * 2 * PAIR_REC;
         // per-image mean of the sigmoid map (smoothness normaliser, utils/depth.py:183-185),
         // from the SIGCH chunk sums of the pre-pass, summed in chunk order in fp64 (wave-uniform
         // scalar loads: written by the previous launch, read-only here)
@@ -447,6 +500,7 @@ struct K12 {
             for (int i = 0; i < SIGCH; ++i) v += (double)sp[i];
             mc = fmaxf((float)(v / ((double)H * W)), 1e-6f);
         }
+        rmc = 1.0f / mc;   // once per wave: the q-eval multiplies (within 1 ulp of dividing)
     }
 
     // d warp / d(ix, iy) of a row slot, both contexts: [slot][m][64] f2 (b64, conflict-free)
@@ -517,8 +571,13 @@ struct K12 {
                 const CamPair cams = load_pair();
                 PairProj pr;
                 cams.project(cams.lift((float)colr, (float)r, d), pr);
-                gather(ctx[0], pb, pr.ix.x, pr.iy.x, H, W, pd[0]);
-                if (NC == 2) gather(ctx[NC - 1], pb, pr.ix.y, pr.iy.y, H, W, pd[NC - 1]);
+                gather(img_rsrc(ctx[0], pb), pb, pr.ix.x, pr.iy.x, H, W, pd[0]);
+                if (NC == 2) gather(img_rsrc(ctx[NC - 1], pb), pb, pr.ix.y, pr.iy.y, H, W, pd[NC - 1]);
+                // what the q-eval of this row (step k + 3, slot I) takes from here instead of
+                // re-running the depth chain and the projection: 1/z of both contexts (negated where
+                // z = p2 was clamped: no gradient through it), the warp depth, d warp / d sigmoid
+                stash[I * 64 + lane] = make_float4(pr.p2.x >= 1e-5f ? pr.iz.x : -pr.iz.x,
+                                                   pr.p2.y >= 1e-5f ? pr.iz.y : -pr.iz.y, d, dc.dwarp_ds(d, d1, inv));
             } else {
                 const CM cams = load_cams();
                 const Lift l = cams.lift((float)colr, (float)r, d);
@@ -526,7 +585,7 @@ struct K12 {
                 for (int j = 0; j < NC; ++j) {
                     typename CM::P pr;
                     cams.project(j, l, pr);
-                    gather(ctx[j], pb, pr.ix, pr.iy, H, W, pd[j]);
+                    gather(img_rsrc(ctx[j], pb), pb, pr.ix, pr.iy, H, W, pd[j]);
                 }
             }
         }
@@ -636,14 +695,14 @@ struct K12 {
             if (pin && col < W - 1) {
                 const float m = (fabsf(S.template Y<IB>()[0] - y_r[0]) + fabsf(S.template Y<IB>()[1] - y_r[1]) +
                                  fabsf(S.template Y<IB>()[2] - y_r[2])) * (1.0f / 3.0f);
-                const float w = expf(-m);
+                const float w = __expf(-m);   // v_exp_f32(-m log2 e): m in [0, 1], within 2 ulp of expf
                 h = sgnf(c - sg_r) * w;
                 if (pout) S.acc_ax += fabsf(c - sg_r) * w;
             }
             if (pin && pv < H - 1) {
                 const float m = (fabsf(S.template Y<IB>()[0] - S.template Y<IC>()[0]) + fabsf(S.template Y<IB>()[1] - S.template Y<IC>()[1]) +
                                  fabsf(S.template Y<IB>()[2] - S.template Y<IC>()[2])) * (1.0f / 3.0f);
-                const float w = expf(-m);
+                const float w = __expf(-m);   // v_exp_f32(-m log2 e): m in [0, 1], within 2 ulp of expf
                 t = sgnf(c - S.template SG<IC>()) * w;
                 if (pout) S.acc_ay += fabsf(c - S.template SG<IC>()) * w;
             }
@@ -660,17 +719,18 @@ struct K12 {
         for (int q = 0; q < NP; ++q) {
             const f2 Gq = f2{G[2 * q], (2 * q + 1 < NC) ? G[2 * q + 1] : 0.0f};
             const f2 kS = Gq * ((-0.5f / 27.0f) * p.ssim_w);
+            const f2 kS2 = kS + kS;   // the E[x^2] term's factor 2 (d x^2 / dx = 2 x) on the coefficient:
+                                      // (x + x) hb == x (2 hb) exactly
             const f2 kL = Gq * (l1w * (1.0f / 3.0f));
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                f2 ha = kS * cf[q][c], hb = kS * cf[q][3 + c], he = kS * cf[q][6 + c];
+                f2 ha = kS * cf[q][c], hb = kS2 * cf[q][3 + c], he = kS * cf[q][6 + c];
                 hsum_w(ha, hb, he);
                 const f2 xa = S.template X<IA>()[q][c], xb = S.template X<IB>()[q][c], xc = S.template X<IC>()[q][c];
-                const f2 xa2 = xa + xa, xb2 = xb + xb, xc2 = xc + xc;
-                S.D0[q][c] += wyd * (ha + xa2 * hb + S.template Y<IA>()[c] * he);
+                S.D0[q][c] += wyd * (ha + xa * hb + S.template Y<IA>()[c] * he);
                 const f2 db = xb - S.template Y<IB>()[c];
-                S.D1[q][c] += (ha + xb2 * hb + S.template Y<IB>()[c] * he) + kL * f2{sgnf(db.x), sgnf(db.y)};
-                S.D2[q][c] = wyu * (ha + xc2 * hb + S.template Y<IC>()[c] * he);
+                S.D1[q][c] += (ha + xb * hb + S.template Y<IB>()[c] * he) + kL * f2{sgnf(db.x), sgnf(db.y)};
+                S.D2[q][c] = wyu * (ha + xc * hb + S.template Y<IC>()[c] * he);
             }
         }
     }
@@ -713,34 +773,46 @@ struct K12 {
             gix += S.D0[0][c] * dv[c];
             giy += S.D0[0][c] * dv[3 + c];
         }
-        float d1, inv;
-        const float d = dc.warp_depth(S.template SG<IQ>(), d1, inv);
-        const float dw = dc.dwarp_ds(d, d1, inv);
         float gs;
-        f2* g2 = reinterpret_cast<f2*>(gt);   // entry m of both contexts
         if constexpr (PAIR_CAM) {
-            const CamPair cams = load_pair();
-            const Lift l = cams.lift((float)col, (float)qv, d);
-            PairProj pr;
-            cams.transform(l, pr);
-            f2 gc[3];
-            const f2 gd = cams.grad(pr, l, gix, giy, gc);
-            gs = (NC == 2 ? gd.x + gd.y : gd.x) * dw;
-            // dL/dT += gc (X, 1)^T for both contexts: lane-private LDS row, b128 read-modify-write
-            float4* g4 = reinterpret_cast<float4*>(gt);
+            // the row's 1/z, warp depth and d warp / d sigmoid from its issue (stash slot IQ); the
+            // projection's first two rows again as p = M X + m, and the adjoint through M^T
+            // (camera.py:111-190): dL/dp -> dL/dX -> dL/d(depth); dL/dp (X, 1)^T accumulated for dL/d[R|t]
+            const float4 st = stash[IQ * 64 + lane];
+            const float d = st.z, dw = st.w;
+            const CamPairBwd cams = load_pair_bwd();
+            const Lift l = psfm::lift(cams.Ki, (float)col, (float)qv, d);
             const f2 X0 = bc(l.X0), X1 = bc(l.X1), X2 = bc(l.X2);
+            const f2 p0 = cams.M[0] * X0 + cams.M[1] * X1 + cams.M[2] * X2 + cams.m[0];
+            const f2 p1 = cams.M[3] * X0 + cams.M[4] * X1 + cams.M[5] * X2 + cams.m[1];
+            const f2 iz = f2{fabsf(st.x), fabsf(st.y)};
+            const f2 t = -(gix * p0 + giy * p1) * (iz * iz);
+            f2 gp[3];
+            gp[0] = gix * iz;
+            gp[1] = giy * iz;
+            gp[2] = f2{st.x > 0.0f ? t.x : 0.0f, st.y > 0.0f ? t.y : 0.0f};
+            const f2 gX0 = cams.M[0] * gp[0] + cams.M[3] * gp[1] + cams.M[6] * gp[2];
+            const f2 gX1 = cams.M[1] * gp[0] + cams.M[4] * gp[1] + cams.M[7] * gp[2];
+            const f2 gX2 = cams.M[2] * gp[0] + cams.M[5] * gp[1] + cams.M[8] * gp[2];
+            const f2 gd = gX0 * bc(l.xn0) + gX1 * bc(l.xn1) + gX2 * bc(l.xn2);
+            gs = (NC == 2 ? gd.x + gd.y : gd.x) * dw;
+            // G += dL/dp (X, 1)^T for both contexts: lane-private LDS row, b128 read-modify-write
+            float4* g4 = reinterpret_cast<float4*>(gt);
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 const float4 ta = g4[2 * i], tb = g4[2 * i + 1];
                 f2 e0 = f2{ta.x, ta.y}, e1 = f2{ta.z, ta.w}, e2 = f2{tb.x, tb.y}, e3 = f2{tb.z, tb.w};
-                e0 += gc[i] * X0;
-                e1 += gc[i] * X1;
-                e2 += gc[i] * X2;
-                e3 += gc[i];
+                e0 += gp[i] * X0;
+                e1 += gp[i] * X1;
+                e2 += gp[i] * X2;
+                e3 += gp[i];
                 g4[2 * i] = make_float4(e0.x, e0.y, e1.x, e1.y);
                 g4[2 * i + 1] = make_float4(e2.x, e2.y, e3.x, e3.y);
             }
         } else {
+            float d1, inv;
+            const float d = dc.warp_depth(S.template SG<IQ>(), d1, inv);
+            const float dw = dc.dwarp_ds(d, d1, inv);
             const CM cams = load_cams();
             const Lift l = cams.lift((float)col, (float)qv, d);
             gs = 0.0f;
@@ -759,8 +831,7 @@ struct K12 {
                 }
             }
         }
-        (void)g2;
-        if (cfg.smooth()) gs += (cx * (S.h_p - h_left) + cy * (S.t_p - S.t_pp)) / mc;
+        if (cfg.smooth()) gs += (cx * (S.h_p - h_left) + cy * (S.t_p - S.t_pp)) * rmc;
         gsig[(uint32_t)(qv * W + col)] = gs;
     }
 };
@@ -823,10 +894,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
         float* o = a.ws.pose_part + ((((size_t)K.s * NC + j) * p.B + K.b) * nu + K.unit) * 12;
+        float t[12];
 #pragma unroll
-        for (int mm = 0; mm < 12; ++mm) {
-            const float t = wave_sum64(K.gt[2 * mm + j]);
-            if (threadIdx.x == 0) o[mm] = t;
+        for (int mm = 0; mm < 12; ++mm) t[mm] = wave_sum64(K.gt[2 * mm + j]);
+        if constexpr (K12<NC, FAST, MODEL, RB>::PAIR_CAM) {
+            // dL/d[R|t] row r' = sum_r K_ref[r][r'] G[r] (G = sum dL/dp (X, 1)^T, rows r of p)
+            cf2* rec = reinterpret_cast<cf2*>(reinterpret_cast<uint64_t>(K.campair));
+            float Kr[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Kr[i] = j ? rec[9 + i].y : rec[9 + i].x;
+            float u[12];
+#pragma unroll
+            for (int r2 = 0; r2 < 3; ++r2)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    u[4 * r2 + c] = Kr[r2] * t[c] + Kr[3 + r2] * t[4 + c] + Kr[6 + r2] * t[8 + c];
+#pragma unroll
+            for (int mm = 0; mm < 12; ++mm) t[mm] = u[mm];
+        }
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int mm = 0; mm < 12; ++mm) o[mm] = t[mm];
         }
     }
     k12_stamp(1);

@@ -779,7 +779,7 @@ struct SigSumArgs {
     int shift[MAXS];
     float* part;  // [S][B][SIGCH]
     const float* cam;  // [S][N][B][CAMREC]
-    float* cam_pairs;  // [S][B][CAMREC][2]
+    float* cam_pairs;  // [S][B][fused::PAIR_REC][2]
     int B, W, N, smooth;
     uint32_t plane;
 };
@@ -790,10 +790,20 @@ struct SigSumArgs {
 __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
     __shared__ float red[NWAVE];
     const int ch = blockIdx.x, b = blockIdx.y, s = blockIdx.z;
-    if (ch == 0 && threadIdx.x < 2 * PSFM_CAMREC) {  // K12's context-paired camera record of (s, b)
+    if (ch == 0 && threadIdx.x < 2 * fused::PAIR_REC) {  // K12's context-paired camera record of (s, b)
         const int k = threadIdx.x >> 1, j = min((int)(threadIdx.x & 1), a.N - 1);
-        a.cam_pairs[((size_t)s * a.B + b) * 2 * PSFM_CAMREC + threadIdx.x] =
-            a.cam[(((size_t)s * a.N + j) * a.B + b) * PSFM_CAMREC + k];
+        const float* c = a.cam + (((size_t)s * a.N + j) * a.B + b) * PSFM_CAMREC;
+        float v = 0.0f;
+        if (k < PSFM_CAMREC) {
+            v = c[k];   // Ki | Kr | T | pad
+        } else if (k < 41) {  // M = K_ref R, row-major (fixed-order fp32 fma chain)
+            const int r = (k - 32) / 3, q = (k - 32) % 3;
+            v = fmaf(c[9 + 3 * r + 2], c[18 + 8 + q], fmaf(c[9 + 3 * r + 1], c[18 + 4 + q], c[9 + 3 * r] * c[18 + q]));
+        } else if (k < 44) {  // m = K_ref t
+            const int r = k - 41;
+            v = fmaf(c[9 + 3 * r + 2], c[18 + 11], fmaf(c[9 + 3 * r + 1], c[18 + 7], c[9 + 3 * r] * c[18 + 3]));
+        }
+        a.cam_pairs[((size_t)s * a.B + b) * 2 * fused::PAIR_REC + threadIdx.x] = v;
     }
     if (!a.smooth) return;
     const int sh = pick4(a.shift, s);
@@ -1173,7 +1183,7 @@ int psfm_workspace_floats(const psfm_params* p, size_t* photo, size_t* smooth, s
     if (argmin_bytes) *argmin_bytes = (size_t)p->S * p->B * p->H * p->W;
     if (unwarp) *unwarp = (p->automask && !p->l1_only) ? (size_t)p->N * p->B * p->H * p->W : 0;
     if (sig_part) *sig_part = (size_t)p->S * p->B * fused::SIGCH;
-    if (cam_pairs) *cam_pairs = (size_t)p->S * p->B * PSFM_CAMREC * 2;
+    if (cam_pairs) *cam_pairs = (size_t)p->S * p->B * fused::PAIR_REC * 2;
     return 0;
 }
 

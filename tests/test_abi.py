@@ -70,7 +70,7 @@ def test_workspace_sizes(hip):
     assert n[5].value == 4 * 4 * 192 * 640
     assert n[6].value == 2 * 4 * 192 * 640
     assert n[7].value == 4 * 4 * 16   # sigmoid chunk sums of the K12 pre-pass
-    assert n[8].value == 4 * 4 * 32 * 2   # context-paired camera records (K12)
+    assert n[8].value == 4 * 4 * 48 * 2   # context-paired camera records (K12: + M = K_ref R, m = K_ref t)
 
 
 def test_fused_path_argument_checks(hip):

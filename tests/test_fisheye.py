@@ -55,10 +55,27 @@ def test_fisheye_loss_and_grads_match_reference(dev, tag):
     out, sigs, vec = _run(z, tag, dev)
     assert gu.rel_err(out["loss"].detach().cpu(), z[f"loss{tag}"]) < LOSS_TOL
     assert gu.rel_err(out["metrics"]["smoothness_loss"].cpu(), z[f"smoothness_loss{tag}"]) < LOSS_TOL
-    if tag:   # multi-resolution maps: no exclusions, the reference golden at 1e-3
-        for i, s in enumerate(sigs):
-            ok, msg = gu.grad_check(s.grad.cpu(), z[f"grad_sig{i}{tag}"], None, GRAD_TOL)
+    if tag:
+        # multi-resolution maps (each scale at its own size, the images resized): the reference golden at
+        # 1e-3 per pixel except the fp32-ambiguous ones (oracle.sensitive_pixels evaluated per scale at
+        # its size: bilinear kinks, min near-ties with their 3x3 SSIM window, L1 sign ties) — bounded:
+        # <= 5 % of a scale's pixels flagged, a flagged pixel within 0.15 * max.  (The no-SLP build of
+        # round 6 flips one near-tie at scale 1: candidates 0.448327 / 0.448326, a 1.3e-6 margin;
+        # tools/diag_fisheye_k12planes.py)
+        image, ctx, intr = _T(z[f"image{tag}"]), [_T(z[f"ctx0{tag}"]), _T(z[f"ctx1{tag}"])], _intr(z)
+        sig_c = [_T(z[f"sig{i}{tag}"]) for i in range(4)]
+        pvec = _T(z[f"pvec{tag}"])
+        mats = [O.pose_vec_to_mat(pvec[:, j]) for j in range(2)]
+        sens = O.sensitive_pixels(image, ctx, sig_c, intr, mats, 0.5, 80.0)
+        for i, (s, sm) in enumerate(zip(sigs, sens)):
+            got, ref, flag = s.grad.cpu(), z[f"grad_sig{i}{tag}"], sm.numpy()
+            ok, msg = gu.grad_check(got, ref, flag, GRAD_TOL)
             assert ok, f"dL/dsig{i}: {msg}"
+            ok, msg2 = gu.grad_check(got, ref, None, 0.15)
+            assert ok, f"dL/dsig{i} (flagged pixels, 0.15 * max): {msg2}"
+            assert flag.mean() <= 0.05, f"dL/dsig{i}: {flag.mean():.1%} of the pixels flagged"
+            print(f"fisheye multires dL/dsig{i}: {msg}; {int(flag.sum())} flagged")
+        # the pose gradient sums every pixel: a flipped near-tie moves it by its window's share
         assert gu.rel_err(vec.grad.cpu(), z[f"grad_vec{tag}"]) < GRAD_TOL
         return
     # full-resolution maps: bounded exclusion of the fp32-ambiguous pixels, as the pinhole cases

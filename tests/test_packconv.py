@@ -393,17 +393,21 @@ def test_pack_layer_composed_path_matches_the_round4_path(monkeypatch, C, d, k, 
 
 @pytest.mark.gpu
 def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monkeypatch):
-    """a whole PackNet01 depth net at B = 2, 192 x 640 — where pack1 and pack2
-    take the composed path (asserted: two PackConvFn calls per forward) — under bf16 autocast, against
-    the SAME weights in fp32 with composition off (MIOpen fp32 + the fp32 pack3d kernels: the chain
-    test_packnet_layer_gradients_match_reference_gpu_fp32 pins to the reference).  A fixed linear
-    loss on the four inverse-depth maps; compared: the maps, dL/drgb and the pack1 / pack2 parameter
-    gradients.  The composed network must be as close to fp32 as the round-4 bf16 network (composition
-    off) is: its relative L2 error at most 1.25x the round-4 path's + 2e-3, and the maps within 2e-2."""
+    """a whole PackNet01 depth net whose pack1 and pack2 take the composed path
+    (asserted: two PackConvFn calls per forward) under bf16 autocast, against the SAME weights in
+    fp32 with composition off (MIOpen fp32 + the fp32 pack3d kernels: the chain
+    test_packnet_layer_gradients_match_reference_gpu_fp32 pins to the reference).  B = 2 at the step
+    goldens' 64 x 192 (the MIOpen kernels the network tests already built; the product policy
+    packconv.beneficial composes the C = 64 layers from B (H/2)(W/2) >= 8192 on — B = 2, 192 x 640 and
+    up — and is bypassed here for them, as the module test does).  A fixed linear loss on the four
+    inverse-depth maps; compared: the maps, dL/drgb and the pack1 / pack2 parameter gradients.  The
+    composed network must be as close to fp32 as the round-4 bf16 network (composition off) is: its
+    relative L2 error at most 1.25x the round-4 path's + 2e-3, and the maps within 2e-2."""
     import __graft_entry__
     __graft_entry__.build()
     from packnet_sfm_amd.networks.layers.packnet import packconv
     torch.backends.cudnn.benchmark = False
+    monkeypatch.setattr(packconv, "beneficial", lambda x, C: C <= 64)
     calls = _spy_pack_conv(monkeypatch, packconv)
     import golden_util as gu
     from test_networks import _packnet_model
@@ -411,7 +415,7 @@ def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monk
     depth, _ = _packnet_model()
     depth = depth.to(dev).train()
     g = torch.Generator().manual_seed(11)
-    B, H, W = 2, 192, 640
+    B, H, W = 2, 64, 192
     rgb = gu.smooth_texture(g, B, 3, H, W).to(dev)
     gys = [torch.randn(B, 1, H >> i, W >> i, generator=g).to(dev) for i in range(4)]
     watched = [depth.pack1.conv.conv_base.weight, depth.pack1.conv3d.weight, depth.pack1.conv3d.bias,
@@ -432,9 +436,10 @@ def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monk
             packconv.ENABLED = True
 
     ref = run(False, False)
+    print("fp32 chain done", flush=True)
     assert not calls
     comp = run(True, True)
-    assert len(calls) == 2 and calls[0][1:] == (64, 192, 640) and calls[1][1:] == (64, 96, 320), calls
+    assert len(calls) == 2 and calls[0][1:] == (64, H, W) and calls[1][1:] == (64, H // 2, W // 2), calls
     calls.clear()
     old = run(True, False)
     assert not calls
