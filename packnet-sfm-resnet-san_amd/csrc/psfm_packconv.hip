@@ -13,8 +13,10 @@
 //                      32-channel chunks of the input (per sub-pixel for P) and, per chunk, the KH
 //                      tap rows.  The chunk's halo tile (4 + KH - 1 rows x 64 + KW - 1 columns) and
 //                      each tap row's weights are staged in LDS (double-buffered, the next step's
-//                      global loads in flight during the current step's MFMAs).  Wave w computes
-//                      output row w: 64 pixels x 64 channels = 4 x 4 accumulator tiles.  The
+//                      global loads in flight during the current step's MFMAs; the
+//                      operand fragments of tap column b + 1 read from LDS during column b's
+//                      MFMAs).  Wave w computes output row w, 64 pixels x 64 channels = 4 x 4
+//                      accumulator tiles (two rows per wave measured slower: DESIGN.md).  The
 //                      epilogue goes through LDS so every store is a 16-byte run.  One kernel
 //                      serves the main forward (epilogue: bias table - edge terms -> bf16 y), the
 //                      main backward (dy in, written through the packing permutation into dx, +
@@ -44,6 +46,9 @@ int fail(int code, const std::string& msg) {
 typedef short bf8 __attribute__((ext_vector_type(8)));
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+// staging registers as a native vector (uint4's struct copies became global -> private -> LDS memcpys
+// that SROA left in scratch)
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 enum { OUT_F32 = 0, OUT_Y = 1, OUT_DX = 2 };
 constexpr int MAXPROB = 8;
@@ -124,29 +129,28 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
         pok |= ok ? 1u << u : 0u;
     }
     const uint16_t* wbase = P.w + (size_t)nb * nq * KH * KW * 2048;
-    uint4 preg[NPE], wreg[KW];
     const uint16_t* pbase = inb;   // the current chunk's source (sub-pixel offset + 32-channel block)
 #define PC_LOADP(q_)                                                                                        \
     {                                                                                                       \
         const int sub_ = (q_) / ncc, cc_ = (q_) - sub_ * ncc;                                               \
         pbase = inb + P.in.sub_off[sub_] + cc_ * 32;                                                        \
         _Pragma("unroll") for (int u = 0; u < NPE; ++u) preg[u] =                                           \
-            (pok >> u) & 1u ? *reinterpret_cast<const uint4*>(pbase + poff[u]) : make_uint4(0, 0, 0, 0);   \
+            (pok >> u) & 1u ? *reinterpret_cast<const u4v*>(pbase + poff[u]) : u4v{0u, 0u, 0u, 0u};         \
     }
 #define PC_STOREP(buf_)                                                                                     \
     _Pragma("unroll") for (int u = 0; u < NPE; ++u) {                                                       \
         const int e_ = t + u * 256;                                                                         \
         if (e_ < 4 * HR * HC)                                                                               \
-            *reinterpret_cast<uint4*>(smem + (buf_) * PB + ((e_ & 3) * NP + (e_ >> 2)) * 16) = preg[u];     \
+            *reinterpret_cast<u4v*>(smem + (buf_) * PB + ((e_ & 3) * NP + (e_ >> 2)) * 16) = preg[u];      \
     }
 #define PC_LOADW(s_)                                                                                        \
     {                                                                                                       \
-        const uint4* src_ = reinterpret_cast<const uint4*>(wbase + (size_t)(s_) * KW * 2048) + t;           \
+        const u4v* src_ = reinterpret_cast<const u4v*>(wbase + (size_t)(s_) * KW * 2048) + t;               \
         _Pragma("unroll") for (int u = 0; u < KW; ++u) wreg[u] = src_[u * 256];                             \
     }
 #define PC_STOREW(buf_)                                                                                     \
     {                                                                                                       \
-        uint4* dst_ = reinterpret_cast<uint4*>(smem + 2 * PB + (buf_) * WB) + t;                            \
+        u4v* dst_ = reinterpret_cast<u4v*>(smem + 2 * PB + (buf_) * WB) + t;                                \
         _Pragma("unroll") for (int u = 0; u < KW; ++u) dst_[u * 256] = wreg[u];                             \
     }
 
@@ -156,31 +160,50 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[f][g] = f4{0.f, 0.f, 0.f, 0.f};
 
-    PC_LOADP(0);
-    PC_LOADW(0);
-    PC_STOREP(0);
-    PC_STOREW(0);
+    {
+        u4v preg[NPE], wreg[KW];
+        PC_LOADP(0);
+        PC_LOADW(0);
+        PC_STOREP(0);
+        PC_STOREW(0);
+    }
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
         const int q = s / KH, a = s - q * KH;
-        const bool nxq = s + 1 < nsteps && a == KH - 1;
+        const bool nxq = s + 1 < nsteps && a == KH - 1;   // the chunk's last step: stage the next chunk
+        // staging registers local to the step (loaded at its top, stored at its end): arrays carried
+        // across iterations were demoted to scratch
+        u4v wreg[KW], preg[NPE];
         // the next step's weights (the last step re-loads its own: no branch around the loads)
         PC_LOADW(s + 1 < nsteps ? s + 1 : s);
         if (nxq) PC_LOADP(q + 1);
-        const uint8_t* Pl = smem + (q & 1) * PB + (kq * NP + (wv + a) * HC + l15) * 16;
+        // the loads above go out before the MFMAs (the scheduler otherwise sinks them to their
+        // LDS stores at the end of the step and the step waits out their whole latency)
+        __builtin_amdgcn_sched_barrier(0);
         const uint8_t* Wl = smem + 2 * PB + (s & 1) * WB + (kq * 64 + l15) * 16;
+        const uint8_t* Pl0 = smem + (q & 1) * PB + (kq * NP + (wv + a) * HC + l15) * 16;
+        // operand fragments double-buffered in registers: tap column b + 1's reads are in flight while
+        // b's MFMAs run (one wave per SIMD: nothing else hides the LDS latency)
+        bf8 Bf[2][4], Af[2][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Bf[0][g] = *reinterpret_cast<const bf8*>(Wl + (16 * g) * 16);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) Af[0][f] = *reinterpret_cast<const bf8*>(Pl0 + (16 * f) * 16);
 #pragma unroll
         for (int b = 0; b < KW; ++b) {
-            bf8 Af[4], Bf[4];
+            const int u = b & 1;
+            if (b + 1 < KW) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) Bf[g] = *reinterpret_cast<const bf8*>(Wl + (b * 256 + 16 * g) * 16);
+                for (int g = 0; g < 4; ++g) Bf[u ^ 1][g] = *reinterpret_cast<const bf8*>(Wl + ((b + 1) * 256 + 16 * g) * 16);
 #pragma unroll
-            for (int f = 0; f < 4; ++f) Af[f] = *reinterpret_cast<const bf8*>(Pl + (16 * f + b) * 16);
+                for (int f = 0; f < 4; ++f) Af[u ^ 1][f] = *reinterpret_cast<const bf8*>(Pl0 + (16 * f + b + 1) * 16);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep b + 1's reads ahead of b's MFMAs
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[f], Bf[g], acc[f][g], 0, 0, 0);
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[u][f], Bf[u][g], acc[f][g], 0, 0, 0);
         }
         PC_STOREW((s + 1) & 1);
         if (nxq) PC_STOREP((q + 1) & 1);
@@ -191,18 +214,21 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
 #undef PC_LOADW
 #undef PC_STOREW
 
-    // epilogue: accumulators -> LDS [wave][px][n] (row stride 68 floats) -> 8-channel runs
-    float* ep = reinterpret_cast<float*>(smem) + wv * 64 * 68;
+    // epilogue: accumulators -> LDS [wave][row][px][n] (row stride 68 floats) -> 8-channel runs
+    {
+        float* ep = reinterpret_cast<float*>(smem) + wv * 64 * 68;
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+        for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+            for (int g = 0; g < 4; ++g)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ep[(16 * f + 4 * kq + r) * 68 + 16 * g + l15] = acc[f][g][r];
+                for (int r = 0; r < 4; ++r) ep[(16 * f + 4 * kq + r) * 68 + 16 * g + l15] = acc[f][g][r];
+    }
     __syncthreads();
     const int Y = r0 + wv;
     if (Y >= P.rows) return;
-#pragma unroll 2
+    const float* ep = reinterpret_cast<const float*>(smem) + wv * 64 * 68;
+#pragma unroll 1
     for (int i = 0; i < 8; ++i) {
         const int item = lane + 64 * i, px = item >> 3, n0 = (item & 7) * 8, X = c0 + px;
         if (X >= P.cols) continue;
@@ -309,26 +335,50 @@ __global__ __launch_bounds__(256, 2) void k_pc_wgrad(const WArgs A) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int ncc = P.in.cin >> 5, nq = P.in.nsub * ncc;
 
+    // staging loads: unconditional, from the tile's own address or (out of range) from the image
+    // base, the zero selected at the LDS store — a load under a lane-divergent branch made the
+    // wait-count pass drain every earlier load before the next one (vmcnt(0) between the loads)
     uint4 greg[NGE], ireg[NIE];
+    uint32_t gok = 0u, iok = 0u;
+    // block-independent parts of this thread's staging entries, once: the channel offset of each IN
+    // entry (sub-pixel plane + 32-channel chunk: a per-lane index into sub_off, selected here rather
+    // than per load) and which entries exist
+    int64_t ich[NIE];
+    uint32_t iq_ok = 0u, g_ok = 0u;
+#pragma unroll
+    for (int u = 0; u < NIE; ++u) {
+        const int e = t + u * 256, ch = e & 7, q = kb * 2 + (ch >> 2);
+        const int sub = q / ncc, cc = q - sub * ncc;
+        const int64_t so = sub == 0 ? P.in.sub_off[0] : sub == 1 ? P.in.sub_off[1] : sub == 2 ? P.in.sub_off[2]
+                                                                                                 : P.in.sub_off[3];
+        ich[u] = so + cc * 32 + (ch & 3) * 8;
+        iq_ok |= (e < HC * 8 && q < nq) ? 1u << u : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < NGE; ++u) g_ok |= (mb * 64 + ((t + u * 256) & 7) * 8 < P.gc) ? 1u << u : 0u;
     auto load = [&](int bi) {
         const int cb = bi % ncb, rr = bi / ncb, r = rr % P.rows, o = rr / P.rows, c0 = cb * TX;
+        const uint16_t* gb = P.g + o * P.g_outer;
+        gok = 0u;
 #pragma unroll
         for (int u = 0; u < NGE; ++u) {
             const int e = t + u * 256, px = e >> 3, ch = e & 7;
-            const bool ok = c0 + px < P.cols && mb * 64 + ch * 8 < P.gc;
-            greg[u] = ok ? *reinterpret_cast<const uint4*>(P.g + o * P.g_outer + r * P.g_row + (c0 + px) * P.g_col +
-                                                           mb * 64 + ch * 8)
-                         : make_uint4(0, 0, 0, 0);
+            const bool ok = ((g_ok >> u) & 1u) && c0 + px < P.cols;
+            const int64_t off = ok ? r * P.g_row + (c0 + px) * P.g_col + mb * 64 + ch * 8 : 0;
+            greg[u] = *reinterpret_cast<const uint4*>(gb + off);
+            gok |= ok ? 1u << u : 0u;
         }
         const int ir = r + a - P.ph;
+        const bool row_ok = ir >= 0 && ir < P.in.rin;   // wave-uniform
+        const uint16_t* ib = P.in.p + o * P.in.s_outer + (row_ok ? ir : 0) * P.in.s_row;
+        iok = 0u;
 #pragma unroll
         for (int u = 0; u < NIE; ++u) {
-            const int e = t + u * 256, px = e >> 3, ch = e & 7, q = kb * 2 + (ch >> 2), ic = c0 + px - P.pw;
-            const int sub = q / ncc, cc = q - sub * ncc;
-            const bool ok = e < HC * 8 && q < nq && ir >= 0 && ir < P.in.rin && ic >= 0 && ic < P.in.cols_in;
-            ireg[u] = ok ? *reinterpret_cast<const uint4*>(P.in.p + o * P.in.s_outer + ir * P.in.s_row + ic * P.in.s_col +
-                                                           P.in.sub_off[sub] + cc * 32 + (ch & 3) * 8)
-                         : make_uint4(0, 0, 0, 0);
+            const int e = t + u * 256, px = e >> 3, ic = c0 + px - P.pw;
+            const bool ok = row_ok && ((iq_ok >> u) & 1u) && ic >= 0 && ic < P.in.cols_in;
+            const int64_t off = ok ? ic * P.in.s_col + ich[u] : 0;
+            ireg[u] = *reinterpret_cast<const uint4*>(ib + off);
+            iok |= ok ? 1u << u : 0u;
         }
     };
     auto store = [&](int buf) {
@@ -337,12 +387,17 @@ __global__ __launch_bounds__(256, 2) void k_pc_wgrad(const WArgs A) {
 #pragma unroll
         for (int u = 0; u < NGE; ++u) {
             const int e = t + u * 256, px = e >> 3, ch = e & 7;
-            *reinterpret_cast<uint4*>(gs + px * 128 + ((ch ^ wswz(px)) << 4)) = greg[u];
+            const uint32_t m = (gok >> u) & 1u ? 0xffffffffu : 0u;   // a value mask, not a select of two arrays
+            *reinterpret_cast<uint4*>(gs + px * 128 + ((ch ^ wswz(px)) << 4)) =
+                make_uint4(greg[u].x & m, greg[u].y & m, greg[u].z & m, greg[u].w & m);
         }
 #pragma unroll
         for (int u = 0; u < NIE; ++u) {
             const int e = t + u * 256, px = e >> 3, ch = e & 7;
-            if (e < HC * 8) *reinterpret_cast<uint4*>(is + px * 128 + ((ch ^ wswz(px)) << 4)) = ireg[u];
+            const uint32_t m = (iok >> u) & 1u ? 0xffffffffu : 0u;
+            if (e < HC * 8)
+                *reinterpret_cast<uint4*>(is + px * 128 + ((ch ^ wswz(px)) << 4)) =
+                    make_uint4(ireg[u].x & m, ireg[u].y & m, ireg[u].z & m, ireg[u].w & m);
         }
     };
 
@@ -364,6 +419,7 @@ __global__ __launch_bounds__(256, 2) void k_pc_wgrad(const WArgs A) {
         const int buf = (bi - bi0) & 1;
         const bool nx = bi + 1 < bi1;
         if (nx) load(bi + 1);
+        __builtin_amdgcn_sched_barrier(0);   // the next block's loads go out before this block's MFMAs
         uint8_t* gs = smem + buf * (GB + IB);
         uint8_t* is = gs + GB;
 #pragma unroll
@@ -1093,7 +1149,8 @@ template <int KH, int KW>
 void launch_conv(const ConvArgs& A, int rows_max, int cols_max, int cop_max, hipStream_t st) {
     ConvArgs a = A;
     a.ntc = (cols_max + 63) / 64;
-    const dim3 grid((unsigned)(((rows_max + 3) / 4) * a.ntc), (unsigned)(cop_max / 64), (unsigned)(a.nprob * a.outer_max));
+    const dim3 grid((unsigned)(((rows_max + 3) / 4) * a.ntc), (unsigned)(cop_max / 64),
+                    (unsigned)(a.nprob * a.outer_max));
     hipLaunchKernelGGL((k_pc_conv<KH, KW>), grid, dim3(256), 0, st, a);
 }
 
