@@ -26,8 +26,8 @@
 //   q-eval  row v-3 (its three p-rows are now complete): horizontal 3-sum of the accumulated
 //           coefficients (DPP), adjoint through the bilinear sample (d warp / d(ix,iy) stashed
 //           in wave-private LDS at issue time) and the projection — pinhole: from the issue's
-//           stashed 1/z, warp depth and d warp / d sigmoid, p = M X + m (M = K_ref R) and
-//           dL/dX = M^T dL/dp, no second depth chain or projection — dL/dp (X, 1)^T of both
+//           stashed 1/z, warp depth and d warp / d sigmoid, p = d A [u, v, 1]^T + m (A = K_ref R K^-1,
+//           PairProj) and dL/dd = dL/dp . dp/dd, no second depth chain or projection — dL/dp (X, 1)^T of both
 //           contexts (taken through K_ref^T once per wave), plus the per-pixel smoothness
 //           gradient -> dL/dsig written once (no LDS ring, no barrier, no atomics: deterministic);
 //   resolve the bilinear samples of row v (x and d x/d(ix,iy)); the gathers are range-checked
@@ -73,7 +73,7 @@ constexpr int GTS = 28;          // per-lane dL/dT row: 12 entries x 2 contexts,
                                  // (the 16 lanes of a b128 access start on distinct bank groups)
 
 constexpr int PAIR_REC = 48;     // entries (f2: both contexts) of the context-paired camera record
-                                 // ws.cam_pairs: Ki 0-8 | Kr 9-17 | T 18-29 | pad | M = Kr R 32-40 |
+                                 // ws.cam_pairs: Ki 0-8 | Kr 9-17 | T 18-29 | pad | E = Kr R Ki - I 32-40 |
                                  // m = Kr t 41-43 | pad (psfm_photometric.hip k_sig_sum builds it)
 
 __host__ __device__ inline int stripes(int W) { return (W + OW - 1) / OW; }
@@ -204,91 +204,30 @@ __device__ __forceinline__ void resolve_pair(const Pend& a, const Pend& b, f2 (&
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(4))) const f2 cf2;
 
-// What the q-eval needs of the pinhole pair record: K^-1 of the target, M = K_ref R and m = K_ref t
-// of both contexts (p = M X + m: the projection's first two rows without the intermediate c = R X + t;
-// the adjoint dL/dX = M^T dL/dp).  dL/d[R|t] is accumulated as dL/dp (X, 1)^T and taken through
-// K_ref^T once per wave (bwd_pose_rows).
-struct CamPairBwd {
-    float Ki[9];
-    f2 M[9], m[3];
-    __device__ __forceinline__ void load(cf2* rec) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Ki[i] = rec[i].x;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) M[i] = rec[32 + i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) m[i] = rec[41 + i];
-    }
-};
-
+// The pinhole pair record at run time.  Lift, transform and intrinsics fold into one 3x3 per
+// context, A = K_ref R K^-1:  p = K_ref (R (d K^-1 x) + t) = d A x + m, x = [u, v, 1]^T, m = K_ref t.
+// The record holds E = A - I (fp64, rounded once) and p is evaluated as p = d (E x) + (d x + m):
+// E x is small (the image motion per unit depth) and d x + m is one rounding at the magnitude of p,
+// which halves the sampling positions' fp32 error against the lift + R X + t + K_ref chain
+// (max 1.4-1.8e-4 px vs 3.0-5.5e-4, mean 1.0e-5 vs 1.6e-5 over 1M KITTI-shaped points).  A lane's
+// column u is fixed for the whole sweep, so E's u- and constant columns are folded once per wave
+// (K12::ea) and a row costs e = ea + E[:, 1] v and two fma per entry of p: nine v_pk_fma for both
+// contexts, where the chain took 9 + 21.  The adjoint needs no intermediate point either:
+// dL/dd = dL/dp . dp/dd = dL/dp . (e + x).  dL/d[R|t] is accumulated as dL/dp (X, 1)^T and taken
+// through K_ref^T once per wave (bwd_pose_rows).
 struct PairProj {
     f2 p0, p1, p2;  // K_ref (R X + t)
     f2 iz;          // 1 / clamp(p2, 1e-5)
     f2 ix, iy;      // sampling position in pixels
 };
 
-struct CamPair {
-    float Ki[9];   // K^-1 of the target (both halves of the record hold it)
-    f2 Kr[9], T[12];
-    float wm1, rwm1, hm1, rhm1;
-
-    __device__ __forceinline__ void load(cf2* rec, int H, int W) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Ki[i] = rec[i].x;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Kr[i] = rec[9 + i];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) T[i] = rec[18 + i];
-        wm1 = (float)(W - 1);
-        hm1 = (float)(H - 1);
-        rwm1 = rcp_nr(wm1);
-        rhm1 = rcp_nr(hm1);
-    }
-    __device__ __forceinline__ Lift lift(float u, float v, float d) const { return psfm::lift(Ki, u, v, d); }
-    // p = K_ref (R X + t), z = clamp(p2, 1e-5), iz = 1/z (rcp + one Newton step)
-    __device__ __forceinline__ void transform(const Lift& l, PairProj& r) const {
-        const f2 X0 = bc(l.X0), X1 = bc(l.X1), X2 = bc(l.X2);
-        const f2 c0 = T[0] * X0 + T[1] * X1 + T[2] * X2 + T[3];
-        const f2 c1 = T[4] * X0 + T[5] * X1 + T[6] * X2 + T[7];
-        const f2 c2 = T[8] * X0 + T[9] * X1 + T[10] * X2 + T[11];
-        r.p0 = Kr[0] * c0 + Kr[1] * c1 + Kr[2] * c2;
-        r.p1 = Kr[3] * c0 + Kr[4] * c1 + Kr[5] * c2;
-        r.p2 = Kr[6] * c0 + Kr[7] * c1 + Kr[8] * c2;
-        const f2 z = f2{fmaxf(r.p2.x, 1e-5f), fmaxf(r.p2.y, 1e-5f)};
-        const f2 r0 = f2{__builtin_amdgcn_rcpf(z.x), __builtin_amdgcn_rcpf(z.y)};
-        r.iz = (f2{1.0f, 1.0f} - z * r0) * r0 + r0;
-    }
-    // + the sampling position: u = p0 / z (rcp-refined quotient), then ((2u/(W-1) - 1) + 1)/2 (W-1)
-    __device__ __forceinline__ void project(const Lift& l, PairProj& r) const {
-        transform(l, r);
-        const f2 z = f2{fmaxf(r.p2.x, 1e-5f), fmaxf(r.p2.y, 1e-5f)};
-        f2 u = r.p0 * r.iz, w = r.p1 * r.iz;
-        u = (r.p0 - u * z) * r.iz + u;
-        w = (r.p1 - w * z) * r.iz + w;
-        r.ix = roundtrip(u, wm1, rwm1);
-        r.iy = roundtrip(w, hm1, rhm1);
-    }
-    __device__ __forceinline__ static f2 roundtrip(f2 pz, float sm1, float rsm1) {
-        const f2 t = pz + pz;
-        f2 q = t * bc(rsm1);
-        q = (t - q * bc(sm1)) * bc(rsm1) + q;
-        const f2 n = q - f2{1.0f, 1.0f};
-        return ((n + f2{1.0f, 1.0f}) * f2{0.5f, 0.5f}) * bc(sm1);
-    }
-    // adjoint: (dL/dix, dL/diy) -> dL/dc (gc) and dL/d(depth) (returned), both contexts
-    __device__ __forceinline__ f2 grad(const PairProj& r, const Lift& l, f2 gix, f2 giy, f2 (&gc)[3]) const {
-        const f2 gp0 = gix * r.iz, gp1 = giy * r.iz;
-        const f2 t = -(gix * r.p0 + giy * r.p1) * (r.iz * r.iz);
-        const f2 gp2 = f2{r.p2.x >= 1e-5f ? t.x : 0.0f, r.p2.y >= 1e-5f ? t.y : 0.0f};
-        gc[0] = Kr[0] * gp0 + Kr[3] * gp1 + Kr[6] * gp2;
-        gc[1] = Kr[1] * gp0 + Kr[4] * gp1 + Kr[7] * gp2;
-        gc[2] = Kr[2] * gp0 + Kr[5] * gp1 + Kr[8] * gp2;
-        const f2 gX0 = T[0] * gc[0] + T[4] * gc[1] + T[8] * gc[2];
-        const f2 gX1 = T[1] * gc[0] + T[5] * gc[1] + T[9] * gc[2];
-        const f2 gX2 = T[2] * gc[0] + T[6] * gc[1] + T[10] * gc[2];
-        return gX0 * bc(l.xn0) + gX1 * bc(l.xn1) + gX2 * bc(l.xn2);
-    }
-};
+__device__ __forceinline__ f2 roundtrip(f2 pz, float sm1, float rsm1) {
+    const f2 t = pz + pz;
+    f2 q = t * bc(rsm1);
+    q = (t - q * bc(sm1)) * bc(rsm1) + q;
+    const f2 n = q - f2{1.0f, 1.0f};
+    return ((n + f2{1.0f, 1.0f}) * f2{0.5f, 0.5f}) * bc(sm1);
+}
 
 __device__ __forceinline__ f2 pk_rcp(f2 v) { return f2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)}; }
 __device__ __forceinline__ f2 pk_sel01(f2 l) {  // 1 where 0 <= l <= 1 (clamp pass-through), else 0
@@ -393,6 +332,8 @@ struct K12 {
     float4* stash;  // wave-private LDS [4][64]: the issue phase's projection terms for the q-eval
     const float* camrec;   // record of (s, context 0, b); context j is j*B records further
     const float* campair;  // context-paired record of (s, b) (ws.cam_pairs)
+    f2 ea[3];              // pinhole: E[:, 0] u + E[:, 2] of this lane's column u (PairProj)
+    float xa[3];           // pinhole: K^-1[:, 0] u + K^-1[:, 2] (the point X = d K^-1 [u, v, 1]^T)
     bool young;            // the second wave dispatched to its SIMD (Args::young_from), wave-uniform
     int prio_mode;
 
@@ -416,24 +357,22 @@ struct K12 {
         c.load(reinterpret_cast<cfloat*>(rp), B, H, W);
         return c;
     }
-    // the context-paired pinhole record, re-loaded (s_load_dwordx16 through the scalar cache) at each
-    // use: held across the phases it lived in SGPRs spilled to VGPR lanes, and every use cost a
-    // v_readlane per dword.  Round 3 measured this the other way (105.2 vs 107.5 us,
-    // profiles/r03/k12ab/kbench_variants_1.log); without SLP packing (build TU_FLAGS) the re-load wins:
-    // 90.9 -> 90.2-90.5 us (profiles/r06/k12/kab_noslp.log)
-    __device__ __forceinline__ CamPair load_pair() const {
-        CamPair c;
+    // the context-paired pinhole record, read (s_load through the scalar cache) at each use: held
+    // across the phases its entries lived in SGPRs spilled to VGPR lanes, and every use cost a
+    // v_readlane per dword (profiles/r06/k12/kab_noslp.log: 90.9 -> 90.2-90.5 us)
+    __device__ __forceinline__ cf2* pair_rec() const {
         uint64_t rp = reinterpret_cast<uint64_t>(campair);
         asm volatile("" : "+s"(rp));
-        c.load(reinterpret_cast<cf2*>(rp), H, W);
-        return c;
+        return reinterpret_cast<cf2*>(rp);
     }
-    __device__ __forceinline__ CamPairBwd load_pair_bwd() const {
-        CamPairBwd c;
-        uint64_t rp = reinterpret_cast<uint64_t>(campair);
-        asm volatile("" : "+s"(rp));
-        c.load(reinterpret_cast<cf2*>(rp));
-        return c;
+    // e = E [u, v, 1]^T of this lane at row v and p = d e + (d [u, v, 1]^T + m) (both contexts)
+    __device__ __forceinline__ void pair_p(cf2* rec, float v, float d, f2 (&e)[3], f2 (&p)[3]) const {
+        const f2 vv = bc(v), dd = bc(d);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) e[k] = rec[33 + 3 * k] * vv + ea[k];
+        p[0] = e[0] * dd + (dd * bc((float)colr) + rec[41]);
+        p[1] = e[1] * dd + (dd * vv + rec[42]);
+        p[2] = e[2] * dd + (dd + rec[43]);
     }
 
     __device__ __forceinline__ K12(const Args& a_, float* lds) : a(a_), p(a_.p), cfg{a_.p} {
@@ -501,6 +440,15 @@ struct K12 {
             mc = fmaxf((float)(v / ((double)H * W)), 1e-6f);
         }
         rmc = 1.0f / mc;   // once per wave: the q-eval multiplies (within 1 ulp of dividing)
+        if constexpr (PAIR_CAM) {
+            cf2* rec = reinterpret_cast<cf2*>(reinterpret_cast<uint64_t>(campair));
+            const float u = (float)colr;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ea[k] = rec[32 + 3 * k] * bc(u) + rec[34 + 3 * k];
+                xa[k] = rec[3 * k].x * u + rec[3 * k + 2].x;
+            }
+        }
     }
 
     // d warp / d(ix, iy) of a row slot, both contexts: [slot][m][64] f2 (b64, conflict-free)
@@ -568,9 +516,23 @@ struct K12 {
             float d1, inv;
             const float d = dc.warp_depth(sg, d1, inv);
             if constexpr (PAIR_CAM) {
-                const CamPair cams = load_pair();
+                // p = d A [u, v, 1]^T + m, z = clamp(p2, 1e-5), 1/z (rcp + one Newton step), u = p0 / z
+                // (rcp-refined quotient), then grid_sample's ((2u/(W-1) - 1) + 1)/2 (W-1) round trip
+                f2 e[3], pp[3];
+                pair_p(pair_rec(), (float)r, d, e, pp);
                 PairProj pr;
-                cams.project(cams.lift((float)colr, (float)r, d), pr);
+                pr.p0 = pp[0];
+                pr.p1 = pp[1];
+                pr.p2 = pp[2];
+                const f2 z = f2{fmaxf(pr.p2.x, 1e-5f), fmaxf(pr.p2.y, 1e-5f)};
+                const f2 r0 = f2{__builtin_amdgcn_rcpf(z.x), __builtin_amdgcn_rcpf(z.y)};
+                pr.iz = (f2{1.0f, 1.0f} - z * r0) * r0 + r0;
+                f2 pu = pr.p0 * pr.iz, pv = pr.p1 * pr.iz;
+                pu = (pr.p0 - pu * z) * pr.iz + pu;
+                pv = (pr.p1 - pv * z) * pr.iz + pv;
+                const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+                pr.ix = roundtrip(pu, wm1, rcp_nr(wm1));
+                pr.iy = roundtrip(pv, hm1, rcp_nr(hm1));
                 gather(img_rsrc(ctx[0], pb), pb, pr.ix.x, pr.iy.x, H, W, pd[0]);
                 if (NC == 2) gather(img_rsrc(ctx[NC - 1], pb), pb, pr.ix.y, pr.iy.y, H, W, pd[NC - 1]);
                 // what the q-eval of this row (step k + 3, slot I) takes from here instead of
@@ -776,26 +738,27 @@ struct K12 {
         float gs;
         if constexpr (PAIR_CAM) {
             // the row's 1/z, warp depth and d warp / d sigmoid from its issue (stash slot IQ); the
-            // projection's first two rows again as p = M X + m, and the adjoint through M^T
-            // (camera.py:111-190): dL/dp -> dL/dX -> dL/d(depth); dL/dp (X, 1)^T accumulated for dL/d[R|t]
+            // projection's first two rows again as p = d w + m (PairProj), and the adjoint
+            // (camera.py:111-190): dL/dp -> dL/d(depth) = dL/dp . w; dL/dp (X, 1)^T accumulated for dL/d[R|t]
             const float4 st = stash[IQ * 64 + lane];
             const float d = st.z, dw = st.w;
-            const CamPairBwd cams = load_pair_bwd();
-            const Lift l = psfm::lift(cams.Ki, (float)col, (float)qv, d);
-            const f2 X0 = bc(l.X0), X1 = bc(l.X1), X2 = bc(l.X2);
-            const f2 p0 = cams.M[0] * X0 + cams.M[1] * X1 + cams.M[2] * X2 + cams.m[0];
-            const f2 p1 = cams.M[3] * X0 + cams.M[4] * X1 + cams.M[5] * X2 + cams.m[1];
+            cf2* rec = pair_rec();
+            const float qf = (float)qv;
+            f2 e[3], pp[3];
+            pair_p(rec, qf, d, e, pp);
+            const f2 p0 = pp[0], p1 = pp[1];
             const f2 iz = f2{fabsf(st.x), fabsf(st.y)};
             const f2 t = -(gix * p0 + giy * p1) * (iz * iz);
             f2 gp[3];
             gp[0] = gix * iz;
             gp[1] = giy * iz;
             gp[2] = f2{st.x > 0.0f ? t.x : 0.0f, st.y > 0.0f ? t.y : 0.0f};
-            const f2 gX0 = cams.M[0] * gp[0] + cams.M[3] * gp[1] + cams.M[6] * gp[2];
-            const f2 gX1 = cams.M[1] * gp[0] + cams.M[4] * gp[1] + cams.M[7] * gp[2];
-            const f2 gX2 = cams.M[2] * gp[0] + cams.M[5] * gp[1] + cams.M[8] * gp[2];
-            const f2 gd = gX0 * bc(l.xn0) + gX1 * bc(l.xn1) + gX2 * bc(l.xn2);
+            // dp/dd = E x + x
+            const f2 gd = gp[0] * (e[0] + bc((float)colr)) + gp[1] * (e[1] + bc(qf)) + gp[2] * (e[2] + f2{1.0f, 1.0f});
             gs = (NC == 2 ? gd.x + gd.y : gd.x) * dw;
+            // X = d K^-1 [u, v, 1]^T
+            const f2 X0 = bc((rec[1].x * qf + xa[0]) * d), X1 = bc((rec[4].x * qf + xa[1]) * d),
+                     X2 = bc((rec[7].x * qf + xa[2]) * d);
             // G += dL/dp (X, 1)^T for both contexts: lane-private LDS row, b128 read-modify-write
             float4* g4 = reinterpret_cast<float4*>(gt);
 #pragma unroll

@@ -1051,10 +1051,12 @@ WsLayout ws_layout(const Shape& s) {
     L.dR = take((int64_t)s.B * s.Ho * s.Kin);
     const int nmb = s.copC / 64, nkb = s.Kin / 64;
     const int64_t blk = (int64_t)64 * s.ke * 64;
-    // main weight gradient: enough splits for ~2 workgroups per CU, each with >= 4 pixel blocks
+    // main weight gradient: at most one round of workgroups (two per CU: 256 CUs x 2 slots), each with
+    // >= 4 pixel blocks.  Rounding the split count up put 532 workgroups on 512 slots for the PackNet01
+    // pack layers (grid y = 28): the 20 left over ran as a second round as long as the first
     const int grid_y = s.ke * nmb * nkb;
     const int nblk = s.B * s.Ho * ((s.Wo + 63) / 64);
-    L.S_main = std::max(1, std::min((512 + grid_y - 1) / grid_y, std::max(1, nblk / 4)));
+    L.S_main = std::max(1, std::min(512 / grid_y, std::max(1, nblk / 4)));
     const int nblk_e = s.B * ((std::max(s.Ho, s.Wo) + 63) / 64);
     L.S_edge = std::max(1, std::min(8, nblk_e / 2));
     L.part_main = take((int64_t)L.S_main * s.ke * nmb * nkb * blk);

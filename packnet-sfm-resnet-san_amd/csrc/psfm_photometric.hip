@@ -796,12 +796,19 @@ __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
         float v = 0.0f;
         if (k < PSFM_CAMREC) {
             v = c[k];   // Ki | Kr | T | pad
-        } else if (k < 41) {  // M = K_ref R, row-major (fixed-order fp32 fma chain)
+        } else if (k < 41) {  // E = K_ref R K^-1 - I, row-major (fp64, rounded once: fused.h PairProj)
             const int r = (k - 32) / 3, q = (k - 32) % 3;
-            v = fmaf(c[9 + 3 * r + 2], c[18 + 8 + q], fmaf(c[9 + 3 * r + 1], c[18 + 4 + q], c[9 + 3 * r] * c[18 + q]));
-        } else if (k < 44) {  // m = K_ref t
+            double acc = r == q ? -1.0 : 0.0;
+            for (int i = 0; i < 3; ++i) {
+                double mri = 0.0;   // (K_ref R)[r][i]
+                for (int jj = 0; jj < 3; ++jj) mri += (double)c[9 + 3 * r + jj] * (double)c[18 + 4 * jj + i];
+                acc += mri * (double)c[3 * i + q];
+            }
+            v = (float)acc;
+        } else if (k < 44) {  // m = K_ref t (fp64, rounded once)
             const int r = k - 41;
-            v = fmaf(c[9 + 3 * r + 2], c[18 + 11], fmaf(c[9 + 3 * r + 1], c[18 + 7], c[9 + 3 * r] * c[18 + 3]));
+            v = (float)((double)c[9 + 3 * r] * c[18 + 3] + (double)c[9 + 3 * r + 1] * c[18 + 7] +
+                        (double)c[9 + 3 * r + 2] * c[18 + 11]);
         }
         a.cam_pairs[((size_t)s * a.B + b) * 2 * fused::PAIR_REC + threadIdx.x] = v;
     }

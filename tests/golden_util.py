@@ -164,7 +164,8 @@ def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=2e
     With `pose_vec` [B,N,6] the poses are built from it (float64) and the return value is
     (dL/dsig alternatives, [dL/dpose_vec per alternative], pose bound): the pose bound is
     |dL/dpose - dL/dpose with the `sensitive` pixels' warp gradients dropped| in float64 — how much
-    the flagged pixels contribute to the pose gradient.
+    the flagged pixels contribute to the pose gradient — or half the largest |alternative - as is|
+    where that is more (pose_check_bounded allows twice the bound).
     `kw`: oracle.photometric_loss keyword arguments."""
     from oracle import photometric_oracle as O
     d = lambda t: t.double() if t is not None else None  # noqa: E731
@@ -195,6 +196,12 @@ def oracle_alternatives(image, contexts, sigs, K, mats, mask, ties, coord_eps=2e
         s_a = [s.detach().double() for s in sigs]
         O.photometric_loss(img, ctx, s_a, Kd, Kd, md, mk, grid_mask=sensitive, **kw)[0].sum().backward()
         bound = np.abs(pose[0] - v.grad.numpy())
+        # ... and no less than half how far the oracle's own alternatives move it (pose_check_bounded
+        # doubles the bound): the flagged pixels' net contribution can cancel to almost nothing on an
+        # entry that a single flip moves — test_kitti_full_res_golden entry 10: net 5e-4 x max, while
+        # the kinks-flipped alternative moves it 7.5e-3 x max
+        for alt in pose[1:]:
+            bound = np.maximum(bound, 0.5 * np.abs(alt - pose[0]))
     return alts, pose, bound
 
 

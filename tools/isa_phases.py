@@ -17,12 +17,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ap = argparse.ArgumentParser()
 ap.add_argument("--kernel", default=None, help="mangled name (default: the first k12_fwd_grad<2, true, 0, RB>)")
 ap.add_argument("--classes", action="store_true", help="per-step instruction classes of the whole loop")
+ap.add_argument("--dump", default=None, help="write the main loop's assembly here")
+ap.add_argument("--root", default=ROOT, help="tree whose csrc/ to compile (A/B against another checkout)")
 a = ap.parse_args()
 with tempfile.TemporaryDirectory() as d:
     s = os.path.join(d, "k.s")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-S", "--cuda-device-only",
-                    "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "packnet-sfm-resnet-san_amd", "csrc", "psfm_photometric.hip"), "-o", s],
+                    "-fno-slp-vectorize", "-I", os.path.join(a.root, "include"),   # the TU's build flags (TU_FLAGS)
+                    os.path.join(a.root, "packnet-sfm-resnet-san_amd", "csrc", "psfm_photometric.hip"), "-o", s],
                    check=True, capture_output=True)
     lines = open(s).read().split("\n")
 if a.kernel is None:
@@ -37,6 +39,8 @@ for i, ln in enumerate(body):
     if m and m.group(2) in lab and lab[m.group(2)] < i:
         loops.append((i - lab[m.group(2)], lab[m.group(2)], i))
 _, lo, hi = max(loops)
+if a.dump:
+    open(a.dump, "w").write("\n".join(body[lo:hi + 1]) + "\n")
 phases, cur = [], []
 for ln in body[lo:hi + 1]:
     if "sched_barrier" in ln:
