@@ -568,6 +568,8 @@ def roofline(args, ktimes, instep=None):
                  "simd_floor_us_2cyc": round(t2, 2), "lone_wave_floor_us_4cyc": round(t4, 2),
                  "note": "VALU instructions x 2 (or 4) cycles / 1024 SIMDs / 2.4 GHz: the launch's VALU issue time "
                          "at perfect 2-wave interleave (or one wave per SIMD); compare dominant_us_per_launch"}
+            # the kernel's distance from its own VALU issue floor (2-wave interleave): 1.0 = VALU-issue bound
+            v["valu_floor_us_over_dominant_us"] = round(t2 / dom_us, 3)
             if k.get("SQ_WAVE_CYCLES"):
                 v["wave_valu_frac"] = round(k["SQ_ACTIVE_INST_VALU"] / k["SQ_WAVE_CYCLES"], 3)
                 if k.get("SQ_WAIT_ANY") is not None:

@@ -89,6 +89,8 @@ struct ConvProb {
 struct ConvArgs {
     ConvProb p[4];
     int nprob, outer_max, ntc;
+    int nbw;   // 64-channel output tiles per workgroup (launch_conv: > 1 only when every problem's input
+               // chunks fit the two P buffers, so the staged tile serves all of them)
 };
 
 __device__ __forceinline__ int row_class(int y, int n, int pk) {
@@ -103,15 +105,16 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
     constexpr int PB = 4 * NP * 16;                   // one P buffer [kq][pix][8 bf16]
     constexpr int WB = KW * 4 * 64 * 16;              // one weight buffer [b][kq][n][8 bf16]
     constexpr int NPE = (4 * HR * HC + 255) / 256;    // P staging entries per thread
-    constexpr int EPB = 4 * 64 * 68 * 4;              // epilogue tile [wave][px][68 floats]
-    constexpr int SMEM = 2 * PB + 2 * WB > EPB ? 2 * PB + 2 * WB : EPB;
+    constexpr int EPB = 4 * 64 * 68 * 4;              // epilogue tile [wave][px][68 floats], after the P buffers
+    constexpr int SMEM = 2 * PB + (2 * WB > EPB ? 2 * WB : EPB);
+    static_assert(SMEM <= 160 * 1024, "k_pc_conv LDS");
     __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
 
     const int prob = blockIdx.z / A.outer_max, o = blockIdx.z - prob * A.outer_max;
     const ConvProb& P = A.p[prob];
     const int tr = blockIdx.x / A.ntc, tc = blockIdx.x - tr * A.ntc;
-    const int r0 = tr * TY, c0 = tc * TX, nb = blockIdx.y;
-    if (o >= P.outer || r0 >= P.rows || c0 >= P.cols || nb * 64 >= P.cop) return;   // whole workgroup
+    const int r0 = tr * TY, c0 = tc * TX, nb0 = blockIdx.y * A.nbw;
+    if (o >= P.outer || r0 >= P.rows || c0 >= P.cols || nb0 * 64 >= P.cop) return;   // whole workgroup
 
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6, l15 = lane & 15, kq = lane >> 4;
     const int ncc = P.in.cin >> 5, nq = P.in.nsub * ncc, nsteps = nq * KH;
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
         poff[u] = ok ? (int)(ir * P.in.s_row + ic * P.in.s_col) + k4 * 8 : 0;
         pok |= ok ? 1u << u : 0u;
     }
-    const uint16_t* wbase = P.w + (size_t)nb * nq * KH * KW * 2048;
+    const uint16_t* wbase = P.w;   // the current 64-channel output tile's weights
     const uint16_t* pbase = inb;   // the current chunk's source (sub-pixel offset + 32-channel block)
 #define PC_LOADP(q_)                                                                                        \
     {                                                                                                       \
@@ -143,17 +146,24 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
         if (e_ < 4 * HR * HC)                                                                               \
             *reinterpret_cast<u4v*>(smem + (buf_) * PB + ((e_ & 3) * NP + (e_ >> 2)) * 16) = preg[u];      \
     }
-#define PC_LOADW(s_)                                                                                        \
+    // a step's weights straight into LDS buffer buf_ (LDS-DMA, no VGPRs: each wave-instruction writes
+    // 1 KB, its 64 lanes' 16 bytes in lane order, and the image is the source's byte order)
+#define PC_DMAW(s_, buf_)                                                                                   \
     {                                                                                                       \
         const u4v* src_ = reinterpret_cast<const u4v*>(wbase + (size_t)(s_) * KW * 2048) + t;               \
-        _Pragma("unroll") for (int u = 0; u < KW; ++u) wreg[u] = src_[u * 256];                             \
-    }
-#define PC_STOREW(buf_)                                                                                     \
-    {                                                                                                       \
-        u4v* dst_ = reinterpret_cast<u4v*>(smem + 2 * PB + (buf_) * WB) + t;                                \
-        _Pragma("unroll") for (int u = 0; u < KW; ++u) dst_[u * 256] = wreg[u];                             \
+        _Pragma("unroll") for (int u = 0; u < KW; ++u) __builtin_amdgcn_global_load_lds(                    \
+            src_ + u * 256, (__attribute__((address_space(3))) void*)(smem + 2 * PB + (buf_) * WB + u * 4096 + wv * 1024), \
+            16, 0, 0);                                                                                      \
     }
 
+    // output tiles nb0 .. nb0 + nbw - 1 in turn; with nbw > 1 every input chunk (nq <= 2) is staged once,
+    // by the first tile, into P buffer q, and the later tiles stage only their weights
+#pragma unroll 1
+    for (int nbi = 0; nbi < A.nbw; ++nbi) {
+    const int nb = nb0 + nbi;
+    if (nb * 64 >= P.cop) break;   // whole workgroup
+    const bool first = nbi == 0;
+    wbase = P.w + (size_t)nb * nq * KH * KW * 2048;
     f4 acc[4][4];
 #pragma unroll
     for (int f = 0; f < 4; ++f)
@@ -161,21 +171,23 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
         for (int g = 0; g < 4; ++g) acc[f][g] = f4{0.f, 0.f, 0.f, 0.f};
 
     {
-        u4v preg[NPE], wreg[KW];
-        PC_LOADP(0);
-        PC_LOADW(0);
-        PC_STOREP(0);
-        PC_STOREW(0);
+        u4v preg[NPE];
+        PC_DMAW(0, 0);
+        if (first) {
+            PC_LOADP(0);
+            PC_STOREP(0);
+        }
     }
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
         const int q = s / KH, a = s - q * KH;
-        const bool nxq = s + 1 < nsteps && a == KH - 1;   // the chunk's last step: stage the next chunk
+        // the chunk's last step: stage the next chunk (resident chunks only once)
+        const bool nxq = first && s + 1 < nsteps && a == KH - 1;
         // staging registers local to the step (loaded at its top, stored at its end): arrays carried
         // across iterations were demoted to scratch
-        u4v wreg[KW], preg[NPE];
-        // the next step's weights (the last step re-loads its own: no branch around the loads)
-        PC_LOADW(s + 1 < nsteps ? s + 1 : s);
+        u4v preg[NPE];
+        // the next step's weights into the other buffer (read by step s - 1, which every wave has left)
+        if (s + 1 < nsteps) PC_DMAW(s + 1, (s + 1) & 1);
         if (nxq) PC_LOADP(q + 1);
         // the loads above go out before the MFMAs (the scheduler otherwise sinks them to their
         // LDS stores at the end of the step and the step waits out their whole latency)
@@ -205,18 +217,13 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
                 for (int g = 0; g < 4; ++g)
                     acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Af[u][f], Bf[u][g], acc[f][g], 0, 0, 0);
         }
-        PC_STOREW((s + 1) & 1);
         if (nxq) PC_STOREP((q + 1) & 1);
-        __syncthreads();
+        __syncthreads();   // with the DMA in flight: vmcnt(0) first
     }
-#undef PC_LOADP
-#undef PC_STOREP
-#undef PC_LOADW
-#undef PC_STOREW
-
-    // epilogue: accumulators -> LDS [wave][row][px][n] (row stride 68 floats) -> 8-channel runs
+    // epilogue: accumulators -> LDS [wave][px][n] (row stride 68 floats, after the P buffers, over the
+    // weight buffers) -> 8-channel runs
     {
-        float* ep = reinterpret_cast<float*>(smem) + wv * 64 * 68;
+        float* ep = reinterpret_cast<float*>(smem + 2 * PB) + wv * 64 * 68;
 #pragma unroll
         for (int f = 0; f < 4; ++f)
 #pragma unroll
@@ -226,10 +233,9 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
     }
     __syncthreads();
     const int Y = r0 + wv;
-    if (Y >= P.rows) return;
-    const float* ep = reinterpret_cast<const float*>(smem) + wv * 64 * 68;
+    const float* ep = reinterpret_cast<const float*>(smem + 2 * PB) + wv * 64 * 68;
 #pragma unroll 1
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < (Y < P.rows ? 8 : 0); ++i) {
         const int item = lane + 64 * i, px = item >> 3, n0 = (item & 7) * 8, X = c0 + px;
         if (X >= P.cols) continue;
         const float4 va = *reinterpret_cast<const float4*>(ep + px * 68 + n0);
@@ -291,6 +297,11 @@ __global__ __launch_bounds__(256, 1) void k_pc_conv(const ConvArgs A) {
                                                        f2bf(v[4]) | f2bf(v[5]) << 16, f2bf(v[6]) | f2bf(v[7]) << 16);
         }
     }
+    __syncthreads();   // the epilogue tile overlays the weight buffers the next output tile stages into
+    }
+#undef PC_LOADP
+#undef PC_STOREP
+#undef PC_DMAW
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1151,7 +1162,12 @@ template <int KH, int KW>
 void launch_conv(const ConvArgs& A, int rows_max, int cols_max, int cop_max, hipStream_t st) {
     ConvArgs a = A;
     a.ntc = (cols_max + 63) / 64;
-    const dim3 grid((unsigned)(((rows_max + 3) / 4) * a.ntc), (unsigned)(cop_max / 64),
+    // every problem's input chunks (nsub x cin / 32) fit the two P buffers: one workgroup runs all the
+    // 64-channel output tiles of its pixel tile, staging the input once (the dx backward: 4 tiles)
+    bool resident = true;
+    for (int i = 0; i < a.nprob; ++i) resident = resident && a.p[i].in.nsub * (a.p[i].in.cin >> 5) <= 2;
+    a.nbw = resident ? cop_max / 64 : 1;
+    const dim3 grid((unsigned)(((rows_max + 3) / 4) * a.ntc), (unsigned)(cop_max / 64 / a.nbw),
                     (unsigned)(a.nprob * a.outer_max));
     hipLaunchKernelGGL((k_pc_conv<KH, KW>), grid, dim3(256), 0, st, a);
 }
