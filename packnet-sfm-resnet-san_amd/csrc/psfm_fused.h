@@ -103,7 +103,9 @@ __device__ __forceinline__ void k12_stamp(int slot) {
     if (sb.p == nullptr) return;  // wave-uniform
     const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    if (L < sb.cap && threadIdx.x == 0) sb.p[2 * L + slot] = t;
+    int tid = threadIdx.x;   // laundered: a lane-0 mask shared with the prologue was kept across the sweep
+    asm volatile("" : "+v"(tid));
+    if (L < sb.cap && tid == 0) sb.p[2 * L + slot] = t;
 }
 
 struct Args {
@@ -812,6 +814,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
     for (int c = 0; c < 3; ++c) S.D0[0][c] = S.D1[0][c] = S.D2[0][c] = f2{0.0f, 0.0f};
 #pragma unroll
     for (int m = 0; m < 24; ++m) K.gt[m] = 0.0f;
+    // the work item (scale, image, unit), which only the partial-sum stores after the sweep need, parked
+    // in lane 0's dL/dT row padding (dwords 24-26 of the GTS = 28) instead of SGPRs across the sweep
+    if (threadIdx.x == 0) {
+        int* pad = reinterpret_cast<int*>(K.gt) + 24;
+        pad[0] = K.s;
+        pad[1] = K.b;
+        pad[2] = K.unit;
+    }
     // rows y0-2 .. y0+RB+1 issued at k = 0 .. RB+3; p-rows y0-1 .. y0+RB at k = 3 .. RB+4;
     // q-rows y0 .. y0+RB-1 at k = 5 .. RB+4.  Step k uses row slot k & 3; the loop leaves after
     // step RB+4 (wave-uniform branches, any RB).  That step's issue is a harmless extra row (reflect-
@@ -839,15 +849,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
         K.template step<0, true, true, true>(S, k + 3);
         if (k + 3 == KE) break;
     }
-    // per-wave partial sums (fixed-order wave butterflies)
+    // per-wave partial sums (fixed-order wave butterflies).  The output pointers are read here, after the
+    // sweep, through a laundered kernarg pointer: read as plain arguments they were loaded in the
+    // prologue and held across the sweep in SGPRs spilled to VGPR lanes
     const psfm_params& p = a.p;
     const int nu = units(p.H, p.W, RB);
+    uint64_t kp = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());   // `a`: offset 0
+    asm volatile("" : "+s"(kp));
+    const __attribute__((address_space(4))) Args* ka = reinterpret_cast<const __attribute__((address_space(4))) Args*>(kp);
+    const int* pad = reinterpret_cast<const int*>(k12_lds + 3 * 6 * 64 * 2) + 24;   // lane 0's row
+    const int ws_ = __builtin_amdgcn_readfirstlane(pad[0]), wb = __builtin_amdgcn_readfirstlane(pad[1]),
+              wu = __builtin_amdgcn_readfirstlane(pad[2]);
+    int tid = threadIdx.x;   // re-derived: the prologue's lane-0 mask was kept across the sweep too
+    asm volatile("" : "+v"(tid));
     const float ph = wave_sum64(S.acc_photo);
     const float ax = wave_sum64(S.acc_ax), ay = wave_sum64(S.acc_ay), m = wave_sum64(S.acc_m);
-    if (threadIdx.x == 0) {
-        a.ws.photo_part[(size_t)K.s * (p.B * nu) + K.b * nu + K.unit] = ph;
+    if (tid == 0) {
+        ka->ws.photo_part[(size_t)ws_ * (p.B * nu) + wb * nu + wu] = ph;
         if (K.cfg.smooth()) {
-            float* o = a.ws.smooth_part + (((size_t)K.s * p.B + K.b) * nu + K.unit) * 4;
+            float* o = ka->ws.smooth_part + (((size_t)ws_ * p.B + wb) * nu + wu) * 4;
             o[0] = ax;
             o[1] = ay;
             o[2] = m;
@@ -856,7 +876,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-        float* o = a.ws.pose_part + ((((size_t)K.s * NC + j) * p.B + K.b) * nu + K.unit) * 12;
+        float* o = ka->ws.pose_part + ((((size_t)ws_ * NC + j) * p.B + wb) * nu + wu) * 12;
         float t[12];
 #pragma unroll
         for (int mm = 0; mm < 12; ++mm) t[mm] = wave_sum64(K.gt[2 * mm + j]);
@@ -875,7 +895,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) voi
 #pragma unroll
             for (int mm = 0; mm < 12; ++mm) t[mm] = u[mm];
         }
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
 #pragma unroll
             for (int mm = 0; mm < 12; ++mm) o[mm] = t[mm];
         }
