@@ -642,6 +642,9 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs f) {
         for (int s = 0; s < c.S; ++s, ++item) {
             if (item % nw != wave) continue;
             double acc = 0.0;
+            // unrolled: the loads of 8 trips go out together (one latency instead of 8; the adds keep
+            // their order)
+#pragma unroll 8
             for (int k = lane; k < nparts; k += 64) acc += (double)c.photo_part[(size_t)s * nparts + k];
             acc = wave_sum_d(acc);
             if (lane == 0) photo_item[ci * MAXS + s] = acc * c.photo_scale;
@@ -656,6 +659,7 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs f) {
                     if (item % nw != wave) continue;
                     const float* sp = c.smooth_part + ((size_t)s * c.B + b) * c.tiles * 4;
                     double ax = 0.0, ay = 0.0, m = 0.0;
+#pragma unroll 4
                     for (int k = lane; k < c.tiles; k += 64) {
                         ax += (double)sp[k * 4];
                         ay += (double)sp[k * 4 + 1];
@@ -665,9 +669,17 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs f) {
                     ay = wave_sum_d(ay);
                     m = wave_sum_d(m);
                     if (lane == 0 && item < MAXS * MAXS * 64) {
-                        smooth_item[item][0] = ax;
-                        smooth_item[item][1] = ay;
-                        smooth_item[item][2] = m;
+                        // the item's smoothness statistics and its term of the loss, here, in parallel
+                        // over the waves (thread 0's serial tail of fp64 divisions took most of the launch)
+                        const float mf = (float)(m / ((double)c.H * c.W));
+                        const float mc = fmaxf(mf, 1e-6f);
+                        smooth_item[item][0] = ax / ((double)c.B * c.H * (c.W - 1)) / mc +
+                                               ay / ((double)c.B * (c.H - 1) * c.W) / mc;
+                        float* st = f.smooth_stats + ((size_t)(c.scale0 + s) * c.B + b) * 4;
+                        st[0] = (float)ax;
+                        st[1] = (float)ay;
+                        st[2] = mf;
+                        st[3] = mc;
                     }
                 }
         }
@@ -685,17 +697,7 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs f) {
             for (int s = 0; s < c.S; ++s) {
                 const int gsi = c.scale0 + s;
                 double term = 0.0;
-                for (int b = 0; b < c.B; ++b, ++item) {
-                    const double ax = smooth_item[item][0], ay = smooth_item[item][1];
-                    const float m = (float)(smooth_item[item][2] / ((double)c.H * c.W));
-                    const float mc = fmaxf(m, 1e-6f);
-                    term += ax / ((double)c.B * c.H * (c.W - 1)) / mc + ay / ((double)c.B * (c.H - 1) * c.W) / mc;
-                    float* st = f.smooth_stats + ((size_t)gsi * c.B + b) * 4;
-                    st[0] = (float)ax;
-                    st[1] = (float)ay;
-                    st[2] = m;
-                    st[3] = mc;
-                }
+                for (int b = 0; b < c.B; ++b, ++item) term += smooth_item[item][0];
                 smooth += term / (double)(1 << gsi);
             }
         }
@@ -760,6 +762,7 @@ __global__ __launch_bounds__(256) void k_pose_reduce(PoseRedArgs r) {
             for (int s = 0; s < c.S; ++s) {
                 const float* pp = c.part + (((size_t)(s * c.N + j) * c.B + b) * c.tiles) * 12;
                 double part = 0.0;
+#pragma unroll 4
                 for (int t = lane; t < c.tiles; t += 64) part += (double)pp[(size_t)t * 12 + k];
                 acc += wave_sum_d(part);
             }
