@@ -822,21 +822,25 @@ __global__ __launch_bounds__(NT) void k_sig_sum(SigSumArgs a) {
     const float* x = pick4(a.sig, s) + (size_t)b * (a.plane >> (2 * sh));
     const uint32_t W = (uint32_t)a.W, Ws = W >> sh;
     float v[1] = {0.0f};
-    // 8 loads in flight per thread, then the adds in the plain loop's order (i = lo + tid, + NT, ...)
-    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * NT) {
-        float t[8];
+    // 16 loads in flight per thread, then the adds in the plain loop's order (i = lo + tid, + NT, ...).
+    // The loads are unconditional (index clamped, the value masked after): a load under `i < hi`
+    // made the compiler branch around each one and wait for it (vmcnt(0)) before the next
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += 16 * NT) {
+        float t[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t i = i0 + u * NT;
+        for (int u = 0; u < 16; ++u) {
+            const uint32_t i = i0 + u * NT, ic = min(i, hi - 1);
+            float val;
             if (sh == 0) {
-                t[u] = i < hi ? x[i] : 0.0f;
+                val = x[ic];
             } else {
-                const uint32_t y = i / W, c = i - y * W;
-                t[u] = i < hi ? x[(y >> sh) * Ws + (c >> sh)] : 0.0f;
+                const uint32_t y = ic / W, c = ic - y * W;
+                val = x[(y >> sh) * Ws + (c >> sh)];
             }
+            t[u] = i < hi ? val : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[0] += t[u];
+        for (int u = 0; u < 16; ++u) v[0] += t[u];
     }
     block_sum<1>(v, red);
     if (threadIdx.x == 0) a.part[((size_t)s * a.B + b) * fused::SIGCH + ch] = v[0];
@@ -902,10 +906,13 @@ __global__ __launch_bounds__(NT) void k_grad_finish(GradFinishArgs a) {
     float* g = pick4(a.g, s) + (size_t)b * cplane;
     const uint32_t i0 = blockIdx.x * (NT * 4) + threadIdx.x;
     if (sh == 0) {
+        float v[4];   // the four loads first, unconditional (clamped index), then the guarded stores
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = gi[min(i0 + u * NT, plane - 1)];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = i0 + u * NT;
-            if (i < plane) g[i] = go * (gi[i] + c);
+            if (i < plane) g[i] = go * (v[u] + c);
         }
         return;
     }
