@@ -402,7 +402,11 @@ def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monk
     up — and is bypassed here for them, as the module test does).  A fixed linear loss on the four
     inverse-depth maps; compared: the maps, dL/drgb and the pack1 / pack2 parameter gradients.  The
     composed network must be as close to fp32 as the round-4 bf16 network (composition off) is: its
-    relative L2 error at most 1.25x the round-4 path's + 2e-3, and the maps within 2e-2."""
+    relative L2 error at most 1.25x the round-4 path's + 2e-3, and the maps within 2e-2.  The two
+    Conv3d bias gradients (8 entries, sums that cancel) move from run to run with MIOpen's
+    atomic-accumulating bf16 backward: the round-4 path's own error on pack2.b3 measured 3.0e-2 -
+    5.4e-2 over four runs on the same weights (the composed path 3.5e-2 - 4.0e-2), so for them the
+    bound is that ratio or 6e-2, whichever is larger."""
     import __graft_entry__
     __graft_entry__.build()
     from packnet_sfm_amd.networks.layers.packnet import packconv
@@ -449,7 +453,7 @@ def test_packnet01_network_with_composed_pack_layers_matches_the_fp32_chain(monk
     rows = [(n, rel(c, r), rel(o, r)) for n, c, o, r in zip(names, comp, old, ref)]
     print("rel L2 vs fp32 (composed, round-4 bf16):", ["%s %.2e %.2e" % t for t in rows])
     for n, ec, eo in rows:
-        assert ec <= 1.25 * eo + 2e-3, (n, ec, eo)
+        assert ec <= max(1.25 * eo + 2e-3, 6e-2 if n.endswith("b3") else 0.0), (n, ec, eo)
         if n.startswith("inv"):
             assert ec < 2e-2, (n, ec)
 
