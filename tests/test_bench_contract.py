@@ -18,7 +18,11 @@ def test_stale_or_foreign_pmc_profile_is_not_attached(tmp_path, monkeypatch):
     got, _, why = bench.stamped_profile(args)
     assert got is not None and why is None
     ktimes = {"K12_photometric_fwd_grad": 100.0, "prepass": 12.0}
-    assert bench.roofline(args, ktimes)["traffic"] == int(7.1e7)
+    r = bench.roofline(args, ktimes)
+    assert r["traffic"] == int(7.1e7)
+    # the kernel's distance from its own VALU issue floor, beside the HBM fraction
+    v = r["valu"]
+    assert abs(v["valu_floor_us_over_dominant_us"] - v["simd_floor_us_2cyc"] / r["dominant_us_per_launch"]) < 2e-3
     prof["source_hash"] = "older00000000000"
     (d / f"{key}.json").write_text(json.dumps(prof))
     got, _, why = bench.stamped_profile(args)
@@ -43,7 +47,7 @@ def test_committed_bench_lines_keep_the_contract():
     import json
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    files = sorted(f for f in glob.glob(os.path.join(root, "profiles", "r04", "final", "bench_*.json"))
+    files = sorted(f for r in ("r04", "r06") for f in glob.glob(os.path.join(root, "profiles", r, "final", "bench_*.json"))
                    if "rehearsal" not in f)   # the N = 2 gloo rehearsal runs without the kernel timing
     assert files
     for f in files:
@@ -57,7 +61,9 @@ def test_committed_bench_lines_keep_the_contract():
             assert k in r, (f, k)
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
         assert "workload" in d["config"]
-        if f.endswith("bench_kitti-resnet-san.json"):
+        if f.endswith("bench_kitti-resnet-san.json") and "r04" in f or "bench_default" in f:
             cb = d["cpu_baseline"]
             for k in ("value", "unit", "cores", "kind", "sample"):
                 assert k in cb, k
+        if "r06" in f and "bench_default" in f:   # the stamped profile of its own sources was attached
+            assert r["traffic"] and r["valu"]["valu_floor_us_over_dominant_us"] > 0
